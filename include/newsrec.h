@@ -1,0 +1,179 @@
+/*
+ * newsrec.h — C-ABI of libnewsrec_hip.so, the MI355X (gfx950) kernels behind
+ * the MIND embed -> pool -> score hot path.
+ *
+ * The reference (AhmedFahim-git/news_recommendation_project_v2) has no native
+ * code and no FFI: its boundary is the Python API of src/news_rec_utils
+ * (SURVEY.md §8(b)).  These entry points replace the torch ops that API calls,
+ * and are bound from Python with ctypes by
+ * news_recommendation_project_v2_amd/_lib.py (see INTEGRATION.md for the
+ * binding a maintainer would add to the reference).
+ *
+ * Conventions
+ *  - Every device buffer is allocated and freed by the caller (PyTorch); the
+ *    library never frees caller memory.  Scratch is an explicit workspace.
+ *  - All calls enqueue asynchronously on `stream` (a hipStream_t passed as
+ *    void*; NULL = the legacy default stream) and never synchronise, so they
+ *    are graph-capturable.
+ *  - Return NR_OK (0) or a negative code; nr_last_error() returns the
+ *    thread-local message of the last failure.  No exception crosses the ABI.
+ *  - Matrices are row-major with explicit leading dimensions in ELEMENTS.
+ *    Linear weights use torch's nn.Linear layout W[out_features][in_features],
+ *    so GEMMs compute C = A · Wᵀ.
+ */
+#ifndef NEWSREC_H
+#define NEWSREC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NR_OK 0
+#define NR_ERR_INVALID -1     /* bad argument / shape */
+#define NR_ERR_HIP -2         /* HIP runtime or launch failure */
+#define NR_ERR_UNSUPPORTED -3 /* valid but not implemented (e.g. dim) */
+
+/* element types */
+#define NR_F32 0
+#define NR_BF16 1
+
+/* history poolers */
+#define NR_POOL_FINAL 0  /* FinalAttention additive per-dim softmax pooler */
+#define NR_POOL_LATENT 1 /* LatentAttentionModel masked mean + L2 normalize */
+
+/* GEMM epilogues (applied to acc = A·Wᵀ) */
+#define NR_EPI_NONE 0   /* C = acc + bias                                   */
+#define NR_EPI_RELU 1   /* C = relu(acc + bias)                             */
+#define NR_EPI_EXP 2    /* C = exp(acc + bias)                              */
+#define NR_EPI_GEGLU 3  /* W rows interleaved in 32-row (a, g) blocks:
+                           C[:, j] = (a_j + ba_j) * gelu_erf(g_j + bg_j);
+                           C has N/2 columns                               */
+#define NR_EPI_RESADD 4 /* C = acc + bias + R                               */
+
+/* Library version (major*100 + minor). */
+int nr_version(void);
+
+/* Select the HIP device for subsequent calls on this host thread and load the
+ * code object once per device.  Replaces the implicit `.to(DEVICE)` of
+ * config.py:19 for the library's own state. */
+int nr_init(int device);
+
+/* Thread-local message of the last failed call ("" if none). */
+const char* nr_last_error(void);
+
+/*
+ * C[M, N] = epilogue(A[M, K] · W[N, K]ᵀ).
+ * Replaces nn.Linear (+ F.relu / torch.exp / GEGLU / residual add) in
+ *   FinalAttention.forward        modeling_utils.py:218-222
+ *   LatentAttentionModel blocks   latent_attention.py:34-36, 59-61, 162-163
+ * dtype_in NR_F32: exact-f32 MFMA (v_mfma_f32_32x32x2_f32);
+ * dtype_in NR_BF16: bf16 MFMA (v_mfma_f32_32x32x16_bf16), f32 accumulate.
+ * A and W share dtype_in; C is dtype_out; bias and R are f32 (bias nullable,
+ * R only for NR_EPI_RESADD, R has dtype_out).  Requires N % 128 == 0,
+ * K % 32 == 0 (f32) or K % 64 == 0 (bf16); M arbitrary.
+ */
+int nr_gemm(int dtype_in, int dtype_out, int epilogue, int64_t M, int64_t N, int64_t K,
+            const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+            const void* R, int64_t ldr, void* C, int64_t ldc, void* stream);
+
+/*
+ * y = LayerNorm(x) * gamma + beta over rows of `dim` (biased variance).
+ * Replaces nn.LayerNorm in PreNorm latent_attention.py:10-12,16-19 and
+ * MyLayer attention.py:165-166,193.  dim % 256 == 0, dim <= 2048.
+ */
+int nr_layernorm(int dtype_in, int dtype_out, int64_t rows, int64_t dim, const void* x,
+                 int64_t ldx, const float* gamma, const float* beta, float eps, void* y,
+                 int64_t ldy, void* stream);
+
+/*
+ * In-place softmax over contiguous groups: x is f32 [rows][groups*64]
+ * (row stride ldx), each run of 64 is one softmax.  Replaces the softmax
+ * inside F.scaled_dot_product_attention at latent_attention.py:72
+ * (64 latents per head).  dtype_out selects the element type of y.
+ */
+int nr_softmax64(int64_t rows, int64_t groups, const float* x, int64_t ldx, int dtype_out,
+                 void* y, int64_t ldy, void* stream);
+
+/*
+ * out[r] = 1 / max(||x_r||_2, eps).  The per-row clamp of F.cosine_similarity
+ * (data_model_helper.py:224-227, torch 2.10 semantics).
+ */
+int nr_row_inv_norm(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps,
+                    float* out, void* stream);
+
+/*
+ * Fused segmented history pooling + candidate cosine scoring.
+ * Replaces get_final_attention_eval (data_model_helper.py:112-131: padded
+ * batches through FinalAttention.forward modeling_utils.py:224-228 or
+ * LatentAttentionModel.forward latent_attention.py:165-170) and the
+ * per-impression F.cosine_similarity loop of get_cos_sim_scores
+ * (data_model_helper.py:199-230).
+ *
+ * hist_table  per-news pooler table in `dtype`, row stride hist_ld:
+ *             NR_POOL_FINAL : row = [x(dim) | exp(w)(dim)]
+ *             NR_POOL_LATENT: row = h(dim)
+ * cand_table  raw news embeddings [*, dim] in `dtype` (row stride cand_ld)
+ * cand_inv_norm  f32 1/max(||cand_table row||, 1e-8)
+ * hist_idx/hist_off, cand_idx/cand_off   CSR (int32 rows, int64 offsets,
+ *             n_imp + 1 entries each)
+ * scores      f32 [cand_off[n_imp]] in impression order
+ * users       nullable f32 [n_imp][dim]: the pooled user vectors
+ *             (FinalAttention output / normalized latent mean)
+ * Supported dim: 1024.
+ */
+int nr_pool_score(int pooler, int dtype, int64_t dim, const void* hist_table, int64_t hist_ld,
+                  const void* cand_table, int64_t cand_ld, const float* cand_inv_norm,
+                  const int32_t* hist_idx, const int64_t* hist_off, const int32_t* cand_idx,
+                  const int64_t* cand_off, int64_t n_imp, float* scores, float* users,
+                  void* stream);
+
+/*
+ * Dense descending rank per impression: ranks[c] = 1 + number of distinct
+ * scores of the same impression that are strictly greater.  Bit-exact
+ * restatement of scipy.stats.rankdata(-x, method="dense") used by
+ * rank_group_preds (data_utils.py:414-415).  Impressions must have at most
+ * 2048 candidates (NR_ERR_UNSUPPORTED otherwise, checked on the device and
+ * reported through `status`, a caller-zeroed int32 on the device).
+ */
+int nr_dense_rank(const float* scores, const int64_t* cand_off, int64_t n_imp, int32_t* ranks,
+                  int32_t* status, void* stream);
+
+/*
+ * FinalAttention per-news transform for n news rows of `emb`:
+ *   x = W3·relu(W2·relu(W1·e + b1) + b2) + b3 ;  p = exp(W5·relu(W4·x + b4))
+ * written as table[n][2][1024] = (x, p) in `dtype` (modeling_utils.py:218-224,
+ * computed once per unique news instead of per padded history slot).
+ * Weights in `dtype` (torch layout), biases f32.  ws must hold
+ * nr_final_attn_workspace_bytes(dtype, n) bytes.
+ */
+int64_t nr_final_attn_workspace_bytes(int dtype, int64_t n);
+int nr_final_attn_transform(int dtype, int64_t n, const void* emb, int64_t emb_ld,
+                            const void* W1, const float* b1, const void* W2, const float* b2,
+                            const void* W3, const float* b3, const void* W4, const float* b4,
+                            const void* W5, void* table, void* ws, int64_t ws_bytes,
+                            void* stream);
+
+/*
+ * LatentAttentionModel per-news transform (latent_attention.py:157-163, K/V of
+ * the 64 latents folded into the query and output projections once per model):
+ *   y  = LN_q(e);  P = softmax_64(y · Aᵀ) per head;  h1 = e + P · Btᵀ
+ *   h  = h1 + W2 · GEGLU(W1i · LN_f(h1) + b1i) + b2
+ * A  [512][1024] rows h*64+j = (K_h[j] · W_q,h) / sqrt(512)   (K,V = to_kv(LN_c(latents)))
+ * Bt [1024][512] column h*64+j = W_o,h · V_h[j]
+ * W1i/b1i are W_1/b_1 with rows interleaved in 32-row (a, g) blocks.
+ * Output table [n][1024] in `dtype`.  ws: nr_latent_workspace_bytes(dtype, n).
+ */
+int64_t nr_latent_workspace_bytes(int dtype, int64_t n);
+int nr_latent_transform(int dtype, int64_t n, const void* emb, int64_t emb_ld,
+                        const float* lnq_g, const float* lnq_b, const void* A, const void* Bt,
+                        const float* lnf_g, const float* lnf_b, const void* W1i,
+                        const float* b1i, const void* W2, const float* b2, void* table,
+                        void* ws, int64_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NEWSREC_H */

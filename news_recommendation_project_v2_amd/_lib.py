@@ -1,0 +1,82 @@
+"""ctypes binding of ``libnewsrec_hip.so`` (C-ABI declared in include/newsrec.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or
+``make -C news_recommendation_project_v2_amd/csrc``).  There is no CPU or
+PyTorch fallback: if the library is missing or a call fails, a
+``NewsRecHIPError`` is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().with_name("libnewsrec_hip.so")
+
+NR_OK = 0
+NR_F32 = 0
+NR_BF16 = 1
+NR_POOL_FINAL = 0
+NR_POOL_LATENT = 1
+NR_EPI_NONE = 0
+NR_EPI_RELU = 1
+NR_EPI_EXP = 2
+NR_EPI_GEGLU = 3
+NR_EPI_RESADD = 4
+
+_p = ctypes.c_void_p
+_i = ctypes.c_int
+_l = ctypes.c_int64
+_f = ctypes.c_float
+
+# name -> (restype, argtypes); must match include/newsrec.h
+SIGNATURES = {
+    "nr_version": (_i, []),
+    "nr_init": (_i, [_i]),
+    "nr_last_error": (ctypes.c_char_p, []),
+    "nr_gemm": (_i, [_i, _i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p]),
+    "nr_layernorm": (_i, [_i, _i, _l, _l, _p, _l, _p, _p, _f, _p, _l, _p]),
+    "nr_softmax64": (_i, [_l, _l, _p, _l, _i, _p, _l, _p]),
+    "nr_row_inv_norm": (_i, [_i, _l, _l, _p, _l, _f, _p, _p]),
+    "nr_pool_score": (_i, [_i, _i, _l, _p, _l, _p, _l, _p, _p, _p, _p, _p, _l, _p, _p, _p]),
+    "nr_dense_rank": (_i, [_p, _p, _l, _p, _p, _p]),
+    "nr_final_attn_workspace_bytes": (_l, [_i, _l]),
+    "nr_final_attn_transform": (_i, [_i, _l, _p, _l, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _l, _p]),
+    "nr_latent_workspace_bytes": (_l, [_i, _l]),
+    "nr_latent_transform": (_i, [_i, _l, _p, _l, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _l, _p]),
+}
+
+
+class NewsRecHIPError(RuntimeError):
+    """A libnewsrec_hip call failed (or the library is not available)."""
+
+
+_LIB = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the HIP library once; raise loudly if it was not built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not LIB_PATH.is_file():
+        raise NewsRecHIPError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback for the MI355X hot path)")
+    lib = ctypes.CDLL(os.fspath(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(rc: int, name: str) -> None:
+    if rc != NR_OK:
+        msg = load().nr_last_error().decode(errors="replace")
+        raise NewsRecHIPError(f"{name} failed ({rc}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)

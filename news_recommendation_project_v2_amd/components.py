@@ -1,0 +1,144 @@
+"""Pipeline components of the hot path (reference components.py).
+
+Kept: TransformData (45-114), EmbeddingsComponent (117-175),
+SaveEmbeddingComponent (178-223), LoadEmbeddingComponent (226-258),
+FinalAttentionComponent (980-1027, transform only), plus
+LatentAttentionComponent — the same scoring with the latent pooler, which the
+reference can only reach through get_latent_attention_model
+(modeling_utils.py:151-155).  Training components and the Azure upload are out
+of scope.
+"""
+from __future__ import annotations
+
+from pathlib import Path
+from typing import Any, Optional
+
+import numpy as np
+import torch
+
+from .data_model_helper import get_embeddings, get_final_second_attention_score
+from .data_utils import split_impressions_and_history
+from .modeling_utils import get_final_attention_model, get_latent_attention_model
+from .pipeline import PipelineComponent, check_req_keys
+
+
+class TransformData(PipelineComponent):
+    """Behaviours -> index arrays + per-news feature tensors (components.py:45-114).
+
+    The reference requires the entity/category keys too; they are optional here
+    because nothing on the embed -> pool -> score path reads them (their
+    tensors are produced when present).
+    """
+
+    required_keys = {"behaviors"}
+
+    def transform(self, context_dict: dict[str, Any]) -> dict[str, Any]:
+        check_req_keys(self.required_keys, context_dict)
+        behaviors = context_dict["behaviors"]
+        new = context_dict.copy()
+        new["ImpressionID"] = behaviors["ImpressionID"]
+        new.update(split_impressions_and_history(behaviors["Impressions"], behaviors["History"]))
+        new["history_bool"] = behaviors["History"].notna()
+        news_list = new["news_list"]
+        for src, dst in (("news_title_entity", "title_entity_embed"),
+                         ("news_abstract_entity", "abstract_entity_embed")):
+            if src in context_dict:
+                new[dst] = torch.stack([torch.tensor(context_dict[src][i], dtype=torch.float32) for i in news_list])
+                new.pop(src)
+        for src, dst in (("news_category", "cat_indices"), ("news_subcategory", "subcat_indices")):
+            if src in context_dict:
+                new[dst] = torch.tensor([context_dict[src][i] for i in news_list], dtype=torch.int32).unsqueeze(-1)
+                new.pop(src)
+        new.pop("behaviors")
+        return new
+
+
+class EmbeddingsComponent(PipelineComponent):
+    """Title encoder over news_list (components.py:117-175)."""
+
+    required_keys = {"news_list", "news_text_dict"}
+
+    def __init__(self, model_path: str):
+        self.model_path = model_path
+
+    def transform(self, context_dict):
+        check_req_keys(self.required_keys, context_dict)
+        new = context_dict.copy()
+        emb = get_embeddings(self.model_path, new["news_list"], new["news_text_dict"])
+        if isinstance(emb, tuple):
+            new["query_news_embeddings"], new["news_embeddings"] = emb
+        else:
+            new["news_embeddings"] = emb
+        return new
+
+
+class SaveEmbeddingComponent(PipelineComponent):
+    """torch.save tables as {save_dir}/{split}.pt (+ query_ prefix) (components.py:193-223)."""
+
+    required_keys = {"news_embeddings", "news_dataset"}
+
+    def __init__(self, save_dir: Path):
+        self.save_dir = Path(save_dir)
+
+    def transform(self, context_dict):
+        check_req_keys(self.required_keys, context_dict)
+        self.save_dir.mkdir(parents=True, exist_ok=True)
+        name = context_dict["news_dataset"].value
+        torch.save(context_dict["news_embeddings"], self.save_dir / f"{name}.pt")
+        if "query_news_embeddings" in context_dict:
+            torch.save(context_dict["query_news_embeddings"], self.save_dir / f"query_{name}.pt")
+        return context_dict
+
+
+class LoadEmbeddingComponent(PipelineComponent):
+    """torch.load(weights_only=True) of the tables (components.py:234-258)."""
+
+    required_keys = {"news_dataset"}
+
+    def __init__(self, save_dir: Path):
+        self.save_dir = Path(save_dir)
+
+    def transform(self, context_dict):
+        check_req_keys(self.required_keys, context_dict)
+        name = context_dict["news_dataset"].value
+        context_dict["news_embeddings"] = torch.load(self.save_dir / f"{name}.pt", weights_only=True)
+        q = self.save_dir / f"query_{name}.pt"
+        if q.exists():
+            context_dict["query_news_embeddings"] = torch.load(q, weights_only=True)
+        return context_dict
+
+
+class FinalAttentionComponent(PipelineComponent):
+    """Pooled cosine scores + dense ranks with FinalAttention (components.py:980-1027)."""
+
+    required_keys = {"news_embeddings", "impression_rev_ind_array", "impression_len_list",
+                     "history_rev_ind_array", "history_len_list", "history_bool"}
+
+    def __init__(self, attention_model_path: Optional[Path] = None, dtype: Optional[torch.dtype] = None, **_):
+        self.attention_model = self._load(attention_model_path)
+        self.dtype = dtype
+
+    @staticmethod
+    def _load(path):
+        return get_final_attention_model(path)
+
+    def transform(self, context_dict):
+        check_req_keys(self.required_keys, context_dict)
+        new = context_dict.copy()
+        new.update(get_final_second_attention_score(
+            new["history_rev_ind_array"][0], new["history_len_list"], new["impression_rev_ind_array"][0],
+            new["impression_len_list"], new["news_embeddings"], new["history_bool"], self.attention_model,
+            dtype=self.dtype))
+        return new
+
+
+class LatentAttentionComponent(FinalAttentionComponent):
+    """Same scoring with LatentAttentionModel (the pooler BASELINE's north star names)."""
+
+    @staticmethod
+    def _load(path):
+        return get_latent_attention_model(path)
+
+
+def labels_of(context_dict) -> np.ndarray:
+    return context_dict["labels"]

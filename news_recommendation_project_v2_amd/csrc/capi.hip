@@ -1,0 +1,132 @@
+// C-ABI plumbing (errors, init, version) and the per-news pooler transforms,
+// which chain the GEMM / row kernels over row chunks with a caller workspace.
+#include "nr_common.h"
+
+#include <mutex>
+#include <string.h>
+
+namespace nr {
+
+static thread_local char g_err[512] = {0};
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+void clear_error() { g_err[0] = 0; }
+
+static int esize(int dtype) { return dtype == NR_F32 ? 4 : 2; }
+
+// Rows per chunk of the transforms: bounds the workspace at
+// 2 x 65536 x 4096 x 4 B = 2 GiB (f32) while keeping every GEMM >= 512 M-tiles.
+constexpr int64_t kChunk = 65536;
+
+}  // namespace nr
+
+extern "C" int nr_version(void) { return 100; }
+
+extern "C" const char* nr_last_error(void) { return nr::g_err; }
+
+extern "C" int nr_init(int device) {
+  nr::clear_error();
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    nr::set_error("nr_init: hipSetDevice(%d): %s", device, hipGetErrorString(e));
+    return NR_ERR_HIP;
+  }
+  return NR_OK;
+}
+
+// ---------------------------------------------------------------- FinalAttention
+extern "C" int64_t nr_final_attn_workspace_bytes(int dtype, int64_t n) {
+  const int64_t m = n < nr::kChunk ? n : nr::kChunk;
+  return 2 * m * 4096 * (int64_t)nr::esize(dtype);
+}
+
+// modeling_utils.py:218-224 on unique news rows (dropout inactive in eval):
+//   X1 = relu(E W1ᵀ + b1); X2 = relu(X1 W2ᵀ + b2); x = X2 W3ᵀ + b3;
+//   Y = relu(x W4ᵀ + b4); p = exp(Y W5ᵀ)  -> table[n][2][1024] = (x, p)
+extern "C" int nr_final_attn_transform(int dtype, int64_t n, const void* emb, int64_t emb_ld,
+                                       const void* W1, const float* b1, const void* W2,
+                                       const float* b2, const void* W3, const float* b3,
+                                       const void* W4, const float* b4, const void* W5,
+                                       void* table, void* ws, int64_t ws_bytes, void* stream) {
+  nr::clear_error();
+  NR_CHECK_ARG(dtype == NR_F32 || dtype == NR_BF16, "nr_final_attn_transform: bad dtype");
+  NR_CHECK_ARG(n >= 0, "nr_final_attn_transform: n < 0");
+  if (n == 0) return NR_OK;
+  NR_CHECK_ARG(emb && W1 && b1 && W2 && b2 && W3 && b3 && W4 && b4 && W5 && table && ws,
+               "nr_final_attn_transform: null pointer");
+  NR_CHECK_ARG(ws_bytes >= nr_final_attn_workspace_bytes(dtype, n),
+               "nr_final_attn_transform: workspace too small (%lld < %lld)", (long long)ws_bytes,
+               (long long)nr_final_attn_workspace_bytes(dtype, n));
+  const int es = nr::esize(dtype);
+  const int64_t D = 1024, H = 4096;
+  hipStream_t s = (hipStream_t)stream;
+  char* w0 = (char*)ws;
+  char* w1 = w0 + (int64_t)(n < nr::kChunk ? n : nr::kChunk) * H * es;
+  for (int64_t r0 = 0; r0 < n; r0 += nr::kChunk) {
+    const int64_t m = (n - r0) < nr::kChunk ? (n - r0) : nr::kChunk;
+    const char* e = (const char*)emb + r0 * emb_ld * es;
+    char* x = (char*)table + r0 * 2 * D * es;
+    char* p = x + D * es;
+    int rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RELU, m, H, D, e, emb_ld, W1, D, b1, nullptr, 0, w0, H, s))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RELU, m, H, H, w0, H, W2, H, b2, nullptr, 0, w1, H, s))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_NONE, m, D, H, w1, H, W3, H, b3, nullptr, 0, x, 2 * D, s))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RELU, m, H, D, x, 2 * D, W4, D, b4, nullptr, 0, w0, H, s))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_EXP, m, D, H, w0, H, W5, H, nullptr, nullptr, 0, p, 2 * D, s))) return rc;
+  }
+  return NR_OK;
+}
+
+// ---------------------------------------------------------------- Latent
+extern "C" int64_t nr_latent_workspace_bytes(int dtype, int64_t n) {
+  const int64_t m = n < nr::kChunk ? n : nr::kChunk;
+  const int64_t es = nr::esize(dtype);
+  // y [m,1024] dtype | s [m,512] f32 | p [m,512] dtype | f [m,4096] dtype
+  return m * (1024 * es + 512 * 4 + 512 * es + 4096 * es);
+}
+
+// latent_attention.py:157-163 with the 64 latents' K/V folded into A and Bt:
+//   y = LN_q(e); P = softmax64(y Aᵀ); h1 = e + P Btᵀ;
+//   h = h1 + GEGLU(LN_f(h1) W1iᵀ + b1i) W2ᵀ + b2     -> table[n][1024]
+extern "C" int nr_latent_transform(int dtype, int64_t n, const void* emb, int64_t emb_ld,
+                                   const float* lnq_g, const float* lnq_b, const void* A,
+                                   const void* Bt, const float* lnf_g, const float* lnf_b,
+                                   const void* W1i, const float* b1i, const void* W2,
+                                   const float* b2, void* table, void* ws, int64_t ws_bytes,
+                                   void* stream) {
+  nr::clear_error();
+  NR_CHECK_ARG(dtype == NR_F32 || dtype == NR_BF16, "nr_latent_transform: bad dtype");
+  NR_CHECK_ARG(n >= 0, "nr_latent_transform: n < 0");
+  if (n == 0) return NR_OK;
+  NR_CHECK_ARG(emb && A && Bt && W1i && b1i && W2 && b2 && table && ws,
+               "nr_latent_transform: null pointer");
+  NR_CHECK_ARG(ws_bytes >= nr_latent_workspace_bytes(dtype, n),
+               "nr_latent_transform: workspace too small");
+  const int es = nr::esize(dtype);
+  const int64_t D = 1024, S = 512, F = 4096;
+  const int64_t mc = n < nr::kChunk ? n : nr::kChunk;
+  hipStream_t st = (hipStream_t)stream;
+  char* wy = (char*)ws;
+  char* wsc = wy + mc * D * es;
+  char* wp = wsc + mc * S * 4;
+  char* wf = wp + mc * S * es;
+  for (int64_t r0 = 0; r0 < n; r0 += nr::kChunk) {
+    const int64_t m = (n - r0) < nr::kChunk ? (n - r0) : nr::kChunk;
+    const char* e = (const char*)emb + r0 * emb_ld * es;
+    char* h = (char*)table + r0 * D * es;
+    int rc;
+    if ((rc = nr::layernorm_dispatch(dtype, dtype, m, D, e, emb_ld, lnq_g, lnq_b, 1e-5f, wy, D, st))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, NR_F32, NR_EPI_NONE, m, S, D, wy, D, A, D, nullptr, nullptr, 0, wsc, S, st))) return rc;
+    if ((rc = nr::softmax64_dispatch(m, S / 64, (const float*)wsc, S, dtype, wp, S, st))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RESADD, m, D, S, wp, S, Bt, S, nullptr, e, emb_ld, h, D, st))) return rc;
+    if ((rc = nr::layernorm_dispatch(dtype, dtype, m, D, h, D, lnf_g, lnf_b, 1e-5f, wy, D, st))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_GEGLU, m, 2 * F, D, wy, D, W1i, D, b1i, nullptr, 0, wf, F, st))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RESADD, m, D, F, wf, F, W2, F, b2, h, D, h, D, st))) return rc;
+  }
+  return NR_OK;
+}

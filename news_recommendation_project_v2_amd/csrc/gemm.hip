@@ -1,0 +1,261 @@
+// MFMA GEMMs with fused epilogues for the per-news pooler transforms (gfx950).
+//
+//   C[M, N] = epilogue(A[M, K] · W[N, K]ᵀ)     (W in torch nn.Linear layout)
+//
+// Replaces nn.Linear (+ F.relu / torch.exp / GEGLU / residual add) in
+//   FinalAttention.forward        modeling_utils.py:218-222
+//   LatentAttentionModel blocks   latent_attention.py:34-36, 59-61, 162-163
+//
+// Two main loops share one tiling and one epilogue:
+//   f32 : v_mfma_f32_32x32x2_f32  (exact f32 fmaf chain; the parity config)
+//   bf16: v_mfma_f32_32x32x16_bf16 (bf16 operands, f32 accumulate)
+// Block tile 128x128, 256 threads = 4 waves in a 2x2 grid, each wave owns a
+// 64x64 output = 2x2 MFMA 32x32 accumulators (64 acc registers).  K is staged
+// through LDS in 128-byte row slices (BK = 32 f32 / 64 bf16) with a 16-byte
+// row pad (144-byte rows) so the ds_read_b128 fragment reads of 32 distinct
+// rows are bank-conflict free; global->register prefetch of tile k+1 overlaps
+// the MFMAs of tile k, one barrier per K tile.
+#include "nr_common.h"
+
+namespace nr {
+
+constexpr int GBM = 128, GBN = 128;
+constexpr int GROW = 36;  // LDS row stride in 32-bit words (128 B data + 16 B pad)
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+template <typename TO>
+__device__ __forceinline__ TO to_out(float v) {
+  if constexpr (sizeof(TO) == 4) return v; else return (TO)v;
+}
+template <typename TO>
+__device__ __forceinline__ float from_out(TO v) {
+  if constexpr (sizeof(TO) == 4) return v; else return (float)v;
+}
+
+// acc[mi][ni]: 32x32 tile at rows wrow + 32 mi, cols wcol + 32 ni.
+// C/D map (gfx950, dtype independent): col = lane & 31,
+// row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5).
+template <int EPI, typename TO>
+__device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], int64_t M, int64_t wrow,
+                                              int64_t wcol, int lane, const float* __restrict__ bias,
+                                              const TO* R, int64_t ldr, TO* C, int64_t ldc) {
+  const int cl = lane & 31;
+  const int rh = 4 * (lane >> 5);
+  if constexpr (EPI == NR_EPI_GEGLU) {
+    // ni = 0 holds the 32 "a" columns, ni = 1 the matching 32 "g" columns.
+    const int64_t ca = wcol + cl, cg = wcol + 32 + cl;
+    const float ba = bias ? bias[ca] : 0.f, bg = bias ? bias[cg] : 0.f;
+    const int64_t oc = wcol / 2 + cl;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int64_t row = wrow + 32 * mi + (reg & 3) + 8 * (reg >> 2) + rh;
+        if (row < M) {
+          const float a = acc[mi][0][reg] + ba;
+          const float g = acc[mi][1][reg] + bg;
+          C[row * ldc + oc] = to_out<TO>(a * gelu_erf(g));
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int64_t col = wcol + 32 * ni + cl;
+      const float b = bias ? bias[col] : 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int64_t row = wrow + 32 * mi + (reg & 3) + 8 * (reg >> 2) + rh;
+          if (row < M) {
+            float v = acc[mi][ni][reg] + b;
+            if constexpr (EPI == NR_EPI_RELU) v = fmaxf(v, 0.f);
+            if constexpr (EPI == NR_EPI_EXP) v = expf(v);
+            if constexpr (EPI == NR_EPI_RESADD) v += from_out<TO>(R[row * ldr + col]);
+            C[row * ldc + col] = to_out<TO>(v);
+          }
+        }
+      }
+    }
+  }
+}
+
+// TI = float (f32 MFMA, BK = 32) or __bf16 (bf16 MFMA, BK = 64).  A row slice
+// of one K tile is always 128 bytes = 8 x 16-byte chunks.
+template <typename TI, int EPI, typename TO>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(int64_t M, int64_t N, int64_t K,
+                                                      const TI* __restrict__ A, int64_t lda,
+                                                      const TI* __restrict__ W, int64_t ldw,
+                                                      const float* __restrict__ bias, const TO* R,
+                                                      int64_t ldr, TO* C, int64_t ldc) {
+  constexpr int BK = 128 / (int)sizeof(TI);
+  constexpr int TILE_WORDS = GBM * GROW;  // one operand tile, 32-bit words
+  __shared__ __attribute__((aligned(16))) uint32_t smem[2 * 2 * TILE_WORDS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t n0 = (int64_t)blockIdx.x * GBN;
+  const int64_t m0 = (int64_t)blockIdx.y * GBM;
+
+  // global -> register staging map: 4 chunks of 16 B per operand per thread
+  int srow[4], schk[4];
+  const uint4* ga[4];
+  const uint4* gw[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int id = tid + 256 * p;
+    srow[p] = id >> 3;
+    schk[p] = id & 7;
+    const int64_t ar = min(m0 + srow[p], M - 1);
+    ga[p] = reinterpret_cast<const uint4*>(A + ar * lda) + schk[p];
+    gw[p] = reinterpret_cast<const uint4*>(W + (n0 + srow[p]) * ldw) + schk[p];
+  }
+  const int64_t kstep16 = BK * (int64_t)sizeof(TI) / 16;  // 16-B chunks per K tile = 8
+
+  uint4 ra[4], rw[4];
+  auto gload = [&](int64_t kt) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      ra[p] = ga[p][kt * kstep16];
+      rw[p] = gw[p][kt * kstep16];
+    }
+  };
+  auto lstore = [&](int buf) {
+    uint32_t* As = smem + buf * 2 * TILE_WORDS;
+    uint32_t* Ws = As + TILE_WORDS;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      *reinterpret_cast<uint4*>(As + srow[p] * GROW + schk[p] * 4) = ra[p];
+      *reinterpret_cast<uint4*>(Ws + srow[p] * GROW + schk[p] * 4) = rw[p];
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+  const int arow0 = (wm * 64 + fr) * GROW, wrow0 = (wn * 64 + fr) * GROW;
+
+  auto compute = [&](int buf) {
+    const uint32_t* As = smem + buf * 2 * TILE_WORDS;
+    const uint32_t* Ws = As + TILE_WORDS;
+    if constexpr (sizeof(TI) == 4) {
+      // lane half h covers k = 16h + 4q + t of the 32-deep tile (A and W alike)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x4 af[2], wf[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          af[i] = *reinterpret_cast<const f32x4*>(As + arow0 + 32 * i * GROW + 16 * fh + 4 * q);
+          wf[i] = *reinterpret_cast<const f32x4*>(Ws + wrow0 + 32 * i * GROW + 16 * fh + 4 * q);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi][t], wf[ni][t], acc[mi][ni], 0, 0, 0);
+      }
+    } else {
+      // lane (r, h) holds k = 16ks + 8h + j, j < 8, of row r (32x32x16 operand map)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        bf16x8 af[2], wf[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          af[i] = *reinterpret_cast<const bf16x8*>(As + arow0 + 32 * i * GROW + 8 * ks + 4 * fh);
+          wf[i] = *reinterpret_cast<const bf16x8*>(Ws + wrow0 + 32 * i * GROW + 8 * ks + 4 * fh);
+        }
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], wf[ni], acc[mi][ni], 0, 0, 0);
+      }
+    }
+  };
+
+  const int64_t nk = K / BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const int cur = (int)(kt & 1);
+    if (kt + 1 < nk) gload(kt + 1);
+    compute(cur);
+    if (kt + 1 < nk) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  gemm_epilogue<EPI, TO>(acc, M, m0 + wm * 64, n0 + wn * 64, lane, bias, R, ldr, C, ldc);
+}
+
+template <typename TI, typename TO>
+static int launch_gemm_t(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                         const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
+                         void* C, int64_t ldc, hipStream_t s) {
+  dim3 grid((unsigned)(N / GBN), (unsigned)((M + GBM - 1) / GBM));
+  const TI* a = (const TI*)A;
+  const TI* w = (const TI*)W;
+  const TO* r = (const TO*)R;
+  TO* c = (TO*)C;
+  switch (epi) {
+    case NR_EPI_NONE: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_NONE, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    case NR_EPI_RELU: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_RELU, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    case NR_EPI_EXP: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_EXP, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    case NR_EPI_GEGLU: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_GEGLU, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    case NR_EPI_RESADD: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_RESADD, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
+  }
+  NR_CHECK_LAUNCH("nr_gemm");
+  return NR_OK;
+}
+
+int gemm_dispatch(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, int64_t K,
+                  const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+                  const void* R, int64_t ldr, void* C, int64_t ldc, hipStream_t s) {
+  NR_CHECK_ARG(dtype_in == NR_F32 || dtype_in == NR_BF16, "nr_gemm: bad dtype_in %d", dtype_in);
+  NR_CHECK_ARG(dtype_out == NR_F32 || dtype_out == NR_BF16, "nr_gemm: bad dtype_out %d", dtype_out);
+  NR_CHECK_ARG(M >= 0 && N > 0 && K > 0, "nr_gemm: bad shape M=%lld N=%lld K=%lld", (long long)M, (long long)N, (long long)K);
+  if (M == 0) return NR_OK;
+  const int64_t bk = dtype_in == NR_F32 ? 32 : 64;
+  if (N % GBN != 0 || K % bk != 0) {
+    set_error("nr_gemm: unsupported shape N=%lld (need %%128) K=%lld (need %%%lld)", (long long)N, (long long)K, (long long)bk);
+    return NR_ERR_UNSUPPORTED;
+  }
+  NR_CHECK_ARG(A && W && C, "nr_gemm: null operand");
+  NR_CHECK_ARG(epi != NR_EPI_RESADD || R, "nr_gemm: RESADD needs R");
+  const int64_t ea = dtype_in == NR_F32 ? 4 : 8;  // elements per 16 B
+  NR_CHECK_ARG(lda >= K && ldw >= K && lda % ea == 0 && ldw % ea == 0 &&
+                   ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0,
+               "nr_gemm: A/W must be 16-byte aligned with 16-byte row strides");
+  const int64_t ncols = epi == NR_EPI_GEGLU ? N / 2 : N;
+  NR_CHECK_ARG(ldc >= ncols, "nr_gemm: ldc too small");
+  NR_CHECK_ARG((M + GBM - 1) / GBM <= 65535, "nr_gemm: M too large (> 8.3M rows)");
+  if (dtype_in == NR_F32) {
+    if (dtype_out == NR_F32) return launch_gemm_t<float, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
+    return launch_gemm_t<float, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
+  }
+  if (dtype_out == NR_F32) return launch_gemm_t<__bf16, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
+  return launch_gemm_t<__bf16, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
+}
+
+}  // namespace nr
+
+extern "C" int nr_gemm(int dtype_in, int dtype_out, int epilogue, int64_t M, int64_t N, int64_t K,
+                       const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+                       const void* R, int64_t ldr, void* C, int64_t ldc, void* stream) {
+  nr::clear_error();
+  return nr::gemm_dispatch(dtype_in, dtype_out, epilogue, M, N, K, A, lda, W, ldw, bias, R, ldr, C,
+                           ldc, (hipStream_t)stream);
+}

@@ -1,0 +1,69 @@
+// Shared helpers for the newsrec HIP library (gfx950 / CDNA4 only).
+//
+// Error model of the C-ABI (include/newsrec.h): every entry point returns
+// NR_OK (0) or a negative code; the message is kept in a thread-local buffer
+// readable through nr_last_error().  No C++ exception crosses the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+#include "../../include/newsrec.h"
+
+namespace nr {
+
+void set_error(const char* fmt, ...);
+void clear_error();
+
+// internal dispatchers (validate + launch, no error reset)
+int gemm_dispatch(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, int64_t K,
+                  const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+                  const void* R, int64_t ldr, void* C, int64_t ldc, hipStream_t s);
+int layernorm_dispatch(int dti, int dto, int64_t rows, int64_t dim, const void* x, int64_t ldx,
+                       const float* g, const float* b, float eps, void* y, int64_t ldy,
+                       hipStream_t s);
+int softmax64_dispatch(int64_t rows, int64_t groups, const float* x, int64_t ldx, int dto, void* y,
+                       int64_t ldy, hipStream_t s);
+int inv_norm_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps,
+                      float* out, hipStream_t s);
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+  return v;
+}
+
+}  // namespace nr
+
+#define NR_CHECK_ARG(cond, ...)                 \
+  do {                                          \
+    if (!(cond)) {                              \
+      nr::set_error(__VA_ARGS__);               \
+      return NR_ERR_INVALID;                    \
+    }                                           \
+  } while (0)
+
+#define NR_CHECK_LAUNCH(name)                                                 \
+  do {                                                                        \
+    hipError_t _e = hipGetLastError();                                        \
+    if (_e != hipSuccess) {                                                   \
+      nr::set_error("%s: launch failed: %s", name, hipGetErrorString(_e));    \
+      return NR_ERR_HIP;                                                      \
+    }                                                                         \
+  } while (0)

@@ -1,0 +1,205 @@
+// Row-wise wavefront kernels: LayerNorm, 64-wide softmax, inverse L2 norm.
+// One wave per row (or per 64-group); 4 rows per 256-thread workgroup; the
+// whole row lives in registers, so every element is read from HBM once and
+// reductions are 64-lane butterflies (no LDS).
+#include "nr_common.h"
+
+namespace nr {
+
+// Lane-local load of 4 consecutive elements at element offset `e` (f32 or bf16).
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, float (&v)[4]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 f = *reinterpret_cast<const float4*>(p);
+    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    v[0] = bf16_lo(u.x); v[1] = bf16_hi(u.x); v[2] = bf16_lo(u.y); v[3] = bf16_hi(u.y);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(T* p, const float (&v)[4]) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    __bf16 b[4] = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    *reinterpret_cast<uint2*>(p) = *reinterpret_cast<uint2*>(b);
+  }
+}
+
+// torch.nn.LayerNorm semantics: biased variance, y = (x - mean) * rsqrt(var + eps) * g + b
+template <typename TI, typename TO, int DIM>
+__global__ __launch_bounds__(256) void layernorm_kernel(int64_t rows, const TI* __restrict__ x,
+                                                        int64_t ldx, const float* __restrict__ g,
+                                                        const float* __restrict__ b, float eps,
+                                                        TO* __restrict__ y, int64_t ldy) {
+  constexpr int NJ = DIM / 256;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float v[NJ][4];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    load4<TI>(x + row * ldx + j * 256 + lane * 4, v[j]);
+    s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+  }
+  const float mean = wave_sum(s) / (float)DIM;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float d = v[j][t] - mean;
+      q = fmaf(d, d, q);
+    }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)DIM + eps);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int e = j * 256 + lane * 4;
+    float o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float gg = g ? g[e + t] : 1.f, bb = b ? b[e + t] : 0.f;
+      o[t] = (v[j][t] - mean) * rstd * gg + bb;
+    }
+    store4<TO>(y + row * ldy + e, o);
+  }
+}
+
+template <typename TO>
+__global__ __launch_bounds__(256) void softmax64_kernel(int64_t items, int64_t groups,
+                                                        const float* __restrict__ x, int64_t ldx,
+                                                        TO* __restrict__ y, int64_t ldy) {
+  const int lane = threadIdx.x & 63;
+  const int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (it >= items) return;
+  const int64_t row = it / groups, grp = it % groups;
+  const float v = x[row * ldx + grp * 64 + lane];
+  const float m = wave_max(v);
+  const float e = expf(v - m);
+  const float s = wave_sum(e);
+  const float o = e / s;
+  if constexpr (sizeof(TO) == 4) y[row * ldy + grp * 64 + lane] = o;
+  else y[row * ldy + grp * 64 + lane] = (TO)o;
+}
+
+template <typename T, int DIM>
+__global__ __launch_bounds__(256) void inv_norm_kernel(int64_t rows, const T* __restrict__ x,
+                                                       int64_t ldx, float eps,
+                                                       float* __restrict__ out) {
+  constexpr int NJ = DIM / 256;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    float v[4];
+    load4<T>(x + row * ldx + j * 256 + lane * 4, v);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) q = fmaf(v[t], v[t], q);
+  }
+  q = wave_sum(q);
+  if (lane == 0) out[row] = 1.0f / fmaxf(sqrtf(q), eps);
+}
+
+template <typename TI, typename TO>
+static int launch_ln(int64_t rows, int64_t dim, const void* x, int64_t ldx, const float* g,
+                     const float* b, float eps, void* y, int64_t ldy, hipStream_t s) {
+  const dim3 grid((unsigned)((rows + 3) / 4));
+#define NR_LN_CASE(D)                                                                      \
+  case D:                                                                                  \
+    hipLaunchKernelGGL((layernorm_kernel<TI, TO, D>), grid, dim3(256), 0, s, rows,        \
+                       (const TI*)x, ldx, g, b, eps, (TO*)y, ldy);                          \
+    break;
+  switch (dim) {
+    NR_LN_CASE(256) NR_LN_CASE(512) NR_LN_CASE(768) NR_LN_CASE(1024) NR_LN_CASE(2048)
+    default: set_error("nr_layernorm: dim %lld unsupported", (long long)dim); return NR_ERR_UNSUPPORTED;
+  }
+#undef NR_LN_CASE
+  NR_CHECK_LAUNCH("nr_layernorm");
+  return NR_OK;
+}
+
+int layernorm_dispatch(int dti, int dto, int64_t rows, int64_t dim, const void* x, int64_t ldx,
+                       const float* g, const float* b, float eps, void* y, int64_t ldy,
+                       hipStream_t s) {
+  NR_CHECK_ARG((dti == NR_F32 || dti == NR_BF16) && (dto == NR_F32 || dto == NR_BF16), "nr_layernorm: bad dtype");
+  NR_CHECK_ARG(rows >= 0 && ldx >= dim && ldy >= dim && ldx % 4 == 0 && ldy % 4 == 0, "nr_layernorm: bad strides");
+  if (rows == 0) return NR_OK;
+  NR_CHECK_ARG(x && y, "nr_layernorm: null pointer");
+  if (dti == NR_F32) {
+    if (dto == NR_F32) return launch_ln<float, float>(rows, dim, x, ldx, g, b, eps, y, ldy, s);
+    return launch_ln<float, __bf16>(rows, dim, x, ldx, g, b, eps, y, ldy, s);
+  }
+  if (dto == NR_F32) return launch_ln<__bf16, float>(rows, dim, x, ldx, g, b, eps, y, ldy, s);
+  return launch_ln<__bf16, __bf16>(rows, dim, x, ldx, g, b, eps, y, ldy, s);
+}
+
+int softmax64_dispatch(int64_t rows, int64_t groups, const float* x, int64_t ldx, int dto, void* y,
+                       int64_t ldy, hipStream_t s) {
+  NR_CHECK_ARG(rows >= 0 && groups > 0 && ldx >= groups * 64 && ldy >= groups * 64, "nr_softmax64: bad shape");
+  NR_CHECK_ARG(dto == NR_F32 || dto == NR_BF16, "nr_softmax64: bad dtype");
+  if (rows == 0) return NR_OK;
+  NR_CHECK_ARG(x && y, "nr_softmax64: null pointer");
+  const int64_t items = rows * groups;
+  const dim3 grid((unsigned)((items + 3) / 4));
+  if (dto == NR_F32)
+    hipLaunchKernelGGL((softmax64_kernel<float>), grid, dim3(256), 0, s, items, groups, x, ldx, (float*)y, ldy);
+  else
+    hipLaunchKernelGGL((softmax64_kernel<__bf16>), grid, dim3(256), 0, s, items, groups, x, ldx, (__bf16*)y, ldy);
+  NR_CHECK_LAUNCH("nr_softmax64");
+  return NR_OK;
+}
+
+int inv_norm_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps,
+                      float* out, hipStream_t s) {
+  NR_CHECK_ARG(dtype == NR_F32 || dtype == NR_BF16, "nr_row_inv_norm: bad dtype");
+  NR_CHECK_ARG(rows >= 0 && ldx >= dim && ldx % 4 == 0, "nr_row_inv_norm: bad strides");
+  if (rows == 0) return NR_OK;
+  NR_CHECK_ARG(x && out, "nr_row_inv_norm: null pointer");
+  const dim3 grid((unsigned)((rows + 3) / 4));
+#define NR_IN_CASE(T, D)                                                                        \
+  case D:                                                                                       \
+    hipLaunchKernelGGL((inv_norm_kernel<T, D>), grid, dim3(256), 0, s, rows, (const T*)x, ldx,  \
+                       eps, out);                                                               \
+    break;
+  if (dtype == NR_F32) {
+    switch (dim) {
+      NR_IN_CASE(float, 256) NR_IN_CASE(float, 512) NR_IN_CASE(float, 768) NR_IN_CASE(float, 1024) NR_IN_CASE(float, 2048)
+      default: set_error("nr_row_inv_norm: dim %lld unsupported", (long long)dim); return NR_ERR_UNSUPPORTED;
+    }
+  } else {
+    switch (dim) {
+      NR_IN_CASE(__bf16, 256) NR_IN_CASE(__bf16, 512) NR_IN_CASE(__bf16, 768) NR_IN_CASE(__bf16, 1024) NR_IN_CASE(__bf16, 2048)
+      default: set_error("nr_row_inv_norm: dim %lld unsupported", (long long)dim); return NR_ERR_UNSUPPORTED;
+    }
+  }
+#undef NR_IN_CASE
+  NR_CHECK_LAUNCH("nr_row_inv_norm");
+  return NR_OK;
+}
+
+}  // namespace nr
+
+extern "C" int nr_layernorm(int dtype_in, int dtype_out, int64_t rows, int64_t dim, const void* x,
+                            int64_t ldx, const float* gamma, const float* beta, float eps, void* y,
+                            int64_t ldy, void* stream) {
+  nr::clear_error();
+  return nr::layernorm_dispatch(dtype_in, dtype_out, rows, dim, x, ldx, gamma, beta, eps, y, ldy,
+                                (hipStream_t)stream);
+}
+
+extern "C" int nr_softmax64(int64_t rows, int64_t groups, const float* x, int64_t ldx,
+                            int dtype_out, void* y, int64_t ldy, void* stream) {
+  nr::clear_error();
+  return nr::softmax64_dispatch(rows, groups, x, ldx, dtype_out, y, ldy, (hipStream_t)stream);
+}
+
+extern "C" int nr_row_inv_norm(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx,
+                               float eps, float* out, void* stream) {
+  nr::clear_error();
+  return nr::inv_norm_dispatch(dtype, rows, dim, x, ldx, eps, out, (hipStream_t)stream);
+}

@@ -1,0 +1,92 @@
+"""Glue between the data layer and the poolers (reference data_model_helper.py).
+
+Same signatures and return types as the reference functions of the hot path;
+the work runs on the MI355X through ``PoolScoreEngine``:
+  reference (CPU/GPU torch)                           here (HIP)
+  pad each batch to its longest history, run the      per-news transform once
+  pooler on every padded slot, mask  (:112-131)       (MFMA GEMM chain) + segmented
+  per-impression F.cosine_similarity loop (:199-230)  pool+score kernel, one launch
+  rankdata per impression (:442, data_utils:414)      nr_dense_rank kernel
+"""
+from __future__ import annotations
+
+from typing import Iterable, Optional
+
+import numpy as np
+import torch
+
+from .config import DEVICE
+from .data_utils import group_items
+from .engine import PoolScoreEngine
+
+# Compute dtype of the table/GEMM path.  float32 is the parity configuration
+# (scores within 1e-4 of the reference); bfloat16 is BASELINE config 3.
+COMPUTE_DTYPE = torch.float32
+
+
+def _engine(model, news_embeddings, query_news_embeddings=None, dtype=None) -> PoolScoreEngine:
+    eng = PoolScoreEngine(model, dtype=dtype or COMPUTE_DTYPE, device=DEVICE)
+    eng.load_news(news_embeddings, query_news_embeddings)
+    return eng
+
+
+def get_final_attention_eval(history_rev_index: np.ndarray, history_len_list: np.ndarray,
+                             news_embeddings: torch.Tensor, model: torch.nn.Module, dtype=None) -> torch.Tensor:
+    """Pooled user vectors [I', D] on the host (data_model_helper.py:112-131)."""
+    eng = _engine(model, news_embeddings, dtype=dtype)
+    n = len(history_len_list)
+    eng.load_impressions(history_rev_index, history_len_list, np.zeros(0, np.int32), np.zeros(n, np.int32))
+    eng.hist_table = eng.transform()
+    eng.inv_norms()
+    _, users = eng.pool_score(want_users=True)
+    return users.cpu()
+
+
+def get_cos_sim_scores(history_rev_index: np.ndarray, history_len_list: np.ndarray, news_rev_index: np.ndarray,
+                       impression_len_list: np.ndarray, news_embeddings: torch.Tensor, model: torch.nn.Module,
+                       query_news_embeddings: Optional[torch.Tensor] = None, dtype=None) -> torch.Tensor:
+    """Cosine score of every candidate against its impression's pooled history,
+    impression-major [C] f32 on the host (data_model_helper.py:174-239)."""
+    assert len(history_len_list) == len(impression_len_list), "Number of rows should be consistent"
+    assert sum(impression_len_list) == len(news_rev_index), \
+        "Number of impressions should match length of impression list"
+    eng = _engine(model, news_embeddings, query_news_embeddings if isinstance(query_news_embeddings, torch.Tensor)
+                  else None, dtype=dtype)
+    eng.load_impressions(history_rev_index, history_len_list, news_rev_index, impression_len_list)
+    scores, _ = eng.step()
+    return scores.cpu()
+
+
+def get_final_second_attention_score(history_rev_index: np.ndarray, history_len_list: np.ndarray,
+                                     news_rev_index: np.ndarray, impression_len_list: np.ndarray,
+                                     news_embeddings: torch.Tensor, history_bool, attention_model: torch.nn.Module,
+                                     dtype=None) -> dict:
+    """Scores of the impressions that have a history, then dense ranks per
+    impression (data_model_helper.py:416-443).
+
+    As in the reference, ``grouped_scores`` groups by the UNFILTERED
+    ``impression_len_list`` (consistent under DataSubset.WITH_HISTORY).
+    """
+    hb = np.asarray(history_bool, dtype=bool)
+    imp_len = np.asarray(impression_len_list)
+    cand_keep = np.repeat(hb, imp_len)
+    sub_news = np.asarray(news_rev_index)[cand_keep]
+    sub_len = imp_len[hb]
+    assert len(history_len_list) == len(sub_len), "Number of rows should be consistent"
+    eng = _engine(attention_model, news_embeddings, dtype=dtype)
+    eng.load_impressions(history_rev_index, history_len_list, sub_news, sub_len)
+    scores_d, _ = eng.step()
+    scores = scores_d.cpu().numpy()
+    if hb.all():
+        ranks = eng.rank(scores_d).cpu().numpy().astype(np.int64)
+        grouped = group_items(ranks, imp_len)
+    else:  # reference quirk: grouping by the unfiltered lengths
+        from .data_utils import rank_group_preds
+        grouped = rank_group_preds(scores, imp_len)
+    return {"scores": scores, "grouped_scores": grouped}
+
+
+def get_embeddings(model_path: str, news_list: Iterable[str], news_text_dict: dict[str, str]):
+    """Title encoder entry (data_model_helper.py:45-84): see encoder.py."""
+    from .encoder import get_embeddings as _ge
+    return _ge(model_path, news_list, news_text_dict)

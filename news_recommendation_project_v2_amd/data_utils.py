@@ -1,0 +1,204 @@
+"""Data layer of the hot path: MIND behaviours -> CSR index arrays.
+
+Mirrors the reference's ``src/news_rec_utils/data_utils.py`` functions that the
+embed -> pool -> score path uses (load_dataset 26-122,
+split_impressions_and_history 168-232, group_items 400-411, rank_group_preds
+414-415, pad_to_maxlen 723-750, eval datasets 485-509).  Outputs are
+bit-identical to the reference's, including its numpy quirks (``labels`` and
+``group_items`` results built with ``np.array(..., dtype=object)``).
+
+``to_csr`` turns the reference's (flat index, per-row length) pairs into the
+device layout the HIP kernels consume: int32 row indices + int64 offsets.
+"""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+from typing import Any, Callable, Optional, Sequence
+
+import numpy as np
+import torch
+from torch.utils.data import Dataset
+
+from .config import DataSubset, NewsDataset
+
+
+def load_dataset(data_dir: Path, news_dataset: NewsDataset, num_samples: Optional[int] = None,
+                 data_subset: Optional[DataSubset] = DataSubset.ALL,
+                 random_state: int | np.random.Generator = 1234):
+    """Read ``{data_dir}/processed/{split}/behaviors.parquet`` and ``news_text.parquet``
+    (layout written by the reference's ``store_processed_data``, data_utils.py:442-455).
+
+    Returns ``(behaviors, feature_dict)`` like data_utils.py:114-122.  Entity
+    embeddings and category maps are optional here (they are not read by the
+    embed -> pool -> score path); missing files give empty dicts.
+    """
+    import pandas as pd
+
+    base = Path(data_dir) / "processed" / news_dataset.value
+    behaviors = pd.read_parquet(base / "behaviors.parquet", columns=["ImpressionID", "History", "Impressions"])
+    news_text = pd.read_parquet(base / "news_text.parquet").set_index("NewsID")
+
+    def _json(p: Path) -> dict:
+        return json.loads(p.read_text()) if p.is_file() else {}
+
+    cat_dict = _json(Path(data_dir) / "categories.json")
+    sub_cat_dict = _json(Path(data_dir) / "sub_categories.json")
+
+    feats: dict[str, Any] = {"news_text_dict": news_text["news_text"].to_dict()}
+    if "Title" in news_text:
+        feats["news_title_dict"] = {k: "News Title: " + v for k, v in news_text["Title"].to_dict().items()}
+    if "Abstract" in news_text:
+        feats["news_abstract_dict"] = {k: "News Abstract: " + v
+                                       for k, v in news_text["Abstract"].dropna().to_dict().items()}
+    if "Category" in news_text:
+        feats["news_category"] = news_text["Category"].map(cat_dict).to_dict()
+    if "SubCategory" in news_text:
+        feats["news_subcategory"] = news_text["SubCategory"].map(sub_cat_dict).to_dict()
+
+    if data_subset == DataSubset.WITH_HISTORY:
+        behaviors = behaviors[behaviors["History"].notna()].reset_index(drop=True)
+    elif data_subset == DataSubset.WITHOUT_HISTORY:
+        behaviors = behaviors[behaviors["History"].isna()].reset_index(drop=True)
+    if num_samples and num_samples < len(behaviors):
+        behaviors = behaviors.sample(n=num_samples, random_state=random_state, replace=False).reset_index(drop=True)
+    return behaviors, feats
+
+
+def split_impressions_and_history(impressions: Sequence[str], history: Sequence[Optional[str]]) -> dict[str, Any]:
+    """Parse behaviours rows into first-appearance-ordered news ids and int32
+    index arrays (data_utils.py:168-232).
+
+    Per row the history ids are registered before the impression ids; a falsy
+    history (None / "") contributes no history row.  Returns the reference's
+    keys: news_list, impression_rev_ind_array [2, C], impression_len_list [I],
+    history_rev_ind_array [2, H], history_len_list [I'], labels.
+    """
+    assert len(impressions) > 0, "No Impressions given"
+    imps = list(impressions)
+    hists = list(history)
+    label_present = "-" in imps[0]
+    position: dict[str, int] = {}
+    news_list: list[str] = []
+
+    def pos(nid: str) -> int:
+        p = position.get(nid)
+        if p is None:
+            p = len(news_list)
+            position[nid] = p
+            news_list.append(nid)
+        return p
+
+    imp_idx: list[int] = []
+    hist_idx: list[int] = []
+    labels: list[tuple] = []
+    hist_len: list[int] = []
+    imp_len: list[int] = []
+    for imp_row, hist_row in zip(imps, hists):
+        if hist_row:
+            toks = hist_row.split()
+            hist_len.append(len(toks))
+            hist_idx.extend([pos(t) for t in toks])
+        toks = imp_row.split()
+        if label_present:
+            pairs = [t.split("-") for t in toks]
+            ids = [p[0] for p in pairs]
+            labels.append(tuple(int(p[1]) for p in pairs))
+        else:
+            ids = toks
+        imp_len.append(len(ids))
+        imp_idx.extend([pos(t) for t in ids])
+
+    imp_len_a = np.array(imp_len, dtype=np.int32)
+    hist_len_a = np.array(hist_len, dtype=np.int32)
+    return {
+        "news_list": np.array(news_list),
+        "impression_rev_ind_array": np.stack([
+            np.array(imp_idx, dtype=np.int32),
+            np.repeat(np.arange(len(imp_len), dtype=np.int32), imp_len_a),
+        ]),
+        "impression_len_list": imp_len_a,
+        "history_rev_ind_array": np.stack([
+            np.array(hist_idx, dtype=np.int32),
+            np.repeat(np.arange(len(hist_len), dtype=np.int32), hist_len_a),
+        ]),
+        "history_len_list": hist_len_a,
+        "labels": np.array(labels, dtype=object),
+    }
+
+
+def group_items(items: np.ndarray, imp_counts: np.ndarray,
+                func: Callable[[np.ndarray], np.ndarray] = lambda x: x) -> np.ndarray:
+    """Split ``items`` into consecutive runs of ``imp_counts`` (data_utils.py:400-411)."""
+    ends = np.cumsum(np.asarray(imp_counts, dtype=np.int64))
+    starts = ends - np.asarray(imp_counts, dtype=np.int64)
+    return np.array([func(items[s:e]) for s, e in zip(starts, ends)], dtype=object)
+
+
+def lengths_to_offsets(lengths: np.ndarray) -> np.ndarray:
+    off = np.zeros(len(lengths) + 1, dtype=np.int64)
+    np.cumsum(np.asarray(lengths, dtype=np.int64), out=off[1:])
+    return off
+
+
+def rank_group_preds(pred_scores: np.ndarray, imp_counts: np.ndarray) -> np.ndarray:
+    """Per-impression dense descending ranks (data_utils.py:414-415), computed by
+    the HIP kernel ``nr_dense_rank`` and grouped into an object array of int64
+    arrays exactly like ``group_items(..., rankdata(-x, 'dense'))``."""
+    from . import ops
+    from .config import DEVICE
+
+    scores = torch.as_tensor(np.ascontiguousarray(pred_scores, dtype=np.float32)).to(DEVICE)
+    # group_items slices past the end of a short score array (the reference's
+    # unfiltered-lengths quirk, data_model_helper.py:442): clip like slicing does
+    off = torch.as_tensor(np.minimum(lengths_to_offsets(imp_counts), len(pred_scores))).to(DEVICE)
+    ranks = ops.dense_rank(scores, off).cpu().numpy().astype(np.int64)
+    return group_items(ranks, imp_counts)
+
+
+def pad_to_maxlen(grouped_items) -> dict[str, np.ndarray]:
+    """Right-pad index groups with 0 and build the int32 mask (data_utils.py:723-750)."""
+    lens = [len(g) for g in grouped_items]
+    width = max(lens)
+    idx = np.zeros((len(lens), width), dtype=np.int32)
+    mask = np.zeros((len(lens), width), dtype=np.int32)
+    for r, g in enumerate(grouped_items):
+        idx[r, :lens[r]] = g
+        mask[r, :lens[r]] = 1
+    return {"indices": idx, "attention_mask": mask}
+
+
+def to_csr(rev_index: np.ndarray, len_list: np.ndarray, device=None):
+    """(flat int32 indices, per-row lengths) -> device (int32 idx, int64 offsets)."""
+    idx = torch.as_tensor(np.ascontiguousarray(rev_index, dtype=np.int32))
+    off = torch.as_tensor(lengths_to_offsets(len_list))
+    if device is not None:
+        idx, off = idx.to(device), off.to(device)
+    return idx, off
+
+
+class NewsTextDataset(Dataset):
+    """news id -> text (data_utils.py:485-487)."""
+
+    def __init__(self, text_list, news_text_dict: dict[str, str]):
+        self.text_list = list(text_list)
+        self.news_text_dict = news_text_dict
+
+    def __len__(self):
+        return len(self.text_list)
+
+    def __getitem__(self, idx):
+        return self.news_text_dict[self.text_list[idx]]
+
+
+class FinalAttentionEvalDataset(Dataset):
+    """Grouped history indices per impression (data_utils.py:501-509)."""
+
+    def __init__(self, history_rev_index: np.ndarray, history_len_list: np.ndarray):
+        self.group_history = group_items(history_rev_index, history_len_list)
+
+    def __len__(self):
+        return len(self.group_history)
+
+    def __getitem__(self, idx):
+        return self.group_history[idx]

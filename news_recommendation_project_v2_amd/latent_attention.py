@@ -1,0 +1,169 @@
+"""Perceiver-style latent-attention history pooler (reference latent_attention.py).
+
+Parameter names match the reference module (latent_attention.py:115-131), so a
+reference state_dict loads unchanged:
+  latents [64, 1024]
+  cross_attend_blocks.0.{norm, norm_context}.{weight, bias}
+  cross_attend_blocks.0.fn.{to_q [4096,1024], to_kv [8192,1024], to_out [1024,4096]}.weight
+  cross_attend_blocks.1.norm.{weight, bias}
+  cross_attend_blocks.1.fn.net.0.{weight [8192,1024], bias}, .net.2.{weight [1024,4096], bias}
+
+MI355X formulation.  Every history item attends to the SAME 64 latents, so the
+keys/values depend only on the weights (latent_attention.py:161-162 rebuilds
+them for every batch row).  They are computed once per model and folded into
+the query and output projections:
+  scores_h = LN_q(e) W_q,hᵀ K_hᵀ / sqrt(512) = LN_q(e) · A_hᵀ,   A_h  = K_h W_q,h / sqrt(512)
+  out      = sum_h W_o,h (P_h V_h)            = P · Btᵀ,        Bt[:, h*64+j] = W_o,h V_h[j]
+which turns the 1024->4096 query and 4096->1024 output projections (16.8
+MFLOP/item) into 1024->512 and 512->1024 GEMMs (2.1 MFLOP/item), exact up to
+f32 rounding.  The fold is done once in float64 on the host (a weight loader
+step, like reading a checkpoint), then moved to the device.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import torch
+
+from . import ops
+from ._lib import NewsRecHIPError
+from .config import (EMBEDDING_DIM, LATENT_CROSS_DIM_HEAD, LATENT_CROSS_HEADS, LATENT_FF_MULT,
+                     LATENT_NUM_LATENTS, REDUCED_DIM)
+
+
+class PreNorm(torch.nn.Module):
+    """LayerNorm on the input (and on the context when context_dim is given)."""
+
+    def __init__(self, dim: int, fn: torch.nn.Module, context_dim: Optional[int] = None):
+        super().__init__()
+        self.fn = fn
+        self.norm = torch.nn.LayerNorm(dim)
+        self.norm_context = torch.nn.LayerNorm(context_dim) if context_dim is not None else None
+
+
+class GEGLU(torch.nn.Module):
+    """a * gelu(g) over the two halves of the last dim (latent_attention.py:24-27)."""
+
+
+class FeedForward(torch.nn.Module):
+    def __init__(self, dim: int, mult: int = 4):
+        super().__init__()
+        self.net = torch.nn.Sequential(torch.nn.Linear(dim, dim * mult * 2), GEGLU(),
+                                       torch.nn.Linear(dim * mult, dim))
+
+
+class Attention(torch.nn.Module):
+    def __init__(self, query_dim: int, context_dim: Optional[int] = None, heads: int = 8, dim_head: int = 64):
+        super().__init__()
+        inner = dim_head * heads
+        context_dim = query_dim if context_dim is None else context_dim
+        self.scale = dim_head ** -0.5
+        self.heads = heads
+        self.to_q = torch.nn.Linear(query_dim, inner, bias=False)
+        self.to_kv = torch.nn.Linear(context_dim, inner * 2, bias=False)
+        self.to_out = torch.nn.Linear(inner, query_dim, bias=False)
+
+
+def interleave_geglu_rows(w: torch.Tensor, block: int = 32) -> torch.Tensor:
+    """[2F, ...] with rows (a_0..a_F-1, g_0..g_F-1) -> 32-row blocks (a, g, a, g, ...)
+    so one 64-column GEMM tile holds matching a/g columns (NR_EPI_GEGLU)."""
+    two_f = w.shape[0]
+    f = two_f // 2
+    a = w[:f].reshape(f // block, block, *w.shape[1:])
+    g = w[f:].reshape(f // block, block, *w.shape[1:])
+    return torch.stack([a, g], dim=1).reshape(two_f, *w.shape[1:])
+
+
+class LatentAttentionModel(torch.nn.Module):
+    """forward(embeddings [B, L, D], attention_mask [B, L] | None).
+
+    mask given : [B, D] = normalize(masked mean over L of the per-item hiddens)
+    mask None  : [B, L, D] per-item hiddens (latent_attention.py:165)
+    """
+
+    pooler_kind = "latent"
+
+    def __init__(self):
+        super().__init__()
+        if EMBEDDING_DIM == 4096:  # latent_attention.py:91-97
+            num_latents, latent_dim, heads, dim_head = 32, REDUCED_DIM, 2, 32
+        else:
+            num_latents, latent_dim, heads, dim_head = (LATENT_NUM_LATENTS, REDUCED_DIM, LATENT_CROSS_HEADS,
+                                                        LATENT_CROSS_DIM_HEAD)
+        dim = REDUCED_DIM
+        self.cross_attend_blocks = torch.nn.ModuleList([
+            PreNorm(latent_dim, Attention(latent_dim, dim, heads=heads, dim_head=dim_head), context_dim=dim),
+            PreNorm(latent_dim, FeedForward(latent_dim, mult=LATENT_FF_MULT)),
+        ])
+        self.output_normalize = True
+        self.latents = torch.nn.Parameter(torch.randn(num_latents, latent_dim))
+        self._hip_cache: Dict[tuple, dict] = {}
+
+    def _param_key(self, dtype):
+        ps = list(self.parameters())
+        return (dtype, ps[0].device, tuple((p.data_ptr(), p._version) for p in ps))
+
+    @torch.no_grad()
+    def folded_weights(self) -> Dict[str, torch.Tensor]:
+        """float64 host fold of the constant latent K/V into A and Bt (see module doc)."""
+        attn_blk, ff_blk = self.cross_attend_blocks
+        attn = attn_blk.fn
+        h = attn.heads
+        d64 = lambda t: t.detach().to("cpu", torch.float64)
+        lat = d64(self.latents)
+        lat_n = torch.nn.functional.layer_norm(lat, lat.shape[-1:], d64(attn_blk.norm_context.weight),
+                                               d64(attn_blk.norm_context.bias), attn_blk.norm_context.eps)
+        kv = lat_n @ d64(attn.to_kv.weight).T                # [nl, 2*inner]
+        inner = kv.shape[1] // 2
+        dh = inner // h
+        k, v = kv[:, :inner], kv[:, inner:]
+        wq = d64(attn.to_q.weight)                         # [inner, D]
+        wo = d64(attn.to_out.weight)                       # [D, inner]
+        scale = 1.0 / math.sqrt(dh)                        # SDPA default scale
+        a_blocks, bt_blocks = [], []
+        for hh in range(h):
+            sl = slice(hh * dh, (hh + 1) * dh)
+            a_blocks.append((k[:, sl] @ wq[sl, :]) * scale)   # [nl, D]
+            bt_blocks.append(wo[:, sl] @ v[:, sl].T)          # [D, nl]
+        ff = ff_blk.fn.net
+        return {
+            "A": torch.cat(a_blocks, 0),
+            "Bt": torch.cat(bt_blocks, 1),
+            "W1i": interleave_geglu_rows(d64(ff[0].weight)),
+            "b1i": interleave_geglu_rows(d64(ff[0].bias)),
+            "W2": d64(ff[2].weight),
+            "b2": d64(ff[2].bias),
+            "lnq_g": d64(attn_blk.norm.weight), "lnq_b": d64(attn_blk.norm.bias),
+            "lnf_g": d64(ff_blk.norm.weight), "lnf_b": d64(ff_blk.norm.bias),
+        }
+
+    def hip_weights(self, dtype: torch.dtype = torch.float32) -> dict:
+        key = self._param_key(dtype)
+        w = self._hip_cache.get(key)
+        if w is None:
+            dev = self.latents.device
+            fw = self.folded_weights()
+            w = {}
+            for name, t in fw.items():
+                tgt = dtype if name in ("A", "Bt", "W1i", "W2") else torch.float32
+                w[name] = t.to(tgt).to(dev).contiguous()
+            self._hip_cache = {key: w}
+        return w
+
+    def item_table(self, rows: torch.Tensor, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+        """Per-item hiddens [n, D] for rows [n, D] (one per unique news)."""
+        dtype = dtype or rows.dtype
+        return ops.latent_transform(rows.to(dtype).contiguous(), self.hip_weights(dtype))
+
+    def forward(self, embeddings: torch.Tensor, attention_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if embeddings.device.type != "cuda":
+            raise NewsRecHIPError("LatentAttentionModel.forward runs on the MI355X HIP path only (got a CPU tensor)")
+        b, l, d = embeddings.shape
+        if attention_mask is None:
+            table = self.item_table(embeddings.reshape(b * l, d).float())
+            return table.reshape(b, l, d)
+        from .modeling_utils import flatten_valid, pool_rows
+        rows, off = flatten_valid(embeddings, attention_mask)
+        table = self.item_table(rows.float())
+        return pool_rows("latent", table, off)

@@ -1,0 +1,220 @@
+"""Tensor-level wrappers over the C-ABI (include/newsrec.h).
+
+Every function takes device tensors (PyTorch-ROCm "cuda" tensors), validates
+shapes/dtypes/strides on the host, and enqueues the HIP kernel on the current
+torch stream.  There is no CPU fallback: non-device tensors raise.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+_DT = {torch.float32: _lib.NR_F32, torch.bfloat16: _lib.NR_BF16}
+_EPI = {
+    "none": _lib.NR_EPI_NONE,
+    "relu": _lib.NR_EPI_RELU,
+    "exp": _lib.NR_EPI_EXP,
+    "geglu": _lib.NR_EPI_GEGLU,
+    "resadd": _lib.NR_EPI_RESADD,
+}
+POOLERS = {"final": _lib.NR_POOL_FINAL, "latent": _lib.NR_POOL_LATENT}
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(dev: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _dev(*ts: Optional[torch.Tensor]) -> torch.device:
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise _lib.NewsRecHIPError(
+                f"HIP kernels need device tensors, got a tensor on {t.device} (no CPU fallback)")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise _lib.NewsRecHIPError(f"tensors on different devices: {dev} vs {t.device}")
+    return dev
+
+
+def _rowmajor(t: torch.Tensor, name: str) -> int:
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise _lib.NewsRecHIPError(f"{name} must be a row-major 2-D tensor (stride(1)==1)")
+    return t.stride(0)
+
+
+def _dtype(t: torch.Tensor, name: str) -> int:
+    if t.dtype not in _DT:
+        raise _lib.NewsRecHIPError(f"{name}: unsupported dtype {t.dtype}")
+    return _DT[t.dtype]
+
+
+def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+         epilogue: str = "none", residual: Optional[torch.Tensor] = None,
+         out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """out = epilogue(a @ w.T + bias [+ residual]); w in nn.Linear layout [N, K]."""
+    dev = _dev(a, w, bias, residual, out)
+    if a.dtype != w.dtype:
+        raise _lib.NewsRecHIPError("gemm: a and w must share a dtype")
+    M, K = a.shape
+    N, K2 = w.shape
+    if K != K2:
+        raise _lib.NewsRecHIPError(f"gemm: K mismatch {K} vs {K2}")
+    epi = _EPI[epilogue]
+    ncols = N // 2 if epilogue == "geglu" else N
+    if out is None:
+        out = torch.empty((M, ncols), dtype=out_dtype or a.dtype, device=dev)
+    if bias is not None and (bias.dtype != torch.float32 or not bias.is_contiguous() or bias.numel() != N):
+        raise _lib.NewsRecHIPError("gemm: bias must be contiguous f32 [N]")
+    if residual is not None and residual.dtype != out.dtype:
+        raise _lib.NewsRecHIPError("gemm: residual must have the output dtype")
+    if out.shape != (M, ncols):
+        raise _lib.NewsRecHIPError(f"gemm: out shape {tuple(out.shape)} != {(M, ncols)}")
+    lda, ldw, ldc = _rowmajor(a, "a"), _rowmajor(w, "w"), _rowmajor(out, "out")
+    ldr = _rowmajor(residual, "residual") if residual is not None else 0
+    _lib.call("nr_gemm", _dtype(a, "a"), _dtype(out, "out"), epi, M, N, K, _ptr(a), lda, _ptr(w), ldw,
+              _ptr(bias), _ptr(residual), ldr, _ptr(out), ldc, _stream(dev))
+    return out
+
+
+def layernorm(x: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optional[torch.Tensor], eps: float,
+              out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    dev = _dev(x, gamma, beta, out)
+    rows, dim = x.shape
+    if out is None:
+        out = torch.empty((rows, dim), dtype=out_dtype or x.dtype, device=dev)
+    _lib.call("nr_layernorm", _dtype(x, "x"), _dtype(out, "out"), rows, dim, _ptr(x), _rowmajor(x, "x"),
+              _ptr(gamma), _ptr(beta), ctypes.c_float(eps), _ptr(out), _rowmajor(out, "out"), _stream(dev))
+    return out
+
+
+def softmax64(x: torch.Tensor, out: Optional[torch.Tensor] = None,
+              out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    dev = _dev(x, out)
+    if x.dtype != torch.float32:
+        raise _lib.NewsRecHIPError("softmax64: x must be f32")
+    rows, width = x.shape
+    if width % 64:
+        raise _lib.NewsRecHIPError("softmax64: width must be a multiple of 64")
+    if out is None:
+        out = torch.empty((rows, width), dtype=out_dtype or torch.float32, device=dev)
+    _lib.call("nr_softmax64", rows, width // 64, _ptr(x), _rowmajor(x, "x"), _dtype(out, "out"), _ptr(out),
+              _rowmajor(out, "out"), _stream(dev))
+    return out
+
+
+def row_inv_norm(x: torch.Tensor, eps: float = 1e-8, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """1 / max(||x_r||, eps) per row, f32 (cosine_similarity's per-vector clamp)."""
+    dev = _dev(x, out)
+    rows, dim = x.shape
+    if out is None:
+        out = torch.empty(rows, dtype=torch.float32, device=dev)
+    _lib.call("nr_row_inv_norm", _dtype(x, "x"), rows, dim, _ptr(x), _rowmajor(x, "x"), ctypes.c_float(eps),
+              _ptr(out), _stream(dev))
+    return out
+
+
+def _check_csr(idx: torch.Tensor, off: torch.Tensor, name: str) -> None:
+    if idx.dtype != torch.int32 or not idx.is_contiguous():
+        raise _lib.NewsRecHIPError(f"{name}_idx must be contiguous int32")
+    if off.dtype != torch.int64 or not off.is_contiguous():
+        raise _lib.NewsRecHIPError(f"{name}_off must be contiguous int64")
+
+
+def pool_score(pooler: str, hist_table: torch.Tensor, cand_table: torch.Tensor, cand_inv_norm: torch.Tensor,
+               hist_idx: torch.Tensor, hist_off: torch.Tensor, cand_idx: torch.Tensor, cand_off: torch.Tensor,
+               n_cand: int, want_users: bool = False, scores: Optional[torch.Tensor] = None):
+    """Fused history pooling + cosine scoring; returns (scores[C] f32, users[I, D] f32 or None).
+
+    ``n_cand`` = cand_off[-1] (passed by the caller so no device sync is needed).
+    """
+    dev = _dev(hist_table, cand_table, cand_inv_norm, hist_idx, hist_off, cand_idx, cand_off, scores)
+    _check_csr(hist_idx, hist_off, "hist")
+    _check_csr(cand_idx, cand_off, "cand")
+    if hist_off.numel() != cand_off.numel():
+        raise _lib.NewsRecHIPError("hist_off and cand_off must both have n_imp + 1 entries")
+    if hist_table.dtype != cand_table.dtype:
+        raise _lib.NewsRecHIPError("hist_table and cand_table must share a dtype")
+    if cand_inv_norm.dtype != torch.float32 or cand_inv_norm.numel() < cand_table.shape[0]:
+        raise _lib.NewsRecHIPError("cand_inv_norm must be f32 with one entry per candidate-table row")
+    n_imp = hist_off.numel() - 1
+    dim = cand_table.shape[1]
+    if scores is None:
+        scores = torch.empty(n_cand, dtype=torch.float32, device=dev)
+    users = torch.empty((n_imp, dim), dtype=torch.float32, device=dev) if want_users else None
+    _lib.call("nr_pool_score", POOLERS[pooler], _dtype(cand_table, "cand_table"), dim, _ptr(hist_table),
+              _rowmajor(hist_table, "hist_table"), _ptr(cand_table), _rowmajor(cand_table, "cand_table"),
+              _ptr(cand_inv_norm), _ptr(hist_idx), _ptr(hist_off), _ptr(cand_idx), _ptr(cand_off), n_imp,
+              _ptr(scores), _ptr(users), _stream(dev))
+    return scores, users
+
+
+def dense_rank(scores: torch.Tensor, cand_off: torch.Tensor, check: bool = True) -> torch.Tensor:
+    """Per-impression dense descending ranks (int32), scipy rankdata(-x, 'dense')."""
+    dev = _dev(scores, cand_off)
+    if scores.dtype != torch.float32 or not scores.is_contiguous():
+        raise _lib.NewsRecHIPError("dense_rank: scores must be contiguous f32")
+    ranks = torch.empty(scores.numel(), dtype=torch.int32, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("nr_dense_rank", _ptr(scores), _ptr(cand_off), cand_off.numel() - 1, _ptr(ranks), _ptr(status),
+              _stream(dev))
+    if check and int(status.item()) != 0:
+        raise _lib.NewsRecHIPError("dense_rank: an impression has more than 2048 candidates")
+    return ranks
+
+
+def final_attn_transform(emb: torch.Tensor, w: dict, out: Optional[torch.Tensor] = None,
+                         workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-news FinalAttention table [n, 2*1024] = (x, exp(w)) in emb.dtype.
+
+    ``w`` holds device weights in emb.dtype (W1..W5) and f32 biases (b1..b4).
+    """
+    dev = _dev(emb, out)
+    dt = _dtype(emb, "emb")
+    n, dim = emb.shape
+    if dim != 1024:
+        raise _lib.NewsRecHIPError("final_attn_transform: dim must be 1024")
+    if out is None:
+        out = torch.empty((n, 2 * dim), dtype=emb.dtype, device=dev)
+    need = _lib.load().nr_final_attn_workspace_bytes(dt, n)
+    if workspace is None or workspace.numel() * workspace.element_size() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=dev)
+    for k in ("W1", "W2", "W3", "W4", "W5"):
+        if w[k].dtype != emb.dtype or not w[k].is_contiguous():
+            raise _lib.NewsRecHIPError(f"final_attn_transform: {k} must be contiguous {emb.dtype}")
+    _lib.call("nr_final_attn_transform", dt, n, _ptr(emb), _rowmajor(emb, "emb"), _ptr(w["W1"]), _ptr(w["b1"]),
+              _ptr(w["W2"]), _ptr(w["b2"]), _ptr(w["W3"]), _ptr(w["b3"]), _ptr(w["W4"]), _ptr(w["b4"]),
+              _ptr(w["W5"]), _ptr(out), _ptr(workspace), need, _stream(dev))
+    return out
+
+
+def latent_transform(emb: torch.Tensor, w: dict, out: Optional[torch.Tensor] = None,
+                     workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-news LatentAttention table [n, 1024] (the pre-pooling hiddens)."""
+    dev = _dev(emb, out)
+    dt = _dtype(emb, "emb")
+    n, dim = emb.shape
+    if dim != 1024:
+        raise _lib.NewsRecHIPError("latent_transform: dim must be 1024")
+    if out is None:
+        out = torch.empty((n, dim), dtype=emb.dtype, device=dev)
+    need = _lib.load().nr_latent_workspace_bytes(dt, n)
+    if workspace is None or workspace.numel() * workspace.element_size() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=dev)
+    for k in ("A", "Bt", "W1i", "W2"):
+        if w[k].dtype != emb.dtype or not w[k].is_contiguous():
+            raise _lib.NewsRecHIPError(f"latent_transform: {k} must be contiguous {emb.dtype}")
+    _lib.call("nr_latent_transform", dt, n, _ptr(emb), _rowmajor(emb, "emb"), _ptr(w["lnq_g"]), _ptr(w["lnq_b"]),
+              _ptr(w["A"]), _ptr(w["Bt"]), _ptr(w["lnf_g"]), _ptr(w["lnf_b"]), _ptr(w["W1i"]), _ptr(w["b1i"]),
+              _ptr(w["W2"]), _ptr(w["b2"]), _ptr(out), _ptr(workspace), need, _stream(dev))
+    return out

@@ -1,0 +1,106 @@
+"""Seeded MIND-shaped synthetic impressions.
+
+No MIND data exists offline.  The generator follows the survey's recipe:
+``rng = np.random.default_rng(seed)``; history length ``clip(geometric(1/33),
+1, 600)``; candidates ``clip(geometric(1/37), 2, 300)``; uniform news ids
+(duplicates allowed); labels ``random < 0.04`` with the first candidate forced
+to 1 and the last to 0 (so every impression's AUC is defined).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+# (n_news, n_impressions) of the public MIND splits (generator assumptions)
+SHAPES = {
+    "mind_small_dev": (42_416, 73_152),
+    "mind_large_dev": (72_023, 376_471),
+    "mind_large_test": (120_961, 2_370_727),
+}
+
+
+@dataclass
+class Impressions:
+    n_news: int
+    hist_idx: np.ndarray   # int32 [H]
+    hist_len: np.ndarray   # int32 [I]
+    cand_idx: np.ndarray   # int32 [C]
+    cand_len: np.ndarray   # int32 [I]
+    labels: np.ndarray     # uint8 [C]
+
+    @property
+    def n_imp(self) -> int:
+        return int(self.cand_len.shape[0])
+
+    @property
+    def n_cand(self) -> int:
+        return int(self.cand_idx.shape[0])
+
+    @property
+    def n_hist(self) -> int:
+        return int(self.hist_idx.shape[0])
+
+    def hist_off(self) -> np.ndarray:
+        o = np.zeros(self.n_imp + 1, dtype=np.int64)
+        np.cumsum(self.hist_len, out=o[1:])
+        return o
+
+    def cand_off(self) -> np.ndarray:
+        o = np.zeros(self.n_imp + 1, dtype=np.int64)
+        np.cumsum(self.cand_len, out=o[1:])
+        return o
+
+    def slice(self, start: int, stop: int) -> "Impressions":
+        ho, co = self.hist_off(), self.cand_off()
+        return Impressions(self.n_news, self.hist_idx[ho[start]:ho[stop]], self.hist_len[start:stop],
+                           self.cand_idx[co[start]:co[stop]], self.cand_len[start:stop],
+                           self.labels[co[start]:co[stop]])
+
+    def grouped_labels(self) -> list:
+        co = self.cand_off()
+        return [self.labels[co[i]:co[i + 1]].astype(np.int64) for i in range(self.n_imp)]
+
+
+def mind_impressions(n_news: int, n_imp: int, seed: int = 1234, mean_hist: float = 33.0,
+                     mean_cand: float = 37.0, max_hist: int = 600, max_cand: int = 300,
+                     min_cand: int = 2, zipf: Optional[float] = None) -> Impressions:
+    rng = np.random.default_rng(seed)
+    hist_len = np.clip(rng.geometric(1.0 / mean_hist, n_imp), 1, max_hist).astype(np.int32)
+    cand_len = np.clip(rng.geometric(1.0 / mean_cand, n_imp), min_cand, max_cand).astype(np.int32)
+    H, C = int(hist_len.sum()), int(cand_len.sum())
+    if zipf is None:
+        hist_idx = rng.integers(0, n_news, H, dtype=np.int32)
+        cand_idx = rng.integers(0, n_news, C, dtype=np.int32)
+    else:  # popularity-skewed ids for cache-sensitivity runs
+        perm = rng.permutation(n_news).astype(np.int32)
+        hist_idx = perm[(rng.zipf(zipf, H) - 1) % n_news]
+        cand_idx = perm[(rng.zipf(zipf, C) - 1) % n_news]
+    labels = (rng.random(C) < 0.04).astype(np.uint8)
+    co = np.zeros(n_imp + 1, dtype=np.int64)
+    np.cumsum(cand_len, out=co[1:])
+    labels[co[:-1]] = 1
+    labels[co[1:] - 1] = 0
+    return Impressions(n_news, hist_idx, hist_len, cand_idx, cand_len, labels)
+
+
+def mind_shaped(name: str = "mind_large_dev", seed: int = 1234, **kw) -> Impressions:
+    n_news, n_imp = SHAPES[name]
+    return mind_impressions(n_news, n_imp, seed=seed, **kw)
+
+
+def to_behaviors(imps: Impressions, with_labels: bool = True, news_prefix: str = "N"):
+    """Render as MIND behaviours strings (History, Impressions) for parser tests."""
+    ho, co = imps.hist_off(), imps.cand_off()
+    hist, impr = [], []
+    for i in range(imps.n_imp):
+        h = imps.hist_idx[ho[i]:ho[i + 1]]
+        hist.append(" ".join(f"{news_prefix}{x}" for x in h) if len(h) else None)
+        c = imps.cand_idx[co[i]:co[i + 1]]
+        lab = imps.labels[co[i]:co[i + 1]]
+        if with_labels:
+            impr.append(" ".join(f"{news_prefix}{x}-{int(y)}" for x, y in zip(c, lab)))
+        else:
+            impr.append(" ".join(f"{news_prefix}{x}" for x in c))
+    return hist, impr

@@ -1,0 +1,123 @@
+"""ORACLE (test infrastructure only): reference pooling + scoring on the CPU.
+
+Restates, in PyTorch fp32 on the CPU, exactly the reference's data flow:
+  get_final_attention_eval  data_model_helper.py:112-131  batches of impressions,
+      each padded to its longest history (pad_to_maxlen data_utils.py:723-750),
+      rows gathered and multiplied by the mask (data_utils.py:784-791), the
+      pooler run on every padded slot (get_model_eval modeling_utils.py:402-417)
+  FinalAttention.forward    modeling_utils.py:195-228
+  LatentAttentionModel.forward  latent_attention.py:134-171 (K/V rebuilt per
+      batch row, SDPA, GEGLU FFN, masked mean, F.normalize)
+  get_cos_sim_scores        data_model_helper.py:174-239 (per-impression loop)
+  get_final_second_attention_score  data_model_helper.py:416-443
+  rank_group_preds          data_utils.py:414-415 (scipy rankdata dense)
+The batch size is fixed (128) because the reference's OOM probe
+(batch_size_finder.py:103-149) only terminates on a GPU.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from scipy.stats import rankdata
+
+
+def final_attention_forward(sd: dict, emb: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """modeling_utils.py:218-228 (dropout inactive)."""
+    x = F.relu(F.linear(emb, sd["linear1.weight"], sd["linear1.bias"]))
+    x = F.relu(F.linear(x, sd["linear2.weight"], sd["linear2.bias"]))
+    x = F.linear(x, sd["linear3.weight"], sd["linear3.bias"])
+    w = F.relu(F.linear(x, sd["linear4.weight"], sd["linear4.bias"]))
+    w = F.linear(w, sd["linear5.weight"])
+    w = torch.exp(w) * mask.unsqueeze(-1)
+    w = w / (w.sum(dim=1, keepdim=True) + 1e-10)
+    return (x * w).sum(dim=1)
+
+
+def latent_hiddens(sd: dict, emb: torch.Tensor, heads: int = 8) -> torch.Tensor:
+    """Per-item hiddens of latent_attention.py:157-163 for emb [b, n, d]."""
+    p = "cross_attend_blocks.0."
+    q_ = "cross_attend_blocks.1."
+    b = emb.shape[0]
+    d = emb.shape[-1]
+    lat = sd["latents"].unsqueeze(0).expand(b, -1, -1)                   # repeat b n d
+    xq = F.layer_norm(emb, (d,), sd[p + "norm.weight"], sd[p + "norm.bias"], 1e-5)
+    ctx = F.layer_norm(lat, (d,), sd[p + "norm_context.weight"], sd[p + "norm_context.bias"], 1e-5)
+    q = F.linear(xq, sd[p + "fn.to_q.weight"])
+    k, v = F.linear(ctx, sd[p + "fn.to_kv.weight"]).chunk(2, dim=-1)
+
+    def split(t):  # "b n (h d) -> (b h) n d"
+        bb, nn, hd = t.shape
+        return t.reshape(bb, nn, heads, hd // heads).permute(0, 2, 1, 3).reshape(bb * heads, nn, hd // heads)
+
+    q, k, v = split(q), split(k), split(v)
+    o = F.scaled_dot_product_attention(q, k, v)
+    bh, nn, dh = o.shape
+    o = o.reshape(b, heads, nn, dh).permute(0, 2, 1, 3).reshape(b, nn, heads * dh)
+    h = F.linear(o, sd[p + "fn.to_out.weight"]) + emb
+    z = F.layer_norm(h, (d,), sd[q_ + "norm.weight"], sd[q_ + "norm.bias"], 1e-5)
+    z = F.linear(z, sd[q_ + "fn.net.0.weight"], sd[q_ + "fn.net.0.bias"])
+    a, g = z.chunk(2, dim=-1)
+    z = a * F.gelu(g)
+    return F.linear(z, sd[q_ + "fn.net.2.weight"], sd[q_ + "fn.net.2.bias"]) + h
+
+
+def latent_attention_forward(sd: dict, emb: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    h = latent_hiddens(sd, emb)
+    s = torch.sum(h * mask.unsqueeze(-1).float(), dim=1)
+    d = mask.sum(dim=1, keepdim=True).float()
+    return F.normalize(s / d, p=2, dim=-1)
+
+
+def group(items: np.ndarray, counts: np.ndarray, func=lambda x: x):
+    cs = np.concatenate([[0], np.cumsum(counts)])
+    return np.array([func(items[cs[i]:cs[i + 1]]) for i in range(len(counts))], dtype=object)
+
+
+def pooled_history(pooler: str, sd: dict, hist_idx: np.ndarray, hist_len: np.ndarray, table: torch.Tensor,
+                   batch_size: int = 128) -> torch.Tensor:
+    """get_final_attention_eval: padded batches through the pooler."""
+    fwd = final_attention_forward if pooler == "final" else latent_attention_forward
+    groups = group(np.asarray(hist_idx), np.asarray(hist_len))
+    out = []
+    with torch.no_grad():
+        for s in range(0, len(groups), batch_size):
+            chunk = groups[s:s + batch_size]
+            width = max(len(g) for g in chunk)
+            idx = np.zeros((len(chunk), width), dtype=np.int32)
+            mask = np.zeros((len(chunk), width), dtype=np.int32)
+            for r, g in enumerate(chunk):
+                idx[r, :len(g)] = g
+                mask[r, :len(g)] = 1
+            m = torch.tensor(mask)
+            e = table[torch.tensor(idx)] * m.unsqueeze(-1)
+            out.append(fwd(sd, e, m))
+    return torch.cat(out)
+
+
+def cos_sim_scores(pooler: str, sd: dict, hist_idx, hist_len, cand_idx, cand_len, table: torch.Tensor,
+                   batch_size: int = 128, return_users: bool = False):
+    """get_cos_sim_scores: pooled users, then per-impression cosine."""
+    users = pooled_history(pooler, sd, hist_idx, hist_len, table, batch_size)
+    res = []
+    with torch.no_grad():
+        for i, sub in enumerate(group(np.asarray(cand_idx), np.asarray(cand_len))):
+            res.append(F.cosine_similarity(users[i], table[torch.as_tensor(sub, dtype=torch.long)]))
+    scores = torch.cat(res) if res else torch.zeros(0)
+    return (scores, users) if return_users else scores
+
+
+def dense_ranks(scores: np.ndarray, counts: np.ndarray):
+    """rank_group_preds: rankdata(-x, 'dense') per impression."""
+    return group(np.asarray(scores), np.asarray(counts), lambda x: rankdata(-x, method="dense"))
+
+
+def final_second_attention_score(pooler: str, sd: dict, hist_idx, hist_len, cand_idx, cand_len, history_bool,
+                                 table: torch.Tensor, batch_size: int = 128) -> dict:
+    hb = np.asarray(history_bool, dtype=bool)
+    cl = np.asarray(cand_len)
+    scores = cos_sim_scores(pooler, sd, hist_idx, hist_len, np.asarray(cand_idx)[np.repeat(hb, cl)], cl[hb],
+                            table, batch_size).numpy()
+    return {"scores": scores, "grouped_scores": dense_ranks(scores, cl)}
