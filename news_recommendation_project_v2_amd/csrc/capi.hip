@@ -19,9 +19,10 @@ void clear_error() { g_err[0] = 0; }
 
 static int esize(int dtype) { return dtype == NR_F32 ? 4 : 2; }
 
-// Rows per chunk of the transforms: bounds the workspace at
-// 2 x 65536 x 4096 x 4 B = 2 GiB (f32) while keeping every GEMM >= 512 M-tiles.
-constexpr int64_t kChunk = 65536;
+// Rows per chunk of the transforms: one chunk covers every MIND split's news
+// table (<= 161k), so each GEMM runs once over all rows; the workspace stays
+// bounded (f32 FinalAttention: 2 x 262144 x 4096 x 4 B = 8 GiB of 288 GB).
+constexpr int64_t kChunk = 262144;
 
 }  // namespace nr
 

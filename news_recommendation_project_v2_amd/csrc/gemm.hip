@@ -17,6 +17,8 @@
 // the MFMAs of tile k, one barrier per K tile.
 #include "nr_common.h"
 
+#include <stdlib.h>
+
 namespace nr {
 
 constexpr int GBM = 128, GBN = 128;
@@ -200,6 +202,222 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(int64_t M, int64_t N, int6
   gemm_epilogue<EPI, TO>(acc, M, m0 + wm * 64, n0 + wn * 64, lane, bias, R, ldr, C, ldc);
 }
 
+// ---------------------------------------------------------------------------
+// bf16, 256x256 block tile, 512 threads = 8 waves (2 along M x 4 along N),
+// each wave 128x64 = 4x2 accumulators of 32x32 (128 acc VGPRs).  K tiles of
+// 64 are staged global -> LDS directly with global_load_lds_dwordx4 (no VGPR
+// round trip) into a 2-stage ring (2 x 64 KiB); the prefetch of tile k+1 is in
+// flight while the MFMAs of tile k run, one barrier per K tile.  LDS image of
+// an operand stage: row r (0..255) = 8 chunks of 16 B, chunk c stored at
+// position c ^ ((r >> 1) & 7): each 16-lane ds_read_b128 group then hits 16
+// distinct 16-B bank slots (T2 swizzle, applied on the glds SOURCE address
+// because the DMA writes LDS lane-linearly).
+constexpr int G2BM = 256, G2BN = 256;
+constexpr int G2_STAGE = (G2BM + G2BN) * 128;  // bytes per stage (A + B, 128-B row slices) = 64 KiB
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void g_void;
+
+template <typename TI, int EPI, typename TO>
+__global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, int64_t K,
+                                                             const TI* __restrict__ A, int64_t lda,
+                                                             const TI* __restrict__ W, int64_t ldw,
+                                                             const float* __restrict__ bias, const TO* R,
+                                                             int64_t ldr, TO* C, int64_t ldc) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int64_t n0 = (int64_t)blockIdx.x * G2BN;
+  const int64_t m0 = (int64_t)blockIdx.y * G2BM;
+
+  // glds source pointers: wave issues 4 A + 4 B instructions per K tile, each
+  // filling 8 rows x 128 B; lane l fills (row R0 + l/8, LDS chunk l%8).
+  constexpr int BK = 128 / (int)sizeof(TI), CE = 16 / (int)sizeof(TI);
+  const TI* asrc[4];
+  const TI* bsrc[4];
+  int ldsoff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r0 = (wave * 4 + j) * 8;
+    const int row = r0 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    const int64_t ar = min(m0 + row, M - 1);
+    asrc[j] = A + ar * lda + chunk * CE;
+    bsrc[j] = W + (n0 + row) * ldw + chunk * CE;
+    ldsoff[j] = r0 * 128;
+  }
+  auto issue = [&](int stage, int64_t kt) {
+    unsigned char* sa = smem + stage * G2_STAGE;
+    unsigned char* sb = sa + G2BM * 128;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __builtin_amdgcn_global_load_lds((g_void*)(asrc[j] + kt * BK), (lds_void*)(sa + ldsoff[j]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((g_void*)(bsrc[j] + kt * BK), (lds_void*)(sb + ldsoff[j]), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+  int aoff[4], boff[2], asw[4], bsw[2];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int row = wm * 128 + mi * 32 + fr;
+    aoff[mi] = row * 128;
+    asw[mi] = (row >> 1) & 7;
+  }
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const int row = wn * 64 + ni * 32 + fr;
+    boff[ni] = G2BM * 128 + row * 128;
+    bsw[ni] = (row >> 1) & 7;
+  }
+
+  auto compute = [&](int stage) {
+    const unsigned char* s = smem + stage * G2_STAGE;
+    if constexpr (sizeof(TI) == 2) {
+      // 32x32x16 bf16: lane (r, h) holds k = 16ks + 8h + j (chunk 2ks + h) of row r
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int c = 2 * ks + fh;
+        bf16x8 af[4], bfr[2];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) af[mi] = *reinterpret_cast<const bf16x8*>(s + aoff[mi] + ((c ^ asw[mi]) << 4));
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) bfr[ni] = *reinterpret_cast<const bf16x8*>(s + boff[ni] + ((c ^ bsw[ni]) << 4));
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
+      }
+    } else {
+      // 32x32x2 f32: lane half h covers k = 16h + 4q + t (chunk 4h + q), A and W alike
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 4 * fh + q;
+        f32x4 af[4], bfr[2];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) af[mi] = *reinterpret_cast<const f32x4*>(s + aoff[mi] + ((c ^ asw[mi]) << 4));
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) bfr[ni] = *reinterpret_cast<const f32x4*>(s + boff[ni] + ((c ^ bsw[ni]) << 4));
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi][t], bfr[ni][t], acc[mi][ni], 0, 0, 0);
+      }
+    }
+  };
+
+  const int64_t nk = K / BK;
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) issue((int)((kt + 1) & 1), kt + 1);
+    compute((int)(kt & 1));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // Epilogue, staged through LDS so global stores are whole 16-byte row
+  // segments (the 32x32 C/D map would give 2-4-byte scattered stores).  Two
+  // passes of 64 rows per wave; bias and activation are applied in registers,
+  // the f32 results parked in the wave's private 16 KiB LDS slab
+  // ([64 rows][COLS] f32), then read back row-wise, residual added, stored.
+  constexpr int COLS = (EPI == NR_EPI_GEGLU) ? 32 : 64;  // output columns per wave
+  constexpr int VEC = 16 / (int)sizeof(TO);               // elements per 16-B store
+  constexpr int LPR = COLS / VEC;                          // lanes per output row
+  constexpr int RPI = 64 / LPR;                            // rows per wave instruction
+  const int cl = lane & 31, rh = 4 * (lane >> 5);
+  float* slab = reinterpret_cast<float*>(smem + wave * 16384);
+  const int64_t wcol = n0 + wn * 64;
+  const int64_t ocol0 = (EPI == NR_EPI_GEGLU) ? wcol / 2 : wcol;
+  float ba = 0.f, bg = 0.f;
+  if (bias) { ba = bias[wcol + cl]; bg = bias[wcol + 32 + cl]; }
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int mi = 2 * pass + h;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int lr = 32 * h + (reg & 3) + 8 * (reg >> 2) + rh;
+        if constexpr (EPI == NR_EPI_GEGLU) {
+          slab[lr * COLS + cl] = (acc[mi][0][reg] + ba) * gelu_erf(acc[mi][1][reg] + bg);
+        } else {
+          float v0 = acc[mi][0][reg] + ba, v1 = acc[mi][1][reg] + bg;
+          if constexpr (EPI == NR_EPI_RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
+          if constexpr (EPI == NR_EPI_EXP) { v0 = expf(v0); v1 = expf(v1); }
+          slab[lr * COLS + cl] = v0;
+          slab[lr * COLS + 32 + cl] = v1;
+        }
+      }
+    }
+    __syncthreads();
+    const int rr = lane / LPR, cc = (lane % LPR) * VEC;
+#pragma unroll
+    for (int it = 0; it < 64 / RPI; ++it) {
+      const int lr = it * RPI + rr;
+      const int64_t row = m0 + wm * 128 + pass * 64 + lr;
+      float v[VEC];
+#pragma unroll
+      for (int q = 0; q < VEC; q += 4) {
+        const float4 f = *reinterpret_cast<const float4*>(slab + lr * COLS + cc + q);
+        v[q] = f.x; v[q + 1] = f.y; v[q + 2] = f.z; v[q + 3] = f.w;
+      }
+      if (row < M) {
+        if constexpr (EPI == NR_EPI_RESADD) {
+          const uint4 rv = *reinterpret_cast<const uint4*>(R + row * ldr + ocol0 + cc);
+          if constexpr (sizeof(TO) == 4) {
+            v[0] += __uint_as_float(rv.x); v[1] += __uint_as_float(rv.y);
+            v[2] += __uint_as_float(rv.z); v[3] += __uint_as_float(rv.w);
+          } else {
+            const uint32_t w4[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { v[2 * q] += bf16_lo(w4[q]); v[2 * q + 1] += bf16_hi(w4[q]); }
+          }
+        }
+        TO o[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) o[q] = to_out<TO>(v[q]);
+        *reinterpret_cast<uint4*>(C + row * ldc + ocol0 + cc) = *reinterpret_cast<const uint4*>(o);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <typename TI, typename TO>
+static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                          const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
+                          void* C, int64_t ldc, hipStream_t s) {
+  dim3 grid((unsigned)(N / G2BN), (unsigned)((M + G2BM - 1) / G2BM));
+  const TI* a = (const TI*)A;
+  const TI* w = (const TI*)W;
+  const TO* r = (const TO*)R;
+  TO* c = (TO*)C;
+  switch (epi) {
+    case NR_EPI_NONE: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_NONE, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    case NR_EPI_RELU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_RELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    case NR_EPI_EXP: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_EXP, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    case NR_EPI_GEGLU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_GEGLU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    case NR_EPI_RESADD: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_RESADD, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
+  }
+  NR_CHECK_LAUNCH("nr_gemm");
+  return NR_OK;
+}
+
 template <typename TI, typename TO>
 static int launch_gemm_t(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                          const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
@@ -242,9 +460,24 @@ int gemm_dispatch(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, in
   const int64_t ncols = epi == NR_EPI_GEGLU ? N / 2 : N;
   NR_CHECK_ARG(ldc >= ncols, "nr_gemm: ldc too small");
   NR_CHECK_ARG((M + GBM - 1) / GBM <= 65535, "nr_gemm: M too large (> 8.3M rows)");
+  // 256x256 glds kernel when the shape allows (every pooler GEMM); the
+  // 128x128 register-staged kernel covers N % 256 != 0 and unaligned outputs.
+  static const bool force_small = getenv("NR_GEMM_SMALL_TILE") != nullptr;  // A/B switch for profiling
+  const int64_t vo = dtype_out == NR_F32 ? 4 : 8;  // the LDS-staged epilogue stores 16 B per lane
+  const bool aligned_out = ((uintptr_t)C & 15) == 0 && ldc % vo == 0 &&
+                           (epi != NR_EPI_RESADD || (((uintptr_t)R & 15) == 0 && ldr % vo == 0));
+  const bool big = (N % G2BN == 0) && aligned_out && !force_small;
   if (dtype_in == NR_F32) {
+    if (big) {
+      if (dtype_out == NR_F32) return launch_gemm256<float, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
+      return launch_gemm256<float, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
+    }
     if (dtype_out == NR_F32) return launch_gemm_t<float, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
     return launch_gemm_t<float, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
+  }
+  if (big) {
+    if (dtype_out == NR_F32) return launch_gemm256<__bf16, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
+    return launch_gemm256<__bf16, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
   }
   if (dtype_out == NR_F32) return launch_gemm_t<__bf16, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
   return launch_gemm_t<__bf16, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);

@@ -149,13 +149,24 @@ def pool_score(pooler: str, hist_table: torch.Tensor, cand_table: torch.Tensor, 
         raise _lib.NewsRecHIPError("cand_inv_norm must be f32 with one entry per candidate-table row")
     n_imp = hist_off.numel() - 1
     dim = cand_table.shape[1]
+    # empty CSR arrays have no storage; the kernel never reads them (offsets are
+    # all equal) but the C-ABI rejects null pointers, so hand it a 1-slot dummy
+    one = None
+    if hist_idx.numel() == 0 or cand_idx.numel() == 0 or n_cand == 0:
+        one = torch.zeros(1, dtype=torch.int32, device=dev)
+    if hist_idx.numel() == 0:
+        hist_idx = one
+    if cand_idx.numel() == 0:
+        cand_idx = one
     if scores is None:
         scores = torch.empty(n_cand, dtype=torch.float32, device=dev)
+    # zero-element tensors report data_ptr() == 0: give the kernel a real (unread) slot
+    scores_buf = scores if scores.numel() > 0 else torch.empty(1, dtype=torch.float32, device=dev)
     users = torch.empty((n_imp, dim), dtype=torch.float32, device=dev) if want_users else None
     _lib.call("nr_pool_score", POOLERS[pooler], _dtype(cand_table, "cand_table"), dim, _ptr(hist_table),
               _rowmajor(hist_table, "hist_table"), _ptr(cand_table), _rowmajor(cand_table, "cand_table"),
               _ptr(cand_inv_norm), _ptr(hist_idx), _ptr(hist_off), _ptr(cand_idx), _ptr(cand_off), n_imp,
-              _ptr(scores), _ptr(users), _stream(dev))
+              _ptr(scores_buf), _ptr(users) if users is not None and users.numel() else None, _stream(dev))
     return scores, users
 
 
