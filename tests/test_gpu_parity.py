@@ -267,3 +267,23 @@ def test_full_size_mind_large_properties(gpu_device):
         e = cand[torch.tensor(imps.cand_idx[co[i]:co[i + 1]], dtype=torch.long, device=gpu_device)].double()
         ref = (e @ u) / u.norm() / e.norm(dim=1).clamp_min(1e-8)
         np.testing.assert_allclose(s[co[i]:co[i + 1]], ref.cpu().numpy(), rtol=0, atol=2e-5)
+
+
+def test_eval_script_synthetic_end_to_end(gpu_device, tmp_path, monkeypatch):
+    """scripts/eval.py runs (pipeline -> scores -> ranks -> metrics -> jsonl)."""
+    import json
+    import runpy
+    import sys
+    from pathlib import Path
+    script = Path(__file__).resolve().parents[1] / "scripts" / "eval.py"
+    for pooler in ("final", "latent"):
+        monkeypatch.setattr(sys, "argv", ["eval.py", "--synthetic", "--num-impressions", "300", "--pooler", pooler,
+                                          "--log-dir", str(tmp_path), "--ckpt", str(tmp_path / "none.pt")])
+        runpy.run_path(str(script), run_name="__main__")
+    lines = (tmp_path / "final_scores.jsonl").read_text().splitlines()
+    assert len(lines) == 2
+    for ln in lines:
+        rec = json.loads(ln)
+        for k in ("train_scores", "val_scores"):
+            s = rec[k]
+            assert s["num_samples"] == 300 and 0.0 <= s["auc"] <= 1.0 and 0.0 < s["mrr"] <= 1.0
