@@ -51,6 +51,7 @@ extern "C" {
                            C[:, j] = (a_j + ba_j) * gelu_erf(g_j + bg_j);
                            C has N/2 columns                               */
 #define NR_EPI_RESADD 4 /* C = acc + bias + R                               */
+#define NR_EPI_GELU 5   /* C = gelu_erf(acc + bias)                         */
 
 /* Library version (major*100 + minor). */
 int nr_version(void);
@@ -171,6 +172,28 @@ int nr_latent_transform(int dtype, int64_t n, const void* emb, int64_t emb_ld,
                         const float* lnf_g, const float* lnf_b, const void* W1i,
                         const float* b1i, const void* W2, const float* b2, void* table,
                         void* ws, int64_t ws_bytes, void* stream);
+
+/*
+ * Title encoder pieces (XLM-R-large / e5-large-instruct), packed varlen tokens.
+ * Replaces transformers XLMRobertaEmbeddings.forward (word + token_type +
+ * position embeddings, LayerNorm) and the self-attention core
+ * softmax(q kᵀ / sqrt(64)) v with the key-padding mask, as run by
+ * get_text_embed_eval (modeling_utils.py:282-300).  The layer GEMMs use
+ * nr_gemm (NR_EPI_RESADD / NR_EPI_GELU), the post-LNs nr_layernorm, and the
+ * masked mean + F.normalize (average_pool, modeling_utils.py:55-59,
+ * data_model_helper.py:65-78) is nr_pool_score with NR_POOL_LATENT over
+ * consecutive token rows.
+ *
+ * nr_embed_ln: out[t] = LN(word[ids[t]] + type[0] + pos_emb[pos[t]]), dim 1024.
+ * nr_attention_varlen: qkv [T][3072] (q | k | v, 16 heads x 64 per part),
+ *   cu_seqlens int32 [n_seq+1], qblock_off int32 [n_seq+1] = prefix sum of
+ *   ceil(L_i / 32), n_qblocks = qblock_off[n_seq]; ctx [T][1024].
+ */
+int nr_embed_ln(int dtype, int64_t n_tokens, const int32_t* ids, const int32_t* pos, const void* word,
+                const void* pos_emb, const void* type_emb, const float* gamma, const float* beta, float eps,
+                void* out, void* stream);
+int nr_attention_varlen(int dtype, int32_t n_seq, int64_t n_qblocks, const void* qkv,
+                        const int32_t* cu_seqlens, const int32_t* qblock_off, void* ctx, void* stream);
 
 #ifdef __cplusplus
 }

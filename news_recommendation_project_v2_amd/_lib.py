@@ -23,6 +23,7 @@ NR_EPI_RELU = 1
 NR_EPI_EXP = 2
 NR_EPI_GEGLU = 3
 NR_EPI_RESADD = 4
+NR_EPI_GELU = 5
 
 _p = ctypes.c_void_p
 _i = ctypes.c_int
@@ -44,6 +45,8 @@ SIGNATURES = {
     "nr_final_attn_transform": (_i, [_i, _l, _p, _l, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _l, _p]),
     "nr_latent_workspace_bytes": (_l, [_i, _l]),
     "nr_latent_transform": (_i, [_i, _l, _p, _l, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _l, _p]),
+    "nr_embed_ln": (_i, [_i, _l, _p, _p, _p, _p, _p, _p, _p, _f, _p, _p]),
+    "nr_attention_varlen": (_i, [_i, ctypes.c_int32, _l, _p, _p, _p, _p, _p]),
 }
 
 

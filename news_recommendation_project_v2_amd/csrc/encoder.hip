@@ -1,0 +1,271 @@
+// Title encoder (XLM-R-large architecture, e5-large-instruct) on gfx950.
+//
+// Replaces the transformers XLMRobertaModel forward that get_embed_from_model /
+// get_text_embed_eval run per padded batch (modeling_utils.py:282-323) and the
+// average_pool + F.normalize that follow (modeling_utils.py:55-59,
+// data_model_helper.py:65-78).  Post-LN BERT layer:
+//   x   = LN_emb(word[id] + pos[p] + type[0])
+//   per layer:  qkv = x Wqkvᵀ + b ; ctx = softmax(q kᵀ / 8) v  (16 heads x 64)
+//               x = LN1(ctx Woᵀ + bo + x) ; x = LN2(gelu(x W1ᵀ + b1) W2ᵀ + b2 + x)
+// Sequences are packed varlen (no padding): cu_seqlens offsets, attention
+// stays inside a sequence, which equals the reference's key-padding mask
+// ((1 - m) * finfo.min -> exp() == 0).  GEMMs reuse gemm.hip; this file holds
+// the embedding+LN kernel and the MFMA attention kernel.
+#include "nr_common.h"
+
+namespace nr {
+
+// ------------------------------------------------------------------ embeddings
+template <typename TO>
+__global__ __launch_bounds__(256) void embed_ln_kernel(int64_t T, const int32_t* __restrict__ ids,
+                                                       const int32_t* __restrict__ pos,
+                                                       const TO* __restrict__ word, const TO* __restrict__ pemb,
+                                                       const TO* __restrict__ temb, const float* __restrict__ g,
+                                                       const float* __restrict__ b, float eps,
+                                                       TO* __restrict__ out) {
+  constexpr int D = 1024, NJ = D / 256;
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;
+  const TO* wr = word + (int64_t)ids[t] * D;
+  const TO* pr = pemb + (int64_t)pos[t] * D;
+  float v[NJ][4];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = j * 256 + lane * 4 + q;
+      // reference order: (word + type) + position  (XLMRobertaEmbeddings.forward)
+      v[j][q] = ((float)wr[e] + (float)temb[e]) + (float)pr[e];
+      s += v[j][q];
+    }
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float qv = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float d = v[j][q] - mean;
+      qv = fmaf(d, d, qv);
+    }
+  const float rstd = 1.0f / sqrtf(wave_sum(qv) / (float)D + eps);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = j * 256 + lane * 4 + q;
+      out[t * D + e] = (TO)((v[j][q] - mean) * rstd * g[e] + b[e]);
+    }
+}
+
+// ------------------------------------------------------------------ attention
+// One wave per (query block of 32 rows, head); 4 heads per 256-thread block.
+// Sᵀ = K·Qᵀ for a 32-key block lands with the query on the lane and the key
+// in the 16 accumulator registers (+4 per lane half), so the per-query online
+// softmax reduces over registers and one lane^32 exchange, and the same
+// registers are directly the A operand of O = P·V (sum over the key = the
+// accumulator's row index, no LDS round trip).  V fragments come straight from
+// L2 in B-operand order (32 consecutive d of one key row per half-wave).  The
+// output tile (query rows in registers, d on the lane) stores 128-B row
+// segments.  Scale 1/8 is folded into Q exactly (power of two).
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+template <typename T>
+__global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qkv, const int32_t* __restrict__ cu,
+                                                        const int32_t* __restrict__ qoff, int32_t n_seq,
+                                                        T* __restrict__ ctx) {
+  constexpr int D = 1024, LD = 3 * D, HD = 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = blockIdx.y * 4 + wave;     // head
+  const int qb_global = blockIdx.x;        // global query-block index
+  // binary search the sequence owning this query block (qoff: prefix of ceil(L/32))
+  int lo = 0, hi = n_seq;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (qoff[mid] <= qb_global) lo = mid; else hi = mid;
+  }
+  const int seq = lo;
+  const int64_t s0 = cu[seq];
+  const int L = cu[seq + 1] - cu[seq];
+  const int q0 = (qb_global - qoff[seq]) * 32;
+  const int li = lane & 31, lh = lane >> 5;
+
+  // Q fragment (B operand of Sᵀ = K Qᵀ): lane (q = li, half lh)
+  const int qrow = min(q0 + li, L - 1);
+  const T* qp = qkv + (s0 + qrow) * LD + h * HD;
+  const int64_t vcol = 2 * D + h * HD;
+
+  f32x16 o[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;  // per query (lane column li)
+
+  if constexpr (sizeof(T) == 4) {
+    float qf[32];  // d = 32*lh + s
+#pragma unroll
+    for (int s4 = 0; s4 < 8; ++s4) {
+      const float4 f = *reinterpret_cast<const float4*>(qp + 32 * lh + 4 * s4);
+      qf[4 * s4] = f.x * 0.125f; qf[4 * s4 + 1] = f.y * 0.125f; qf[4 * s4 + 2] = f.z * 0.125f; qf[4 * s4 + 3] = f.w * 0.125f;
+    }
+    for (int kb = 0; kb < L; kb += 32) {
+      const int krow = min(kb + li, L - 1);
+      const float* kp = reinterpret_cast<const float*>(qkv) + (s0 + krow) * LD + D + h * HD + 32 * lh;
+      f32x16 sacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+#pragma unroll
+      for (int s4 = 0; s4 < 8; ++s4) {
+        const float4 kf = *reinterpret_cast<const float4*>(kp + 4 * s4);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf.x, qf[4 * s4 + 0], sacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf.y, qf[4 * s4 + 1], sacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf.z, qf[4 * s4 + 2], sacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(kf.w, qf[4 * s4 + 3], sacc, 0, 0, 0);
+      }
+      // mask keys past L, online softmax per query column
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (kb + acc_row(r, lh) >= L) sacc[r] = -INFINITY;
+        mx = fmaxf(mx, sacc[r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = expf(m_run - m_new);
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sacc[r] = expf(sacc[r] - m_new); ps += sacc[r]; }
+      ps += __shfl_xor(ps, 32, 64);
+      l_run = l_run * alpha + ps;
+      m_run = m_new;
+      // rescale O (query rows live in registers: q = acc_row(r, lh)) by alpha[q]
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float a = __shfl(alpha, acc_row(r, lh), 64);
+        o[0][r] *= a;
+        o[1][r] *= a;
+      }
+      // O += P V : step r uses keys acc_row(r, 0/1); A = P regs, B = V rows
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kr = min(kb + acc_row(r, lh), L - 1);
+        const float* vp = reinterpret_cast<const float*>(qkv) + (s0 + kr) * LD + vcol + li;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(sacc[r], vp[32 * dt], o[dt], 0, 0, 0);
+      }
+    }
+  } else {
+    bf16x8 qf[4];  // step s: d = 16s + 8lh + j
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 raw = *reinterpret_cast<const bf16x8*>(qp + 16 * s + 8 * lh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)raw[j] * 0.125f);
+    }
+    for (int kb = 0; kb < L; kb += 32) {
+      const int krow = min(kb + li, L - 1);
+      const T* kp = qkv + (s0 + krow) * LD + D + h * HD;
+      f32x16 sacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kp + 16 * s + 8 * lh);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc, 0, 0, 0);
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (kb + acc_row(r, lh) >= L) sacc[r] = -INFINITY;
+        mx = fmaxf(mx, sacc[r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = expf(m_run - m_new);
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { sacc[r] = expf(sacc[r] - m_new); ps += sacc[r]; }
+      ps += __shfl_xor(ps, 32, 64);
+      l_run = l_run * alpha + ps;
+      m_run = m_new;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float a = __shfl(alpha, acc_row(r, lh), 64);
+        o[0][r] *= a;
+        o[1][r] *= a;
+      }
+      // A operand from the P accumulator (guide §3): k-step s (s = 0, 1) uses
+      // registers 8s..8s+7, element j <-> key 16s + 8(j>>2) + 4lh + (j&3).
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pa;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pa[j] = (__bf16)sacc[8 * s + j];
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          bf16x8 vb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int kr = min(kb + 16 * s + 8 * (j >> 2) + 4 * lh + (j & 3), L - 1);
+            vb[j] = qkv[(s0 + kr) * LD + vcol + 32 * dt + li];
+          }
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, vb, o[dt], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // normalise by l[q] and store rows q0 + acc_row(r, lh), d = 32 dt + li
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int q = acc_row(r, lh);
+    const float inv = 1.0f / __shfl(l_run, q, 64);
+    if (q0 + q < L) {
+      T* op = ctx + (s0 + q0 + q) * D + h * HD + li;
+      op[0] = (T)(o[0][r] * inv);
+      op[32] = (T)(o[1][r] * inv);
+    }
+  }
+}
+
+}  // namespace nr
+
+extern "C" int nr_embed_ln(int dtype, int64_t n_tokens, const int32_t* ids, const int32_t* pos,
+                           const void* word, const void* pos_emb, const void* type_emb, const float* gamma,
+                           const float* beta, float eps, void* out, void* stream) {
+  nr::clear_error();
+  NR_CHECK_ARG(dtype == NR_F32 || dtype == NR_BF16, "nr_embed_ln: bad dtype");
+  if (n_tokens <= 0) return NR_OK;
+  NR_CHECK_ARG(ids && pos && word && pos_emb && type_emb && gamma && beta && out, "nr_embed_ln: null pointer");
+  const dim3 grid((unsigned)((n_tokens + 3) / 4));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == NR_F32)
+    hipLaunchKernelGGL(nr::embed_ln_kernel<float>, grid, dim3(256), 0, s, n_tokens, ids, pos, (const float*)word,
+                       (const float*)pos_emb, (const float*)type_emb, gamma, beta, eps, (float*)out);
+  else
+    hipLaunchKernelGGL(nr::embed_ln_kernel<__bf16>, grid, dim3(256), 0, s, n_tokens, ids, pos, (const __bf16*)word,
+                       (const __bf16*)pos_emb, (const __bf16*)type_emb, gamma, beta, eps, (__bf16*)out);
+  NR_CHECK_LAUNCH("nr_embed_ln");
+  return NR_OK;
+}
+
+extern "C" int nr_attention_varlen(int dtype, int32_t n_seq, int64_t n_qblocks, const void* qkv,
+                                   const int32_t* cu_seqlens, const int32_t* qblock_off, void* ctx, void* stream) {
+  nr::clear_error();
+  NR_CHECK_ARG(dtype == NR_F32 || dtype == NR_BF16, "nr_attention_varlen: bad dtype");
+  if (n_seq <= 0 || n_qblocks <= 0) return NR_OK;
+  NR_CHECK_ARG(qkv && cu_seqlens && qblock_off && ctx, "nr_attention_varlen: null pointer");
+  NR_CHECK_ARG(n_qblocks <= 0x7fffffff, "nr_attention_varlen: too many query blocks");
+  const dim3 grid((unsigned)n_qblocks, 4);  // 4 blocks x 4 waves = 16 heads
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == NR_F32)
+    hipLaunchKernelGGL(nr::attention_kernel<float>, grid, dim3(256), 0, s, (const float*)qkv, cu_seqlens,
+                       qblock_off, n_seq, (float*)ctx);
+  else
+    hipLaunchKernelGGL(nr::attention_kernel<__bf16>, grid, dim3(256), 0, s, (const __bf16*)qkv, cu_seqlens,
+                       qblock_off, n_seq, (__bf16*)ctx);
+  NR_CHECK_LAUNCH("nr_attention_varlen");
+  return NR_OK;
+}

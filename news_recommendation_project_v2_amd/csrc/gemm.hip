@@ -77,6 +77,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], int64_t
             float v = acc[mi][ni][reg] + b;
             if constexpr (EPI == NR_EPI_RELU) v = fmaxf(v, 0.f);
             if constexpr (EPI == NR_EPI_EXP) v = expf(v);
+            if constexpr (EPI == NR_EPI_GELU) v = gelu_erf(v);
             if constexpr (EPI == NR_EPI_RESADD) v += from_out<TO>(R[row * ldr + col]);
             C[row * ldc + col] = to_out<TO>(v);
           }
@@ -358,6 +359,7 @@ __global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, i
           float v0 = acc[mi][0][reg] + ba, v1 = acc[mi][1][reg] + bg;
           if constexpr (EPI == NR_EPI_RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
           if constexpr (EPI == NR_EPI_EXP) { v0 = expf(v0); v1 = expf(v1); }
+          if constexpr (EPI == NR_EPI_GELU) { v0 = gelu_erf(v0); v1 = gelu_erf(v1); }
           slab[lr * COLS + cl] = v0;
           slab[lr * COLS + 32 + cl] = v1;
         }
@@ -412,6 +414,7 @@ static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* 
     case NR_EPI_EXP: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_EXP, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
     case NR_EPI_GEGLU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_GEGLU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
     case NR_EPI_RESADD: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_RESADD, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    case NR_EPI_GELU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_GELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
     default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
   }
   NR_CHECK_LAUNCH("nr_gemm");
@@ -433,6 +436,7 @@ static int launch_gemm_t(int epi, int64_t M, int64_t N, int64_t K, const void* A
     case NR_EPI_EXP: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_EXP, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
     case NR_EPI_GEGLU: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_GEGLU, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
     case NR_EPI_RESADD: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_RESADD, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    case NR_EPI_GELU: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_GELU, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
     default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
   }
   NR_CHECK_LAUNCH("nr_gemm");

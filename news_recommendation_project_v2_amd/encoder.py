@@ -1,0 +1,180 @@
+"""Title encoder on the MI355X path.
+
+Replaces, for the e5-large-instruct / XLM-R-large encoder that
+``get_embeddings`` (data_model_helper.py:45-84) runs through
+``get_embed_from_model`` / ``get_text_embed_eval`` (modeling_utils.py:282-323):
+  * padded batches of tokenised titles, the full HF forward, the D2H copy of
+    every [B, L, 1024] hidden state and ``average_pool`` + ``F.normalize`` on
+    the host,
+with packed varlen token rows on the device (no padding), one embedding+LN
+kernel, per layer a fused QKV GEMM, the MFMA varlen attention kernel, GEMMs
+with residual / GELU epilogues, post-LayerNorms, and the masked mean +
+L2-normalise done by the segmented pool kernel (latent pooler over
+consecutive token rows).  Only the [B, 1024] embeddings leave the device.
+
+Weights use the transformers ``XLMRobertaModel`` state-dict keys
+(``embeddings.*``, ``encoder.layer.{i}.*``; a ``roberta.``/``model.`` prefix is
+stripped), loaded with ``torch.load(weights_only=True)`` or safetensors.
+"""
+from __future__ import annotations
+
+import math
+from pathlib import Path
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import ops
+
+PAD_ID = 1          # XLM-R <pad>; positions start at PAD_ID + 1
+LN_EPS = 1e-5       # XLM-R layer_norm_eps (NOT XLMRobertaConfig's 1e-12 default)
+HIDDEN = 1024
+HEADS = 16
+FFN = 4096
+
+
+def strip_prefix(sd: dict) -> dict:
+    out = {}
+    for k, v in sd.items():
+        for p in ("roberta.", "model.", "xlm_roberta."):
+            if k.startswith(p):
+                k = k[len(p):]
+        out[k] = v
+    return out
+
+
+def positions_for(ids: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    """HF create_position_ids_from_input_ids per packed sequence:
+    pad + cumsum(id != pad) * (id != pad)."""
+    m = (np.asarray(ids) != PAD_ID).astype(np.int64)
+    lens = np.asarray(lens, dtype=np.int64)
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    cs = np.cumsum(m)
+    before = np.where(starts > 0, cs[np.maximum(starts - 1, 0)], 0)  # non-pad count before each sequence
+    return ((cs - np.repeat(before, lens)) * m + PAD_ID).astype(np.int32)
+
+
+class XLMREncoder:
+    def __init__(self, state_dict: dict, dtype: torch.dtype = torch.float32, device=None,
+                 max_tokens: int = 262144):
+        sd = strip_prefix(state_dict)
+        self.dtype = dtype
+        self.device = device or torch.device("cuda")
+        self.max_tokens = max_tokens
+        n = 0
+        while f"encoder.layer.{n}.attention.self.query.weight" in sd:
+            n += 1
+        self.n_layers = n
+        dev, dt = self.device, dtype
+        w = lambda k: sd[k].to(dev, dt).contiguous()
+        f = lambda k: sd[k].to(dev, torch.float32).contiguous()
+        self.word = w("embeddings.word_embeddings.weight")
+        self.pos = w("embeddings.position_embeddings.weight")
+        self.type0 = w("embeddings.token_type_embeddings.weight")[0].contiguous()
+        self.eln = (f("embeddings.LayerNorm.weight"), f("embeddings.LayerNorm.bias"))
+        self.layers = []
+        for i in range(n):
+            p = f"encoder.layer.{i}."
+            a = p + "attention."
+            wqkv = torch.cat([sd[a + "self.query.weight"], sd[a + "self.key.weight"], sd[a + "self.value.weight"]])
+            bqkv = torch.cat([sd[a + "self.query.bias"], sd[a + "self.key.bias"], sd[a + "self.value.bias"]])
+            self.layers.append({
+                "wqkv": wqkv.to(dev, dt).contiguous(), "bqkv": bqkv.to(dev, torch.float32).contiguous(),
+                "wo": w(a + "output.dense.weight"), "bo": f(a + "output.dense.bias"),
+                "ln1": (f(a + "output.LayerNorm.weight"), f(a + "output.LayerNorm.bias")),
+                "w1": w(p + "intermediate.dense.weight"), "b1": f(p + "intermediate.dense.bias"),
+                "w2": w(p + "output.dense.weight"), "b2": f(p + "output.dense.bias"),
+                "ln2": (f(p + "output.LayerNorm.weight"), f(p + "output.LayerNorm.bias")),
+            })
+
+    @classmethod
+    def from_pretrained_dir(cls, path, **kw) -> "XLMREncoder":
+        """Local HF directory (model.safetensors or pytorch_model.bin); no network."""
+        path = Path(path)
+        st = path / "model.safetensors"
+        if st.is_file():
+            from safetensors.torch import load_file
+            sd = load_file(str(st))
+        else:
+            sd = torch.load(path / "pytorch_model.bin", weights_only=True, map_location="cpu")
+        return cls(sd, **kw)
+
+    # ------------------------------------------------------------------ forward
+    def _chunk_forward(self, ids: np.ndarray, lens: np.ndarray) -> torch.Tensor:
+        dev, dt = self.device, self.dtype
+        T = int(lens.sum())
+        ids_d = torch.as_tensor(ids.astype(np.int32)).to(dev)
+        pos_d = torch.as_tensor(positions_for(ids, lens)).to(dev)
+        cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        qb = np.concatenate([[0], np.cumsum((lens + 31) // 32)]).astype(np.int64)
+        cu_i32 = torch.as_tensor(cu.astype(np.int32)).to(dev)
+        qb_i32 = torch.as_tensor(qb.astype(np.int32)).to(dev)
+        x = ops.embed_ln(ids_d, pos_d, self.word, self.pos, self.type0, self.eln[0], self.eln[1], LN_EPS)
+        qkv = torch.empty((T, 3 * HIDDEN), dtype=dt, device=dev)
+        ctx = torch.empty((T, HIDDEN), dtype=dt, device=dev)
+        tmp = torch.empty((T, HIDDEN), dtype=dt, device=dev)
+        ffn = torch.empty((T, FFN), dtype=dt, device=dev)
+        for L in self.layers:
+            ops.gemm(x, L["wqkv"], L["bqkv"], out=qkv)
+            ops.attention_varlen(qkv, cu_i32, qb_i32, int(qb[-1]), out=ctx)
+            ops.gemm(ctx, L["wo"], L["bo"], epilogue="resadd", residual=x, out=tmp)
+            ops.layernorm(tmp, L["ln1"][0], L["ln1"][1], LN_EPS, out=x)
+            ops.gemm(x, L["w1"], L["b1"], epilogue="gelu", out=ffn)
+            ops.gemm(ffn, L["w2"], L["b2"], epilogue="resadd", residual=x, out=tmp)
+            ops.layernorm(tmp, L["ln2"][0], L["ln2"][1], LN_EPS, out=x)
+        # average_pool + F.normalize == latent pooling over each sequence's rows
+        from .modeling_utils import pool_rows
+        return pool_rows("latent", x, torch.as_tensor(cu).to(dev))
+
+    def encode_packed(self, ids: np.ndarray, lens: np.ndarray) -> torch.Tensor:
+        """ids: flat int tokens of all sequences; lens: tokens per sequence.
+        Returns L2-normalised mean-pooled embeddings [B, 1024] f32 on device."""
+        ids = np.asarray(ids)
+        lens = np.asarray(lens, dtype=np.int64)
+        if np.any(lens <= 0):
+            raise ValueError("every sequence needs at least one token")
+        out = []
+        off = np.concatenate([[0], np.cumsum(lens)])
+        s = 0
+        while s < len(lens):
+            e = s + 1
+            while e < len(lens) and off[e + 1] - off[s] <= self.max_tokens:
+                e += 1
+            out.append(self._chunk_forward(ids[off[s]:off[e]], lens[s:e]))
+            s = e
+        return torch.cat(out) if out else torch.zeros((0, HIDDEN), device=self.device)
+
+    def encode_padded(self, input_ids: torch.Tensor, attention_mask: torch.Tensor) -> torch.Tensor:
+        """Tokenizer-style right-padded batch -> embeddings (drops padded slots)."""
+        m = attention_mask.bool().cpu().numpy()
+        ids = input_ids.cpu().numpy()
+        return self.encode_packed(ids[m], m.sum(1))
+
+
+def tokenize(tokenizer, texts: Sequence[str], max_len: int) -> tuple[np.ndarray, np.ndarray]:
+    """Tokenise to packed ids + lengths (eval_collate_fn data_utils.py:471-482
+    without padding: truncation at max_len, special tokens added)."""
+    enc = tokenizer(list(texts), max_length=max_len, truncation=True, padding=False)
+    lens = np.array([len(x) for x in enc["input_ids"]], dtype=np.int64)
+    ids = np.concatenate([np.asarray(x, dtype=np.int32) for x in enc["input_ids"]]) if len(lens) else np.zeros(0, np.int32)
+    return ids, lens
+
+
+def get_embeddings(model_path: str, news_list: Iterable[str], news_text_dict: dict[str, str],
+                   dtype: torch.dtype = torch.float32):
+    """data_model_helper.get_embeddings (data_model_helper.py:45-84) for a LOCAL
+    model directory: returns (query_embeds, passage_embeds) for e5-instruct
+    models (query text = QUERY_INSTRUCTION + text), else passage embeds."""
+    from transformers import AutoTokenizer
+
+    from .config import NEWS_TEXT_MAXLEN, QUERY_INSTRUCTION
+    tok = AutoTokenizer.from_pretrained(model_path)
+    enc = XLMREncoder.from_pretrained_dir(model_path, dtype=dtype)
+    news = list(news_list)
+    passages = [news_text_dict[n] for n in news]
+    p = enc.encode_packed(*tokenize(tok, passages, NEWS_TEXT_MAXLEN)).cpu()
+    if "e5" in str(model_path) and "instruct" in str(model_path):
+        q = enc.encode_packed(*tokenize(tok, [QUERY_INSTRUCTION + t for t in passages], NEWS_TEXT_MAXLEN)).cpu()
+        return q, p
+    return p

@@ -20,6 +20,7 @@ _EPI = {
     "exp": _lib.NR_EPI_EXP,
     "geglu": _lib.NR_EPI_GEGLU,
     "resadd": _lib.NR_EPI_RESADD,
+    "gelu": _lib.NR_EPI_GELU,
 }
 POOLERS = {"final": _lib.NR_POOL_FINAL, "latent": _lib.NR_POOL_LATENT}
 
@@ -228,4 +229,35 @@ def latent_transform(emb: torch.Tensor, w: dict, out: Optional[torch.Tensor] = N
     _lib.call("nr_latent_transform", dt, n, _ptr(emb), _rowmajor(emb, "emb"), _ptr(w["lnq_g"]), _ptr(w["lnq_b"]),
               _ptr(w["A"]), _ptr(w["Bt"]), _ptr(w["lnf_g"]), _ptr(w["lnf_b"]), _ptr(w["W1i"]), _ptr(w["b1i"]),
               _ptr(w["W2"]), _ptr(w["b2"]), _ptr(out), _ptr(workspace), need, _stream(dev))
+    return out
+
+
+def embed_ln(ids: torch.Tensor, pos: torch.Tensor, word: torch.Tensor, pos_emb: torch.Tensor, type_emb: torch.Tensor,
+             gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """LN(word[ids] + type_emb + pos_emb[pos]) for packed token rows (XLM-R embeddings)."""
+    dev = _dev(ids, pos, word, pos_emb, type_emb, gamma, beta, out)
+    if ids.dtype != torch.int32 or pos.dtype != torch.int32:
+        raise _lib.NewsRecHIPError("embed_ln: ids/pos must be int32")
+    if word.shape[1] != 1024:
+        raise _lib.NewsRecHIPError("embed_ln: hidden size must be 1024")
+    n = ids.numel()
+    if out is None:
+        out = torch.empty((n, 1024), dtype=word.dtype, device=dev)
+    _lib.call("nr_embed_ln", _dtype(word, "word"), n, _ptr(ids), _ptr(pos), _ptr(word), _ptr(pos_emb),
+              _ptr(type_emb), _ptr(gamma), _ptr(beta), ctypes.c_float(eps), _ptr(out), _stream(dev))
+    return out
+
+
+def attention_varlen(qkv: torch.Tensor, cu_seqlens: torch.Tensor, qblock_off: torch.Tensor, n_qblocks: int,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """16-head x 64 self-attention per packed sequence: qkv [T, 3072] -> ctx [T, 1024]."""
+    dev = _dev(qkv, cu_seqlens, qblock_off, out)
+    if qkv.shape[1] != 3072 or not qkv.is_contiguous():
+        raise _lib.NewsRecHIPError("attention_varlen: qkv must be contiguous [T, 3072]")
+    if cu_seqlens.dtype != torch.int32 or qblock_off.dtype != torch.int32:
+        raise _lib.NewsRecHIPError("attention_varlen: offsets must be int32")
+    if out is None:
+        out = torch.empty((qkv.shape[0], 1024), dtype=qkv.dtype, device=dev)
+    _lib.call("nr_attention_varlen", _dtype(qkv, "qkv"), cu_seqlens.numel() - 1, n_qblocks, _ptr(qkv),
+              _ptr(cu_seqlens), _ptr(qblock_off), _ptr(out), _stream(dev))
     return out

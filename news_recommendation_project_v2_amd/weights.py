@@ -133,6 +133,34 @@ def latent_attention_state_dict(seed: int = 1234, dim: int = 1024, num_latents: 
     return {k: sd[k] for k in order}
 
 
+def xlmr_state_dict(seed: int = 1234, n_layers: int = 24, vocab: int = 250002, hidden: int = 1024,
+                    ffn: int = 4096, max_pos: int = 514) -> Dict[str, torch.Tensor]:
+    """transformers XLMRobertaModel keys (encoder part; the unused CLS pooler is
+    omitted).  Linear layers use the nn.Linear bound; embeddings U(-0.05, 0.05);
+    LayerNorms gamma = 1 + U(-0.1, 0.1), beta = U(-0.02, 0.02) so they are exercised."""
+    sd: Dict[str, torch.Tensor] = {}
+    e = "embeddings."
+    sd[e + "word_embeddings.weight"] = uniform_tensor(seed, e + "word", (vocab, hidden), 0.05)
+    sd[e + "position_embeddings.weight"] = uniform_tensor(seed, e + "pos", (max_pos, hidden), 0.05)
+    sd[e + "token_type_embeddings.weight"] = uniform_tensor(seed, e + "type", (1, hidden), 0.05)
+
+    def ln(prefix):
+        sd[prefix + "weight"] = 1.0 + uniform_tensor(seed, prefix + "weight", (hidden,), 0.1)
+        sd[prefix + "bias"] = uniform_tensor(seed, prefix + "bias", (hidden,), 0.02)
+
+    ln(e + "LayerNorm.")
+    for i in range(n_layers):
+        p = f"encoder.layer.{i}."
+        for nm in ("query", "key", "value"):
+            sd.update(linear_params(seed, p + f"attention.self.{nm}.", hidden, hidden))
+        sd.update(linear_params(seed, p + "attention.output.dense.", hidden, hidden))
+        ln(p + "attention.output.LayerNorm.")
+        sd.update(linear_params(seed, p + "intermediate.dense.", ffn, hidden))
+        sd.update(linear_params(seed, p + "output.dense.", hidden, ffn))
+        ln(p + "output.LayerNorm.")
+    return sd
+
+
 def news_table(seed: int, n: int, dim: int = 1024, name: str = "news_table") -> torch.Tensor:
     """Synthetic news-embedding table: N(0,1) rows, matching the statistics of
     the LayerNorm-output ``new_embeddings/`` that eval.py loads."""

@@ -147,6 +147,49 @@ def gen_pooler(dmh, model, sd_seed_name, pooler, n_news=512, n_imp=64, extra_unp
                         fs_scores=fs["scores"], fs_ranks_flat=rf.astype(np.int64), fs_ranks_len=rl, **extra)
 
 
+ENC_LENS = [2, 7, 20, 31, 32, 33, 45, 64, 65, 130]
+
+
+def encoder_inputs(vocab: int, seed: int = 99):
+    rng = np.random.default_rng(seed)
+    seqs = []
+    for L in ENC_LENS:
+        mid = rng.integers(5, vocab, L - 2) if L > 2 else np.zeros(0, np.int64)
+        seqs.append(np.concatenate([[0], mid, [2]]).astype(np.int64))
+    return seqs
+
+
+def gen_encoder(mu, n_layers: int, vocab: int = 1000):
+    """transformers 5.15 XLMRobertaModel (third-party, e5-large-instruct's
+    architecture) with deterministic weights, run through the reference's
+    get_text_embed_eval (modeling_utils.py:282-300: average_pool) + F.normalize
+    (data_model_helper.py:65-78)."""
+    import torch.nn.functional as F
+    from transformers import BatchEncoding, XLMRobertaConfig, XLMRobertaModel
+    from news_recommendation_project_v2_amd import weights as W
+    cfg = XLMRobertaConfig(vocab_size=vocab, hidden_size=1024, num_hidden_layers=n_layers, num_attention_heads=16,
+                           intermediate_size=4096, max_position_embeddings=514, layer_norm_eps=1e-5,
+                           type_vocab_size=1, pad_token_id=1, hidden_act="gelu")
+    cfg.architectures = ["XLMRobertaModel"]
+    model = XLMRobertaModel(cfg, add_pooling_layer=False)
+    missing, unexpected = model.load_state_dict(W.xlmr_state_dict(1234, n_layers, vocab), strict=False)
+    assert not unexpected and all("position_ids" in k or "token_type_ids" in k for k in missing), (missing, unexpected)
+    model.eval()
+    seqs = encoder_inputs(vocab)
+    width = max(len(s) for s in seqs)
+    ids = torch.ones((len(seqs), width), dtype=torch.long)
+    mask = torch.zeros((len(seqs), width), dtype=torch.long)
+    for i, s in enumerate(seqs):
+        ids[i, :len(s)] = torch.tensor(s)
+        mask[i, :len(s)] = 1
+    batches = [BatchEncoding({"input_ids": ids[:5], "attention_mask": mask[:5]}),
+               BatchEncoding({"input_ids": ids[5:], "attention_mask": mask[5:]})]
+    with torch.no_grad():
+        emb = F.normalize(mu.get_text_embed_eval(model, batches), p=2, dim=1).numpy()
+    np.savez_compressed(HERE / f"encoder_l{n_layers}.npz", n_layers=n_layers, vocab=vocab, weight_seed=1234,
+                        ids=np.concatenate(seqs).astype(np.int32), lens=np.array(ENC_LENS, np.int64), emb=emb)
+
+
 def main():
     assert REF_SRC.is_dir(), "the reference is only available in the build container"
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
@@ -163,6 +206,8 @@ def main():
     lm.load_state_dict(W.latent_attention_state_dict(1234, ln_random=True))
     lm.eval()
     gen_pooler(dmh, lm, "latent", "latent", extra_unpooled=True)
+    gen_encoder(mu, 2)
+    gen_encoder(mu, 24)
     for p in sorted(HERE.glob("*.npz")):
         print(p.name, p.stat().st_size)
 
