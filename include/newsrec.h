@@ -38,6 +38,7 @@ extern "C" {
 /* element types */
 #define NR_F32 0
 #define NR_BF16 1
+#define NR_F16 2 /* input-only, nr_gather_layernorm (token states are stored fp16) */
 
 /* history poolers */
 #define NR_POOL_FINAL 0  /* FinalAttention additive per-dim softmax pooler */
@@ -87,6 +88,22 @@ int nr_gemm(int dtype_in, int dtype_out, int epilogue, int64_t M, int64_t N, int
 int nr_layernorm(int dtype_in, int dtype_out, int64_t rows, int64_t dim, const void* x,
                  int64_t ldx, const float* gamma, const float* beta, float eps, void* y,
                  int64_t ldy, void* stream);
+
+/*
+ * Gathered LayerNorm chain, f32 out:
+ *   out[i] = LN_{n_ln-1}( ... LN_0(x[row_idx[i]]) ... ),  gammas/betas [n_ln][dim]
+ * (nullable: gamma 1, beta 0), biased variance, f32 math.  row_idx nullable
+ * (identity).  x may be NR_F32, NR_BF16 or NR_F16.
+ * Replaces the token-attention encoder + last_token_pool of
+ * FirstAttentionPoolFunc (modeling_utils.py:498-513 -> MyEncoder
+ * attention.py:197-207, whose layers return g_mlp_layernorm(hidden_states),
+ * attention.py:193, eps 1e-12 :155; last_token_pool modeling_utils.py:37-48):
+ * with row_idx = the last valid token of each sequence only those rows are read.
+ * dim in {256, 512, 1024, 2048}.
+ */
+int nr_gather_layernorm(int dtype_in, int64_t n, int64_t dim, const void* x, int64_t ldx,
+                        const int64_t* row_idx, int n_ln, const float* gammas, const float* betas,
+                        float eps, float* out, int64_t ldo, void* stream);
 
 /*
  * In-place softmax over contiguous groups: x is f32 [rows][groups*64]

@@ -9,7 +9,7 @@ import importlib
 import sys
 
 _PKG = "news_recommendation_project_v2_amd"
-_SUBMODULES = ("config", "data_utils", "modeling_utils", "latent_attention", "data_model_helper", "evaluation",
+_SUBMODULES = ("config", "attention", "data_utils", "modeling_utils", "latent_attention", "data_model_helper", "evaluation",
                "pipeline", "components", "engine", "ops", "synthetic", "weights")
 
 for _name in _SUBMODULES:

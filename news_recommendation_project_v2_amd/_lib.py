@@ -16,6 +16,7 @@ LIB_PATH = Path(__file__).resolve().with_name("libnewsrec_hip.so")
 NR_OK = 0
 NR_F32 = 0
 NR_BF16 = 1
+NR_F16 = 2
 NR_POOL_FINAL = 0
 NR_POOL_LATENT = 1
 NR_EPI_NONE = 0
@@ -37,6 +38,7 @@ SIGNATURES = {
     "nr_last_error": (ctypes.c_char_p, []),
     "nr_gemm": (_i, [_i, _i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p]),
     "nr_layernorm": (_i, [_i, _i, _l, _l, _p, _l, _p, _p, _f, _p, _l, _p]),
+    "nr_gather_layernorm": (_i, [_i, _l, _l, _p, _l, _p, _i, _p, _p, _f, _p, _l, _p]),
     "nr_softmax64": (_i, [_l, _l, _p, _l, _i, _p, _l, _p]),
     "nr_row_inv_norm": (_i, [_i, _l, _l, _p, _l, _f, _p, _p]),
     "nr_pool_score": (_i, [_i, _i, _l, _p, _l, _p, _l, _p, _p, _p, _p, _p, _l, _p, _p, _p]),

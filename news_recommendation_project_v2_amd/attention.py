@@ -1,0 +1,118 @@
+"""Token-attention encoder of the reference (attention.py), MI355X path.
+
+Parameter names and shapes follow the reference modules exactly
+(``MyAttention`` attention.py:28-113, ``GatedMLP`` :116-148, ``MyLayer``
+:151-194, ``MyEncoder`` :197-207), so a checkpoint saved by the reference
+(``encoder.layer.0.attention.qkv_proj.weight`` ...) loads with
+``load_state_dict`` unchanged.
+
+What the forward computes.  ``MyLayer.forward`` runs the attention, the
+dropout, ``attn_layernorm`` and ``g_mlp_layernorm`` on the attention output,
+and then overwrites the result with ``g_mlp_layernorm(hidden_states)``
+(attention.py:193): the layer's output is the LayerNorm (eps 1e-12) of its
+INPUT, and nothing computed before that line reaches it (``g_mlp`` is never
+called; dropout does not touch the returned tensor, so train and eval agree).
+``MyEncoder`` therefore equals a chain of ``g_mlp_layernorm``s, one per layer.
+The HIP path computes exactly that chain (``nr_gather_layernorm``) and skips
+the dead attention — a documented build decision: the
+outputs are identical, only the wasted QKV/SDPA/O-projection work is gone.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import ops
+from ._lib import NewsRecHIPError
+from .config import EMBEDDING_DIM, NUM_HIDDEN_LAYERS, REDUCED_DIM
+
+LN_EPS = 1e-12  # MyLayer layer_norm_eps (attention.py:155)
+
+
+class MyAttention(nn.Module):
+    """Parameter container of attention.py:28-64 (its output is dead, see module doc)."""
+
+    def __init__(self, hidden_size=EMBEDDING_DIM, num_attention_heads=8, pack_qkv=True):
+        super().__init__()
+        if hidden_size % num_attention_heads != 0:
+            raise ValueError(
+                f"The hidden size ({hidden_size}) is not a multiple of the number of attention "
+                f"heads ({num_attention_heads})")
+        self.hidden_size = hidden_size
+        self.num_attention_heads = num_attention_heads
+        self.attention_head_size = hidden_size // num_attention_heads
+        self.all_head_size = self.num_attention_heads * self.attention_head_size
+        self.pack_qkv = pack_qkv
+        if pack_qkv:
+            self.qkv_proj = nn.Linear(hidden_size, self.all_head_size * 3, bias=True)
+        else:
+            self.q_proj = nn.Linear(hidden_size, self.all_head_size, bias=True)
+            self.k_proj = nn.Linear(hidden_size, self.all_head_size, bias=True)
+            self.v_proj = nn.Linear(hidden_size, self.all_head_size, bias=True)
+        self.dropout = nn.Dropout(0)
+        self.o_proj = nn.Linear(hidden_size, hidden_size, bias=True)
+
+
+class GatedMLP(nn.Module):
+    """Parameter container of attention.py:116-133 (never called by MyLayer)."""
+
+    def __init__(self, hidden_size=EMBEDDING_DIM, intermediate_size=3072, hidden_act="gelu",
+                 hidden_dropout_prob=0.1):
+        super().__init__()
+        self.intermediate_size = intermediate_size
+        self.up_gate_proj = nn.Linear(hidden_size, intermediate_size * 2, bias=False)
+        self.down_proj = nn.Linear(intermediate_size, hidden_size, bias=True)
+        self.hidden_dropout = nn.Dropout(hidden_dropout_prob) if hidden_dropout_prob > 0 else None
+
+
+class MyLayer(nn.Module):
+    """attention.py:151-194; output = g_mlp_layernorm(hidden_states)."""
+
+    def __init__(self, hidden_size=REDUCED_DIM, layer_norm_eps=LN_EPS, residual_connection=False,
+                 hidden_dropout_prob=0.1):
+        super().__init__()
+        self.attention = MyAttention(hidden_size=hidden_size)
+        self.g_mlp = GatedMLP(hidden_size=hidden_size, hidden_dropout_prob=hidden_dropout_prob)
+        self.attn_layernorm = nn.LayerNorm(hidden_size, eps=layer_norm_eps)
+        self.g_mlp_layernorm = nn.LayerNorm(hidden_size, eps=layer_norm_eps)
+        self.residual_connection = residual_connection
+        self.hidden_dropout = nn.Dropout(hidden_dropout_prob) if hidden_dropout_prob > 0 else None
+
+    def forward(self, hidden_states: torch.Tensor, attention_mask: torch.Tensor = None) -> torch.Tensor:
+        return MyEncoder.ln_chain([self], hidden_states)
+
+
+class MyEncoder(nn.Module):
+    """attention.py:197-207: a stack of MyLayer (== a chain of g_mlp_layernorms)."""
+
+    def __init__(self, hidden_size=REDUCED_DIM, num_hidden_layers=NUM_HIDDEN_LAYERS):
+        super().__init__()
+        self.layer = nn.ModuleList([MyLayer(hidden_size=hidden_size) for _ in range(num_hidden_layers)])
+
+    def ln_params(self):
+        """(gammas [n_layers, D], betas [n_layers, D], eps) of the g_mlp_layernorm chain."""
+        return self.ln_params_of(list(self.layer))
+
+    @staticmethod
+    def ln_params_of(layers):
+        g = torch.stack([l.g_mlp_layernorm.weight.detach().float() for l in layers]).contiguous()
+        b = torch.stack([l.g_mlp_layernorm.bias.detach().float() for l in layers]).contiguous()
+        eps = {l.g_mlp_layernorm.eps for l in layers}
+        if len(eps) != 1:
+            raise NewsRecHIPError("MyEncoder: layers with different LayerNorm eps are not supported")
+        return g, b, eps.pop()
+
+    @staticmethod
+    def ln_chain(layers, hidden_states: torch.Tensor, row_idx: torch.Tensor = None) -> torch.Tensor:
+        if hidden_states.device.type != "cuda":
+            raise NewsRecHIPError("MyEncoder runs on the MI355X HIP path only (got a CPU tensor)")
+        shape = hidden_states.shape
+        x = hidden_states.reshape(-1, shape[-1])
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        g, b, eps = MyEncoder.ln_params_of(layers)
+        out = ops.gather_layernorm(x, row_idx, g, b, eps)
+        return out if row_idx is not None else out.reshape(shape)
+
+    def forward(self, hidden_states: torch.Tensor, attention_mask: torch.Tensor = None) -> torch.Tensor:
+        return self.ln_chain(list(self.layer), hidden_states)

@@ -2,7 +2,8 @@
 
 Kept: TransformData (45-114), EmbeddingsComponent (117-175),
 SaveEmbeddingComponent (178-223), LoadEmbeddingComponent (226-258),
-FinalAttentionComponent (980-1027, transform only), plus
+TokenEmbeddingsComponent (955-977), FinalAttentionComponent (980-1027,
+transform only), plus
 LatentAttentionComponent — the same scoring with the latent pooler, which the
 reference can only reach through get_latent_attention_model
 (modeling_utils.py:151-155).  Training components and the Azure upload are out
@@ -16,7 +17,7 @@ from typing import Any, Optional
 import numpy as np
 import torch
 
-from .data_model_helper import get_embeddings, get_final_second_attention_score
+from .data_model_helper import apply_token_attn, get_embeddings, get_final_second_attention_score
 from .data_utils import split_impressions_and_history
 from .modeling_utils import get_final_attention_model, get_latent_attention_model
 from .pipeline import PipelineComponent, check_req_keys
@@ -106,6 +107,22 @@ class LoadEmbeddingComponent(PipelineComponent):
         if q.exists():
             context_dict["query_news_embeddings"] = torch.load(q, weights_only=True)
         return context_dict
+
+
+class TokenEmbeddingsComponent(PipelineComponent):
+    """news_embeddings from the sqlite token-state DB through the token-attention
+    model (components.py:955-977): ``apply_token_attn(model_path, db_name, len(news_list))``."""
+
+    required_keys = {"news_list", "db_name"}
+
+    def __init__(self, model_path: Path):
+        self.model_path = model_path
+
+    def transform(self, context_dict):
+        check_req_keys(self.required_keys, context_dict)
+        new = context_dict.copy()
+        new["news_embeddings"] = apply_token_attn(self.model_path, new["db_name"], len(new["news_list"]))
+        return new
 
 
 class FinalAttentionComponent(PipelineComponent):

@@ -18,6 +18,13 @@ __device__ __forceinline__ void load4(const T* p, float (&v)[4]) {
   }
 }
 
+template <>
+__device__ __forceinline__ void load4<_Float16>(const _Float16* p, float (&v)[4]) {
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  const h4 h = *reinterpret_cast<const h4*>(p);
+  v[0] = (float)h[0]; v[1] = (float)h[1]; v[2] = (float)h[2]; v[3] = (float)h[3];
+}
+
 template <typename T>
 __device__ __forceinline__ void store4(T* p, const float (&v)[4]) {
   if constexpr (sizeof(T) == 4) {
@@ -182,7 +189,88 @@ int inv_norm_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64
   return NR_OK;
 }
 
+
+// Gathered chain of LayerNorms: out[i] = LN_{n-1}(...LN_0(x[row_idx[i]])...),
+// f32 math and output.  The token-attention encoder's effective forward
+// (attention.py:174-194 returns g_mlp_layernorm(hidden_states); the attention
+// branch is dead) followed by last_token_pool (modeling_utils.py:37-48) is one
+// such LN of the last valid token row, so only those rows are ever read.
+template <typename TI, int DIM>
+__global__ __launch_bounds__(256) void gather_ln_kernel(int64_t n, const TI* __restrict__ x, int64_t ldx,
+                                                        const int64_t* __restrict__ row_idx, int n_ln,
+                                                        const float* __restrict__ g, const float* __restrict__ b,
+                                                        float eps, float* __restrict__ y, int64_t ldy) {
+  constexpr int NJ = DIM / 256;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int64_t row = row_idx ? row_idx[i] : i;
+  float v[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) load4<TI>(x + row * ldx + j * 256 + lane * 4, v[j]);
+  for (int l = 0; l < n_ln; ++l) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+    const float mean = wave_sum(s) / (float)DIM;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float d = v[j][t] - mean;
+        q = fmaf(d, d, q);
+      }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)DIM + eps);
+    const float* gl = g ? g + (int64_t)l * DIM : nullptr;
+    const float* bl = b ? b + (int64_t)l * DIM : nullptr;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int e = j * 256 + lane * 4 + t;
+        v[j][t] = (v[j][t] - mean) * rstd * (gl ? gl[e] : 1.f) + (bl ? bl[e] : 0.f);
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) store4<float>(y + i * ldy + j * 256 + lane * 4, v[j]);
+}
+
+int gather_ln_dispatch(int dti, int64_t n, int64_t dim, const void* x, int64_t ldx, const int64_t* row_idx,
+                       int n_ln, const float* g, const float* b, float eps, float* y, int64_t ldy,
+                       hipStream_t s) {
+  NR_CHECK_ARG(dti == NR_F32 || dti == NR_BF16 || dti == NR_F16, "nr_gather_layernorm: bad dtype");
+  NR_CHECK_ARG(n >= 0 && n_ln >= 0 && ldx >= dim && ldy >= dim && ldx % 4 == 0 && ldy % 4 == 0,
+               "nr_gather_layernorm: bad shape/strides");
+  if (n == 0) return NR_OK;
+  NR_CHECK_ARG(x && y, "nr_gather_layernorm: null pointer");
+  NR_CHECK_ARG(dim == 1024 || dim == 512 || dim == 2048 || dim == 256, "nr_gather_layernorm: dim %lld unsupported",
+               (long long)dim);
+  const dim3 grid((unsigned)((n + 3) / 4));
+#define NR_GL(T, D)                                                                                   \
+  if (dim == D) {                                                                                     \
+    hipLaunchKernelGGL((gather_ln_kernel<T, D>), grid, dim3(256), 0, s, n, (const T*)x, ldx, row_idx, \
+                       n_ln, g, b, eps, y, ldy);                                                      \
+  }
+#define NR_GL_ALL(T) NR_GL(T, 256) NR_GL(T, 512) NR_GL(T, 1024) NR_GL(T, 2048)
+  if (dti == NR_F32) { NR_GL_ALL(float) }
+  else if (dti == NR_BF16) { NR_GL_ALL(__bf16) }
+  else { NR_GL_ALL(_Float16) }
+#undef NR_GL_ALL
+#undef NR_GL
+  NR_CHECK_LAUNCH("nr_gather_layernorm");
+  return NR_OK;
+}
+
 }  // namespace nr
+
+extern "C" int nr_gather_layernorm(int dtype_in, int64_t n, int64_t dim, const void* x, int64_t ldx,
+                                   const int64_t* row_idx, int n_ln, const float* gammas, const float* betas,
+                                   float eps, float* out, int64_t ldo, void* stream) {
+  nr::clear_error();
+  return nr::gather_ln_dispatch(dtype_in, n, dim, x, ldx, row_idx, n_ln, gammas, betas, eps, out, ldo,
+                                (hipStream_t)stream);
+}
 
 extern "C" int nr_layernorm(int dtype_in, int dtype_out, int64_t rows, int64_t dim, const void* x,
                             int64_t ldx, const float* gamma, const float* beta, float eps, void* y,

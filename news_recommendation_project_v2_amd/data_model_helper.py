@@ -90,3 +90,41 @@ def get_embeddings(model_path: str, news_list: Iterable[str], news_text_dict: di
     """Title encoder entry (data_model_helper.py:45-84): see encoder.py."""
     from .encoder import get_embeddings as _ge
     return _ge(model_path, news_list, news_text_dict)
+
+
+def apply_token_attn(model_path, db_name, num_samples: int) -> torch.Tensor:
+    """Token-attention table of news 0..num_samples-1 from the sqlite token DB
+    (data_model_helper.py:390-413): ``FirstAttentionPoolFunc(last_token_pool)``
+    per news -> [N, D] f32 on the host.
+
+    The reference pads each batch of token states, ships them to the device and
+    runs the (dead) attention; its output is the g_mlp_layernorm chain of each
+    news' last valid token (attention.py:193, modeling_utils.py:37-48), so only
+    those rows are uploaded and the LN runs in ``nr_gather_layernorm``."""
+    import sqlite3
+
+    from .data_utils import iter_token_states
+    from .modeling_utils import get_token_attn_model
+    model = get_token_attn_model(model_path)
+    out = []
+    with sqlite3.connect(str(db_name)) as conn:
+        for rows, lens in iter_token_states(conn, num_samples):
+            last = rows[torch.as_tensor(np.cumsum(lens) - 1)]
+            dev_rows = last.to(DEVICE).contiguous()
+            seg = torch.arange(len(lens) + 1, dtype=torch.int64, device=DEVICE)
+            out.append(model.forward_packed(dev_rows, seg).cpu())
+    return torch.cat(out) if out else torch.zeros((0, 1024))
+
+
+def store_embeddings(model_path: str, news_list: Iterable[str], news_text_dict: dict[str, str], db_name,
+                     dtype: torch.dtype = torch.float32) -> int:
+    """Per-token title hidden states -> sqlite token DB (data_model_helper.py:374-387),
+    with the MI355X title encoder on a LOCAL model directory."""
+    from transformers import AutoTokenizer
+
+    from .config import NEWS_TEXT_MAXLEN
+    from .encoder import XLMREncoder, store_token_states, tokenize
+    tok = AutoTokenizer.from_pretrained(model_path)
+    enc = XLMREncoder.from_pretrained_dir(model_path, dtype=dtype)
+    texts = [news_text_dict[n] for n in news_list]
+    return store_token_states(enc, *tokenize(tok, texts, NEWS_TEXT_MAXLEN), db_name)

@@ -202,3 +202,69 @@ class FinalAttentionEvalDataset(Dataset):
 
     def __getitem__(self, idx):
         return self.group_history[idx]
+
+
+# --------------------------------------------------------------- token states
+# The sqlite token-state store: table ``tensors(id INTEGER
+# PRIMARY KEY, data BLOB)``, row id = news index + 1, each blob a
+# ``torch.save`` of that news title's fp16 per-token hidden states
+# [L_valid, 1024] (writer: modeling_utils.py:456-478 / data_model_helper.py:374-387).
+
+def read_token_blob(blob: bytes) -> torch.Tensor:
+    """One stored token-state tensor (torch.load, weights_only: executes nothing)."""
+    import io
+    with io.BytesIO(blob) as f:
+        return torch.load(f, weights_only=True)
+
+
+def tensor_pad_to_maxlen(grouped_items: Sequence[torch.Tensor]) -> dict[str, torch.Tensor]:
+    """Right-pad [L_i, D] tensors to [B, L_max, D] + int32 mask (data_utils.py:753-781)."""
+    lens = [len(t) for t in grouped_items]
+    width = max(lens)
+    emb = torch.zeros((len(lens), width) + tuple(grouped_items[0].shape[1:]), dtype=grouped_items[0].dtype)
+    mask = torch.zeros((len(lens), width), dtype=torch.int32)
+    for r, t in enumerate(grouped_items):
+        emb[r, :lens[r]] = t
+        mask[r, :lens[r]] = 1
+    return {"embeddings": emb, "attention_mask": mask}
+
+
+def get_embeds_from_db(conn, indices) -> dict[str, torch.Tensor]:
+    """Token states of news ``indices`` (ids = index + 1), padded (data_utils.py:878-890).
+
+    Like the reference's ``WHERE id IN (...)`` query, rows come back in
+    ascending id order and missing ids are skipped."""
+    ids = ",".join(str(int(i) + 1) for i in indices)
+    rows = conn.execute(f"SELECT data FROM tensors WHERE id IN ({ids}) ORDER BY id;").fetchall()
+    return tensor_pad_to_maxlen([read_token_blob(r[0]) for r in rows])
+
+
+def iter_token_states(conn, num_items: int, chunk: int = 4096):
+    """Packed token states of news 0..num_items-1 in id order: yields
+    (rows [T, D] tensor, per-news lengths int64 [n]) per chunk of ids."""
+    for a in range(0, num_items, chunk):
+        b = min(num_items, a + chunk)
+        res = conn.execute("SELECT data FROM tensors WHERE id BETWEEN ? AND ? ORDER BY id;", (a + 1, b)).fetchall()
+        ts = [read_token_blob(r[0]) for r in res]
+        if not ts:
+            continue
+        yield torch.cat(ts), np.array([len(t) for t in ts], dtype=np.int64)
+
+
+class TokenAttnEvalDataset(Dataset):
+    """Sequential news indices (data_utils.py:918-926)."""
+
+    def __init__(self, num_items: int):
+        self.num_items = num_items
+
+    def __len__(self):
+        return self.num_items
+
+    def __getitem__(self, idx):
+        return idx
+
+
+def token_attention_eval_collate_fn(input, conn):
+    """(f32 token states [B, L, D], int32 mask [B, L]) of a batch of news (data_utils.py:929-933)."""
+    res = get_embeds_from_db(conn, input)
+    return res["embeddings"].to(dtype=torch.float32), res["attention_mask"].to(dtype=torch.int32)

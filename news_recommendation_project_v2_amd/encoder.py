@@ -102,6 +102,13 @@ class XLMREncoder:
 
     # ------------------------------------------------------------------ forward
     def _chunk_forward(self, ids: np.ndarray, lens: np.ndarray) -> torch.Tensor:
+        x, cu = self._chunk_hidden(ids, lens)
+        # average_pool + F.normalize == latent pooling over each sequence's rows
+        from .modeling_utils import pool_rows
+        return pool_rows("latent", x, torch.as_tensor(cu).to(self.device))
+
+    def _chunk_hidden(self, ids: np.ndarray, lens: np.ndarray):
+        """last_hidden_state of the valid tokens, packed [T, 1024] (+ host offsets)."""
         dev, dt = self.device, self.dtype
         T = int(lens.sum())
         ids_d = torch.as_tensor(ids.astype(np.int32)).to(dev)
@@ -123,9 +130,18 @@ class XLMREncoder:
             ops.gemm(x, L["w1"], L["b1"], epilogue="gelu", out=ffn)
             ops.gemm(ffn, L["w2"], L["b2"], epilogue="resadd", residual=x, out=tmp)
             ops.layernorm(tmp, L["ln2"][0], L["ln2"][1], LN_EPS, out=x)
-        # average_pool + F.normalize == latent pooling over each sequence's rows
-        from .modeling_utils import pool_rows
-        return pool_rows("latent", x, torch.as_tensor(cu).to(dev))
+        return x, cu
+
+    def _chunks(self, lens: np.ndarray):
+        """Consecutive sequence ranges [s, e) of at most max_tokens tokens."""
+        off = np.concatenate([[0], np.cumsum(lens)])
+        s = 0
+        while s < len(lens):
+            e = s + 1
+            while e < len(lens) and off[e + 1] - off[s] <= self.max_tokens:
+                e += 1
+            yield s, e, off
+            s = e
 
     def encode_packed(self, ids: np.ndarray, lens: np.ndarray) -> torch.Tensor:
         """ids: flat int tokens of all sequences; lens: tokens per sequence.
@@ -134,16 +150,20 @@ class XLMREncoder:
         lens = np.asarray(lens, dtype=np.int64)
         if np.any(lens <= 0):
             raise ValueError("every sequence needs at least one token")
-        out = []
-        off = np.concatenate([[0], np.cumsum(lens)])
-        s = 0
-        while s < len(lens):
-            e = s + 1
-            while e < len(lens) and off[e + 1] - off[s] <= self.max_tokens:
-                e += 1
-            out.append(self._chunk_forward(ids[off[s]:off[e]], lens[s:e]))
-            s = e
+        out = [self._chunk_forward(ids[off[s]:off[e]], lens[s:e]) for s, e, off in self._chunks(lens)]
         return torch.cat(out) if out else torch.zeros((0, HIDDEN), device=self.device)
+
+    def hidden_states_packed(self, ids: np.ndarray, lens: np.ndarray):
+        """Per-token last_hidden_state of every sequence (the tensors the reference
+        stores per news in its sqlite token DB, modeling_utils.py:456-478).
+        Yields (first sequence index, packed rows [T, 1024] on device, lengths)."""
+        ids = np.asarray(ids)
+        lens = np.asarray(lens, dtype=np.int64)
+        if np.any(lens <= 0):
+            raise ValueError("every sequence needs at least one token")
+        for s, e, off in self._chunks(lens):
+            x, _ = self._chunk_hidden(ids[off[s]:off[e]], lens[s:e])
+            yield s, x, lens[s:e]
 
     def encode_padded(self, input_ids: torch.Tensor, attention_mask: torch.Tensor) -> torch.Tensor:
         """Tokenizer-style right-padded batch -> embeddings (drops padded slots)."""
@@ -159,6 +179,29 @@ def tokenize(tokenizer, texts: Sequence[str], max_len: int) -> tuple[np.ndarray,
     lens = np.array([len(x) for x in enc["input_ids"]], dtype=np.int64)
     ids = np.concatenate([np.asarray(x, dtype=np.int32) for x in enc["input_ids"]]) if len(lens) else np.zeros(0, np.int32)
     return ids, lens
+
+
+def store_token_states(encoder: "XLMREncoder", ids: np.ndarray, lens: np.ndarray, db_name,
+                       dtype: torch.dtype = torch.float16) -> int:
+    """Write every sequence's per-token hidden states into the reference's
+    sqlite token DB layout (store_text_embed_full_eval, modeling_utils.py:456-478):
+    table ``tensors(id INTEGER PRIMARY KEY, data BLOB)``, ids 1.., each blob a
+    ``torch.save`` of a [L_valid, 1024] tensor (fp16 like the reference's fp16
+    model outputs).  Returns the number of rows written."""
+    import io
+    import sqlite3
+    n = 0
+    with sqlite3.connect(str(db_name)) as conn:
+        conn.execute("DROP TABLE IF EXISTS tensors;")
+        conn.execute("CREATE TABLE tensors (id INTEGER PRIMARY KEY, data BLOB)")
+        for _, x, ln in encoder.hidden_states_packed(ids, lens):
+            host = x.to(dtype).cpu()
+            for t in torch.split(host, [int(v) for v in ln]):
+                buf = io.BytesIO()
+                torch.save(t.clone(), buf)
+                conn.execute("INSERT INTO tensors (data) VALUES (?)", (buf.getvalue(),))
+                n += 1
+    return n
 
 
 def get_embeddings(model_path: str, news_list: Iterable[str], news_text_dict: dict[str, str],

@@ -16,7 +16,8 @@ import torch.nn.functional as F
 
 from . import ops
 from ._lib import NewsRecHIPError
-from .config import DEVICE, FINAL_ATTENTION_HIDDEN_DIM, REDUCED_DIM
+from .attention import MyEncoder
+from .config import DEVICE, EMBEDDING_DIM, FINAL_ATTENTION_HIDDEN_DIM, NUM_HIDDEN_LAYERS, REDUCED_DIM
 from .latent_attention import LatentAttentionModel
 
 
@@ -28,6 +29,19 @@ def last_token_pool(last_hidden_states: torch.Tensor, attention_mask: torch.Tens
         return last_hidden_states[:, -1]
     last = attention_mask.sum(dim=1) - 1
     return last_hidden_states[torch.arange(last_hidden_states.shape[0], device=last_hidden_states.device), last]
+
+
+def last_token_rows(attention_mask: torch.Tensor) -> torch.Tensor:
+    """Flat row index (b * L + position) that ``last_token_pool`` selects per row,
+    with its exact semantics (modeling_utils.py:37-48): position L-1 for all rows
+    when every row's last mask slot is set, else ``mask.sum - 1`` (an all-zero
+    row gives -1, which torch indexing wraps to L-1)."""
+    B, L = attention_mask.shape
+    if bool((attention_mask[:, -1].sum() == B).item()):
+        pos = torch.full((B,), L - 1, dtype=torch.int64, device=attention_mask.device)
+    else:
+        pos = (attention_mask.sum(dim=1).to(torch.int64) - 1) % L
+    return torch.arange(B, device=attention_mask.device, dtype=torch.int64) * L + pos
 
 
 def first_token_pool(last_hidden_states: torch.Tensor, *args, **kwargs) -> torch.Tensor:
@@ -125,6 +139,48 @@ class FinalAttention(torch.nn.Module):
         rows, off = flatten_valid(embeddings, attention_mask)
         table = self.item_table(rows.float())
         return pool_rows("final", table, off)
+
+
+class FirstAttentionPoolFunc(torch.nn.Module):
+    """Token-attention encoder + pooling (modeling_utils.py:498-513).
+
+    ``self.encoder`` is the reference's ``MyEncoder`` (same state-dict keys),
+    whose output is a chain of g_mlp_layernorms of its input (attention.py:193).
+    With ``last_token_pool`` the whole forward is one gathered LayerNorm of each
+    row's last valid token (``nr_gather_layernorm``): only B rows are read.
+    Other pool functions get the full LN'd sequence.
+    """
+
+    def __init__(self, pool_func, embedding_dim=EMBEDDING_DIM, num_layers=NUM_HIDDEN_LAYERS):
+        super().__init__()
+        self.pool_func = pool_func
+        self.encoder = MyEncoder(hidden_size=embedding_dim, num_hidden_layers=num_layers)
+
+    def forward(self, embeddings: torch.Tensor, attention_mask: torch.Tensor) -> torch.Tensor:
+        if embeddings.device.type != "cuda":
+            raise NewsRecHIPError("FirstAttentionPoolFunc runs on the MI355X HIP path only (got a CPU tensor)")
+        if self.pool_func is last_token_pool:
+            rows = last_token_rows(attention_mask)
+            return MyEncoder.ln_chain(list(self.encoder.layer), embeddings, row_idx=rows)
+        return self.pool_func(self.encoder(embeddings, attention_mask), attention_mask)
+
+    def forward_packed(self, rows: torch.Tensor, seg_off: torch.Tensor) -> torch.Tensor:
+        """Packed variant: ``rows`` [T, D] holds every sequence's valid tokens back
+        to back, ``seg_off`` [B+1] int64 the offsets; returns the last_token_pool
+        output [B, D] f32 (each sequence must have >= 1 token)."""
+        if self.pool_func is not last_token_pool:
+            raise NewsRecHIPError("forward_packed implements last_token_pool only")
+        last = (seg_off[1:] - 1).to(torch.int64).contiguous()
+        return MyEncoder.ln_chain(list(self.encoder.layer), rows, row_idx=last)
+
+
+def get_token_attn_model(model_path: Optional[Path] = None) -> FirstAttentionPoolFunc:
+    """modeling_utils.py:516-524."""
+    model = FirstAttentionPoolFunc(pool_func=last_token_pool, embedding_dim=EMBEDDING_DIM,
+                                   num_layers=NUM_HIDDEN_LAYERS)
+    if model_path:
+        model.load_state_dict(torch.load(model_path, weights_only=True))
+    return model.to(DEVICE)
 
 
 def get_final_attention_model(model_path: Optional[Path] = None) -> FinalAttention:

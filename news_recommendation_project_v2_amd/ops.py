@@ -99,6 +99,41 @@ def layernorm(x: torch.Tensor, gamma: Optional[torch.Tensor], beta: Optional[tor
     return out
 
 
+def gather_layernorm(x: torch.Tensor, row_idx: Optional[torch.Tensor], gammas: Optional[torch.Tensor],
+                     betas: Optional[torch.Tensor], eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[i] = LN chain (gammas/betas [n_ln, D]) of x[row_idx[i]] (identity if None), f32 out.
+
+    x may be f32, bf16 or f16 (the token-state blobs are fp16)."""
+    dev = _dev(x, row_idx, gammas, betas, out)
+    if x.dim() != 2 or x.stride(1) != 1:
+        raise _lib.NewsRecHIPError("gather_layernorm: x must be row-major 2-D")
+    dt = {torch.float32: _lib.NR_F32, torch.bfloat16: _lib.NR_BF16, torch.float16: _lib.NR_F16}.get(x.dtype)
+    if dt is None:
+        raise _lib.NewsRecHIPError(f"gather_layernorm: unsupported dtype {x.dtype}")
+    dim = x.shape[1]
+    if row_idx is not None:
+        if row_idx.dtype != torch.int64 or not row_idx.is_contiguous():
+            raise _lib.NewsRecHIPError("gather_layernorm: row_idx must be contiguous int64")
+        n = row_idx.numel()
+    else:
+        n = x.shape[0]
+    n_ln = 0
+    for t in (gammas, betas):
+        if t is not None:
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.dim() != 2 or t.shape[1] != dim:
+                raise _lib.NewsRecHIPError("gather_layernorm: gammas/betas must be contiguous f32 [n_ln, D]")
+            n_ln = max(n_ln, t.shape[0])
+    if gammas is not None and betas is not None and gammas.shape != betas.shape:
+        raise _lib.NewsRecHIPError("gather_layernorm: gammas and betas differ in shape")
+    if out is None:
+        out = torch.empty((n, dim), dtype=torch.float32, device=dev)
+    if out.dtype != torch.float32 or out.shape != (n, dim):
+        raise _lib.NewsRecHIPError("gather_layernorm: out must be f32 [n, D]")
+    _lib.call("nr_gather_layernorm", dt, n, dim, _ptr(x), x.stride(0), _ptr(row_idx), n_ln, _ptr(gammas),
+              _ptr(betas), ctypes.c_float(eps), _ptr(out), _rowmajor(out, "out"), _stream(dev))
+    return out
+
+
 def softmax64(x: torch.Tensor, out: Optional[torch.Tensor] = None,
               out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
     dev = _dev(x, out)

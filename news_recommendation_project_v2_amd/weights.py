@@ -161,6 +161,26 @@ def xlmr_state_dict(seed: int = 1234, n_layers: int = 24, vocab: int = 250002, h
     return sd
 
 
+def token_attn_state_dict(seed: int = 1234, hidden: int = 1024, num_layers: int = 1, heads: int = 8,
+                          intermediate: int = 3072) -> Dict[str, torch.Tensor]:
+    """State dict with the reference ``FirstAttentionPoolFunc`` keys
+    (modeling_utils.py:498-513 -> attention.py:28-207): ``encoder.layer.{i}.``
+    attention.qkv_proj / o_proj, g_mlp.up_gate_proj / down_proj, and the two
+    LayerNorms (gamma = 1 + U(-0.25, 0.25), beta = U(-0.25, 0.25) so they are
+    exercised)."""
+    sd: Dict[str, torch.Tensor] = {}
+    for i in range(num_layers):
+        p = f"encoder.layer.{i}."
+        sd.update(linear_params(seed, p + "attention.qkv_proj.", 3 * hidden, hidden))
+        sd.update(linear_params(seed, p + "attention.o_proj.", hidden, hidden))
+        sd.update(linear_params(seed, p + "g_mlp.up_gate_proj.", 2 * intermediate, hidden, bias=False))
+        sd.update(linear_params(seed, p + "g_mlp.down_proj.", hidden, intermediate))
+        for ln in ("attn_layernorm.", "g_mlp_layernorm."):
+            sd[p + ln + "weight"] = 1.0 + uniform_tensor(seed, p + ln + "weight", (hidden,), 0.25)
+            sd[p + ln + "bias"] = uniform_tensor(seed, p + ln + "bias", (hidden,), 0.25)
+    return sd
+
+
 def news_table(seed: int, n: int, dim: int = 1024, name: str = "news_table") -> torch.Tensor:
     """Synthetic news-embedding table: N(0,1) rows, matching the statistics of
     the LayerNorm-output ``new_embeddings/`` that eval.py loads."""

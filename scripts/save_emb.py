@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Encoder entry point: title embeddings -> {save_dir}/{split}.pt (+ query_{split}.pt)
+(reference scripts/save_emb.py:20-102).
+
+Pipeline as in the reference: TransformData -> EmbeddingsComponent (the
+XLM-R-large / e5-large-instruct title encoder, here the MI355X kernels of
+news_recommendation_project_v2_amd/encoder.py) -> SaveEmbeddingComponent, then
+a TransformData -> LoadEmbeddingComponent pipeline that reloads the tables.
+
+Flags (the reference hard-codes them): --data-dir --save-dir --model-path
+(a LOCAL HF directory: weights + tokenizer; nothing is downloaded) --splits
+--dtype {fp32,bf16} --num-impressions --token-db (also write the per-token
+sqlite store that the token-attention path reads, data_model_helper.py:374-387).
+--synthetic runs without MIND data or a checkpoint: seeded MIND-shaped
+behaviours, synthetic title token ids (passage ~20, query ~46 tokens) and the
+deterministic XLM-R-large-shaped weights of weights.xlmr_state_dict.
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from news_recommendation_project_v2_amd import weights as W  # noqa: E402
+from news_recommendation_project_v2_amd.components import (EmbeddingsComponent,  # noqa: E402
+                                                           LoadEmbeddingComponent, SaveEmbeddingComponent,
+                                                           TransformData)
+from news_recommendation_project_v2_amd.config import MODEL_PATH, NewsDataset  # noqa: E402
+from news_recommendation_project_v2_amd.pipeline import Pipeline, PipelineComponent  # noqa: E402
+
+
+def synthetic_titles(n: int, seed: int, vocab: int, mean_len: int, prefix_len: int = 0):
+    """Token ids framed <s> ... </s> (0 / 2), lengths ~ mean_len +- 6."""
+    rng = np.random.default_rng(seed)
+    lens = np.clip(np.rint(rng.normal(mean_len, 6, n)), 3, 512).astype(np.int64) + prefix_len
+    ids = rng.integers(5, vocab, int(lens.sum())).astype(np.int32)
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    ids[starts] = 0
+    ids[starts + lens - 1] = 2
+    return ids, lens
+
+
+class SyntheticEmbeddingsComponent(PipelineComponent):
+    """EmbeddingsComponent stand-in for --synthetic: the same encoder kernels on
+    synthetic token ids (query = instruction prefix + title, passage = title)."""
+
+    required_keys = {"news_list"}
+
+    def __init__(self, encoder, seed: int, vocab: int):
+        self.encoder, self.seed, self.vocab = encoder, seed, vocab
+
+    def transform(self, ctx):
+        n = len(ctx["news_list"])
+        t0 = time.time()
+        p_ids, p_lens = synthetic_titles(n, self.seed, self.vocab, 20)
+        q_ids, q_lens = synthetic_titles(n, self.seed, self.vocab, 20, prefix_len=26)
+        new = ctx.copy()
+        new["news_embeddings"] = self.encoder.encode_packed(p_ids, p_lens).cpu()
+        new["query_news_embeddings"] = self.encoder.encode_packed(q_ids, q_lens).cpu()
+        dt = time.time() - t0
+        tok = int(p_lens.sum() + q_lens.sum())
+        print(f"[save_emb] {ctx['news_dataset'].value}: {n} news, {tok} tokens in {dt:.2f}s "
+              f"({tok / dt:.3g} tokens/s incl. host)", flush=True)
+        return new
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--data-dir", type=Path, default=Path("data"))
+    ap.add_argument("--save-dir", type=Path, default=Path("embeddings"))
+    ap.add_argument("--model-path", default=MODEL_PATH)
+    ap.add_argument("--splits", default="MINDsmall_train,MINDsmall_dev")
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--num-impressions", type=int, default=None)
+    ap.add_argument("--token-db", type=Path, default=None)
+    ap.add_argument("--synthetic", action="store_true")
+    ap.add_argument("--layers", type=int, default=24, help="--synthetic: encoder depth")
+    ap.add_argument("--vocab", type=int, default=250002, help="--synthetic: vocabulary size")
+    args = ap.parse_args()
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+
+    rng = np.random.default_rng(1234)
+    splits = [NewsDataset[s] for s in args.splits.split(",")]
+    ctxs = []
+    if args.synthetic:
+        sys.path.insert(0, str(Path(__file__).resolve().parent))
+        from eval import synthetic_context
+        from news_recommendation_project_v2_amd.encoder import XLMREncoder
+        encoder = XLMREncoder(W.xlmr_state_dict(1234, args.layers, args.vocab), dtype=dtype)
+        for i, sp in enumerate(splits):
+            ctxs.append(synthetic_context(sp, args.num_impressions or 2000, seed=1234 + i))
+        embed = [SyntheticEmbeddingsComponent(encoder, 1234 + i, args.vocab) for i in range(len(splits))]
+    else:
+        from news_recommendation_project_v2_amd.data_utils import load_dataset
+        for sp in splits:
+            beh, feats = load_dataset(args.data_dir, sp, num_samples=args.num_impressions, random_state=rng)
+            ctxs.append({"news_dataset": sp, "behaviors": beh, **feats})
+        embed = [EmbeddingsComponent(args.model_path)] * len(splits)
+
+    for ctx, emb in zip(ctxs, embed):
+        save = Pipeline(f"save_emb_{ctx['news_dataset'].value}",
+                        [("init_transform", TransformData()), ("model_embed", emb),
+                         ("save_embedding", SaveEmbeddingComponent(args.save_dir))])
+        out, _ = save.transform(dict(ctx))
+        if args.token_db is not None and not args.synthetic:
+            from news_recommendation_project_v2_amd.data_model_helper import store_embeddings
+            db = args.token_db.with_name(f"{args.token_db.stem}_{ctx['news_dataset'].value}{args.token_db.suffix}")
+            n = store_embeddings(args.model_path, out["news_list"], out["news_text_dict"], db, dtype=dtype)
+            print(f"[save_emb] wrote {n} token-state rows to {db}", flush=True)
+        load = Pipeline(f"load_emb_{ctx['news_dataset'].value}",
+                        [("init_transform", TransformData()), ("load_embedding", LoadEmbeddingComponent(args.save_dir))])
+        back, _ = load.transform(dict(ctx))
+        print(tuple(back["news_embeddings"].shape), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -61,3 +61,15 @@ def test_pool_oracle_matches_reference(pooler):
         with torch.no_grad():
             out = pool_ref.latent_hiddens(sd, table[rows])
         np.testing.assert_allclose(out.numpy(), g["unpooled_out"], rtol=0, atol=1e-5)
+
+
+def test_token_attn_oracle_matches_reference():
+    from oracle import token_ref
+    g = golden("token_attn")
+    sd = W.token_attn_state_dict(int(g["weight_seed"]))
+    for name in ("ragged", "full", "empty_row"):
+        got = token_ref.first_attention_pool(sd, torch.from_numpy(g[f"{name}_x"]), torch.from_numpy(g[f"{name}_mask"]))
+        np.testing.assert_allclose(got.numpy(), g[f"{name}_out"], rtol=0, atol=1e-5)
+    states = torch.split(torch.from_numpy(g["db_states"]), list(g["db_lens"]))
+    got = token_ref.apply_token_attn(sd, states)
+    np.testing.assert_allclose(got.numpy(), g["db_out"], rtol=0, atol=1e-5)
