@@ -53,6 +53,10 @@ extern "C" {
                            C has N/2 columns                               */
 #define NR_EPI_RESADD 4 /* C = acc + bias + R                               */
 #define NR_EPI_GELU 5   /* C = gelu_erf(acc + bias)                         */
+#define NR_EPI_RELU_DROPOUT 6 /* C = relu(acc + bias) * keep / (1 - p), training
+                                 forward only: use nr_gemm_relu_dropout      */
+#define NR_EPI_DRELU 7  /* C = R > 0 ? acc * scale : 0 (backward of relu+dropout
+                           given its forward output R): nr_gemm_drelu       */
 
 /* Library version (major*100 + minor). */
 int nr_version(void);
@@ -79,6 +83,28 @@ const char* nr_last_error(void);
 int nr_gemm(int dtype_in, int dtype_out, int epilogue, int64_t M, int64_t N, int64_t K,
             const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
             const void* R, int64_t ldr, void* C, int64_t ldc, void* stream);
+
+/*
+ * nr_gemm with the training-forward epilogue of FinalAttention
+ * (modeling_utils.py:218-221: dropout(relu(linear(x))), p = 0.1 in train mode):
+ *   C = relu(A·Wᵀ + bias) * keep(row, col) / (1 - p)
+ * keep = drop_hash(seed, row * N + col) >= p * 2^32, drop_hash = the splitmix64
+ * finaliser of seed + (idx + 1) * 0x9E3779B97F4A7C15, upper 32 bits (restated
+ * in oracle/train_ref.py).  Replaces nn.Dropout's Philox stream: the masks are
+ * a different (equally distributed) draw, reproducible from (seed, row, col).
+ */
+int nr_gemm_relu_dropout(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K, const void* A,
+                         int64_t lda, const void* W, int64_t ldw, const float* bias, void* C, int64_t ldc,
+                         uint64_t seed, float p, void* stream);
+
+/*
+ * Data-grad GEMM through relu + dropout: C = Y > 0 ? (A·Wᵀ) * scale : 0, where
+ * Y is the forward output relu(z) * keep / (1 - p) (so Y > 0 <=> z > 0 and kept)
+ * and scale = 1 / (1 - p).  Y has dtype_out.
+ */
+int nr_gemm_drelu(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                  const void* W, int64_t ldw, const void* Y, int64_t ldy, void* C, int64_t ldc, float scale,
+                  void* stream);
 
 /*
  * y = LayerNorm(x) * gamma + beta over rows of `dim` (biased variance).
@@ -211,6 +237,71 @@ int nr_embed_ln(int dtype, int64_t n_tokens, const int32_t* ids, const int32_t* 
                 void* out, void* stream);
 int nr_attention_varlen(int dtype, int32_t n_seq, int64_t n_qblocks, const void* qkv,
                         const int32_t* cu_seqlens, const int32_t* qblock_off, void* ctx, void* stream);
+
+/*
+ * ---- Training step of config 5 (scripts/train_v3.py ->
+ * AttentionAttentionTrainer.train_one_epoch, trainer.py:1030-1117) ----------
+ * FinalAttention runs once per VALID history slot (the reference runs it per
+ * padded slot and masks; padded slots carry zero gradient), slots packed in
+ * CSR order (off[b]..off[b+1]) and padded with zero rows up to a multiple of
+ * 64 so every weight-grad GEMM has K % 64 == 0.
+ */
+
+/* dst[i] = src[idx[i]] (idx NULL: identity; idx[i] < 0: zero row), dtype cast.
+ * The history gather first_res[hist_indices] * mask (trainer.py:1052-1054). */
+int nr_gather_rows(int dtype_in, int dtype_out, int64_t n, int64_t dim, const void* src, int64_t lds,
+                   const int32_t* idx, void* dst, int64_t ldd, void* stream);
+
+/* dst[c][r] = src[r][c] (dtype cast allowed): the operands of the data-grad
+ * (dY·W = dY·(Wᵀ)ᵀ) and weight-grad (dYᵀ·X) GEMMs on the C = A·Wᵀ kernel. */
+int nr_transpose(int dtype_in, int dtype_out, int64_t rows, int64_t cols, const void* src, int64_t lds,
+                 void* dst, int64_t ldd, void* stream);
+
+/* FinalAttention pooling forward over consecutive rows of xp = [x | exp(w)]
+ * (row stride ld >= 2048, modeling_utils.py:224-228):
+ * users[b] = sum x p / (sum p + 1e-10), z[b] = sum p + 1e-10 (both f32 [n_seg][1024]). */
+int nr_final_pool_fwd(int dtype, int64_t n_seg, const int64_t* off, const void* xp, int64_t ld, float* users,
+                      float* z, void* stream);
+
+/* Its backward: dx_i = du p_i / z, dw_i = du (x_i - u) p_i / z (w = pre-exp
+ * logit).  Rows off[n_seg]..n_rows-1 (padding) are zeroed. */
+int nr_final_pool_bwd(int dtype, int64_t n_seg, const int64_t* off, int64_t n_rows, const void* xp, int64_t ld,
+                      const float* users, const float* z, const float* du, void* dx, int64_t lddx, void* dw,
+                      int64_t lddw, void* stream);
+
+/* s_pos = cos(users[b], E[pos[b]]), s_neg = cos(users[b], E[neg[b]])
+ * (F.cosine_similarity, per-vector clamp 1e-8, trainer.py:1058-1061) and
+ * MarginRankingLoss(margin)(s_pos, s_neg, 1) = mean clamp_min(margin - s_pos + s_neg, 0)
+ * (trainer.py:985,1063-1066).  *loss += the mean (caller zeroes it); du written;
+ * dE rows accumulated (atomics, caller zeroes dE); s_out [2B] nullable. */
+int nr_cosine_margin(int64_t B, const float* users, const float* E, int64_t lde, const int32_t* pos,
+                     const int32_t* neg, float margin, float* s_out, float* loss, float* du, float* dE,
+                     void* stream);
+
+/* dst[idx[i]] += src[i] (f32 atomics; idx < 0 skipped): the gradient of the
+ * history gather back to the unique-news rows. */
+int nr_scatter_add_rows(int dtype, int64_t n, int64_t dim, const void* src, int64_t lds, const int32_t* idx,
+                        float* dst, int64_t ldd, void* stream);
+
+/* out[c] += sum_r src[r][c] (bias gradients; caller zeroes out). */
+int nr_col_sum(int dtype, int64_t rows, int64_t cols, const void* src, int64_t lds, float* out, void* stream);
+
+/* Token-model LayerNorm parameter grads (E = LN(x[row_idx]) g + b):
+ * dgamma += sum dE xhat, dbeta += sum dE.  dim 1024; x f32 / bf16 / f16. */
+int nr_ln_param_grad(int dtype_in, int64_t n, int64_t dim, const void* x, int64_t ldx, const int64_t* row_idx,
+                     float eps, const float* dy, int64_t lddy, float* dgamma, float* dbeta, void* stream);
+
+/* *out += sum x^2 (the global grad norm of clip_grad_norm_, trainer.py:1067-1071). */
+int nr_sumsq(int64_t n, const float* x, float* out, void* stream);
+
+/* torch.optim.AdamW step (trainer.py:979-983: lr 1e-6, betas (0.9, 0.999),
+ * eps 1e-8, weight_decay 0.01) over a flat f32 parameter buffer, with the
+ * clip_grad_norm_(max_norm) coefficient min(max_norm / (sqrt(*sumsq) + 1e-6), 1)
+ * folded in (sumsq NULL: no clipping).  p_bf16 (nullable) receives a bf16
+ * copy of the updated parameters. */
+int nr_adamw(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf16, int64_t step, float lr,
+             float beta1, float beta2, float eps, float weight_decay, float max_norm, const float* sumsq,
+             void* stream);
 
 #ifdef __cplusplus
 }

@@ -25,6 +25,8 @@ NR_EPI_EXP = 2
 NR_EPI_GEGLU = 3
 NR_EPI_RESADD = 4
 NR_EPI_GELU = 5
+NR_EPI_RELU_DROPOUT = 6
+NR_EPI_DRELU = 7
 
 _p = ctypes.c_void_p
 _i = ctypes.c_int
@@ -37,6 +39,8 @@ SIGNATURES = {
     "nr_init": (_i, [_i]),
     "nr_last_error": (ctypes.c_char_p, []),
     "nr_gemm": (_i, [_i, _i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p]),
+    "nr_gemm_relu_dropout": (_i, [_i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, ctypes.c_uint64, _f, _p]),
+    "nr_gemm_drelu": (_i, [_i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _l, _p, _l, _f, _p]),
     "nr_layernorm": (_i, [_i, _i, _l, _l, _p, _l, _p, _p, _f, _p, _l, _p]),
     "nr_gather_layernorm": (_i, [_i, _l, _l, _p, _l, _p, _i, _p, _p, _f, _p, _l, _p]),
     "nr_softmax64": (_i, [_l, _l, _p, _l, _i, _p, _l, _p]),
@@ -49,6 +53,16 @@ SIGNATURES = {
     "nr_latent_transform": (_i, [_i, _l, _p, _l, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _l, _p]),
     "nr_embed_ln": (_i, [_i, _l, _p, _p, _p, _p, _p, _p, _p, _f, _p, _p]),
     "nr_attention_varlen": (_i, [_i, ctypes.c_int32, _l, _p, _p, _p, _p, _p]),
+    "nr_gather_rows": (_i, [_i, _i, _l, _l, _p, _l, _p, _p, _l, _p]),
+    "nr_transpose": (_i, [_i, _i, _l, _l, _p, _l, _p, _l, _p]),
+    "nr_final_pool_fwd": (_i, [_i, _l, _p, _p, _l, _p, _p, _p]),
+    "nr_final_pool_bwd": (_i, [_i, _l, _p, _l, _p, _l, _p, _p, _p, _p, _l, _p, _l, _p]),
+    "nr_cosine_margin": (_i, [_l, _p, _p, _l, _p, _p, _f, _p, _p, _p, _p, _p]),
+    "nr_scatter_add_rows": (_i, [_i, _l, _l, _p, _l, _p, _p, _l, _p]),
+    "nr_col_sum": (_i, [_i, _l, _l, _p, _l, _p, _p]),
+    "nr_ln_param_grad": (_i, [_i, _l, _l, _p, _l, _p, _f, _p, _l, _p, _p, _p]),
+    "nr_sumsq": (_i, [_l, _p, _p, _p]),
+    "nr_adamw": (_i, [_l, _p, _p, _p, _p, _p, _l, _f, _f, _f, _f, _f, _f, _p, _p]),
 }
 
 

@@ -28,6 +28,13 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
+// Extra epilogue arguments (dropout of the training forward; unused otherwise).
+struct EpiArgs {
+  uint64_t seed;  // dropout stream
+  uint32_t thr;   // drop iff drop_hash(seed, row * N + col) < thr  (thr = p * 2^32)
+  float scale;    // 1 / (1 - p)
+};
+
 template <typename TO>
 __device__ __forceinline__ TO to_out(float v) {
   if constexpr (sizeof(TO) == 4) return v; else return (TO)v;
@@ -43,7 +50,8 @@ __device__ __forceinline__ float from_out(TO v) {
 template <int EPI, typename TO>
 __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], int64_t M, int64_t wrow,
                                               int64_t wcol, int lane, const float* __restrict__ bias,
-                                              const TO* R, int64_t ldr, TO* C, int64_t ldc) {
+                                              const TO* R, int64_t ldr, TO* C, int64_t ldc,
+                                              int64_t N, const EpiArgs& ea) {
   const int cl = lane & 31;
   const int rh = 4 * (lane >> 5);
   if constexpr (EPI == NR_EPI_GEGLU) {
@@ -76,9 +84,12 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], int64_t
           if (row < M) {
             float v = acc[mi][ni][reg] + b;
             if constexpr (EPI == NR_EPI_RELU) v = fmaxf(v, 0.f);
+            if constexpr (EPI == NR_EPI_RELU_DROPOUT)
+              v = drop_hash(ea.seed, (uint64_t)(row * N + col)) < ea.thr ? 0.f : fmaxf(v, 0.f) * ea.scale;
             if constexpr (EPI == NR_EPI_EXP) v = expf(v);
             if constexpr (EPI == NR_EPI_GELU) v = gelu_erf(v);
             if constexpr (EPI == NR_EPI_RESADD) v += from_out<TO>(R[row * ldr + col]);
+            if constexpr (EPI == NR_EPI_DRELU) v = from_out<TO>(R[row * ldr + col]) > 0.f ? v * ea.scale : 0.f;
             C[row * ldc + col] = to_out<TO>(v);
           }
         }
@@ -94,7 +105,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(int64_t M, int64_t N, int6
                                                       const TI* __restrict__ A, int64_t lda,
                                                       const TI* __restrict__ W, int64_t ldw,
                                                       const float* __restrict__ bias, const TO* R,
-                                                      int64_t ldr, TO* C, int64_t ldc) {
+                                                      int64_t ldr, TO* C, int64_t ldc, EpiArgs ea) {
   constexpr int BK = 128 / (int)sizeof(TI);
   constexpr int TILE_WORDS = GBM * GROW;  // one operand tile, 32-bit words
   __shared__ __attribute__((aligned(16))) uint32_t smem[2 * 2 * TILE_WORDS];
@@ -200,7 +211,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(int64_t M, int64_t N, int6
     __syncthreads();
   }
 
-  gemm_epilogue<EPI, TO>(acc, M, m0 + wm * 64, n0 + wn * 64, lane, bias, R, ldr, C, ldc);
+  gemm_epilogue<EPI, TO>(acc, M, m0 + wm * 64, n0 + wn * 64, lane, bias, R, ldr, C, ldc, N, ea);
 }
 
 // ---------------------------------------------------------------------------
@@ -224,7 +235,7 @@ __global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, i
                                                              const TI* __restrict__ A, int64_t lda,
                                                              const TI* __restrict__ W, int64_t ldw,
                                                              const float* __restrict__ bias, const TO* R,
-                                                             int64_t ldr, TO* C, int64_t ldc) {
+                                                             int64_t ldr, TO* C, int64_t ldc, EpiArgs ea) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
@@ -358,6 +369,11 @@ __global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, i
         } else {
           float v0 = acc[mi][0][reg] + ba, v1 = acc[mi][1][reg] + bg;
           if constexpr (EPI == NR_EPI_RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
+          if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
+            const uint64_t gi = (uint64_t)((m0 + wm * 128 + pass * 64 + lr) * N + wcol + cl);
+            v0 = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(v0, 0.f) * ea.scale;
+            v1 = drop_hash(ea.seed, gi + 32) < ea.thr ? 0.f : fmaxf(v1, 0.f) * ea.scale;
+          }
           if constexpr (EPI == NR_EPI_EXP) { v0 = expf(v0); v1 = expf(v1); }
           if constexpr (EPI == NR_EPI_GELU) { v0 = gelu_erf(v0); v1 = gelu_erf(v1); }
           slab[lr * COLS + cl] = v0;
@@ -378,15 +394,21 @@ __global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, i
         v[q] = f.x; v[q + 1] = f.y; v[q + 2] = f.z; v[q + 3] = f.w;
       }
       if (row < M) {
-        if constexpr (EPI == NR_EPI_RESADD) {
+        if constexpr (EPI == NR_EPI_RESADD || EPI == NR_EPI_DRELU) {
           const uint4 rv = *reinterpret_cast<const uint4*>(R + row * ldr + ocol0 + cc);
+          float r[VEC];
           if constexpr (sizeof(TO) == 4) {
-            v[0] += __uint_as_float(rv.x); v[1] += __uint_as_float(rv.y);
-            v[2] += __uint_as_float(rv.z); v[3] += __uint_as_float(rv.w);
+            r[0] = __uint_as_float(rv.x); r[1] = __uint_as_float(rv.y);
+            r[2] = __uint_as_float(rv.z); r[3] = __uint_as_float(rv.w);
           } else {
             const uint32_t w4[4] = {rv.x, rv.y, rv.z, rv.w};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) { v[2 * q] += bf16_lo(w4[q]); v[2 * q + 1] += bf16_hi(w4[q]); }
+            for (int q = 0; q < 4; ++q) { r[2 * q] = bf16_lo(w4[q]); r[2 * q + 1] = bf16_hi(w4[q]); }
+          }
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) {
+            if constexpr (EPI == NR_EPI_RESADD) v[q] += r[q];
+            else v[q] = r[q] > 0.f ? v[q] * ea.scale : 0.f;
           }
         }
         TO o[VEC];
@@ -402,19 +424,21 @@ __global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, i
 template <typename TI, typename TO>
 static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                           const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
-                          void* C, int64_t ldc, hipStream_t s) {
+                          void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
   dim3 grid((unsigned)(N / G2BN), (unsigned)((M + G2BM - 1) / G2BM));
   const TI* a = (const TI*)A;
   const TI* w = (const TI*)W;
   const TO* r = (const TO*)R;
   TO* c = (TO*)C;
   switch (epi) {
-    case NR_EPI_NONE: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_NONE, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
-    case NR_EPI_RELU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_RELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
-    case NR_EPI_EXP: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_EXP, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
-    case NR_EPI_GEGLU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_GEGLU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
-    case NR_EPI_RESADD: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_RESADD, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
-    case NR_EPI_GELU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_GELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    case NR_EPI_NONE: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_NONE, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_RELU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_RELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_EXP: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_EXP, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_GEGLU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_GEGLU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_RESADD: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_RESADD, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_GELU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_GELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_RELU_DROPOUT: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_RELU_DROPOUT, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_DRELU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_DRELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
     default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
   }
   NR_CHECK_LAUNCH("nr_gemm");
@@ -424,19 +448,21 @@ static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* 
 template <typename TI, typename TO>
 static int launch_gemm_t(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                          const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
-                         void* C, int64_t ldc, hipStream_t s) {
+                         void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
   dim3 grid((unsigned)(N / GBN), (unsigned)((M + GBM - 1) / GBM));
   const TI* a = (const TI*)A;
   const TI* w = (const TI*)W;
   const TO* r = (const TO*)R;
   TO* c = (TO*)C;
   switch (epi) {
-    case NR_EPI_NONE: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_NONE, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
-    case NR_EPI_RELU: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_RELU, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
-    case NR_EPI_EXP: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_EXP, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
-    case NR_EPI_GEGLU: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_GEGLU, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
-    case NR_EPI_RESADD: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_RESADD, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
-    case NR_EPI_GELU: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_GELU, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc); break;
+    case NR_EPI_NONE: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_NONE, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_RELU: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_RELU, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_EXP: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_EXP, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_GEGLU: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_GEGLU, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_RESADD: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_RESADD, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_GELU: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_GELU, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_RELU_DROPOUT: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_RELU_DROPOUT, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_DRELU: hipLaunchKernelGGL((gemm_kernel<TI, NR_EPI_DRELU, TO>), grid, dim3(256), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
     default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
   }
   NR_CHECK_LAUNCH("nr_gemm");
@@ -446,6 +472,13 @@ static int launch_gemm_t(int epi, int64_t M, int64_t N, int64_t K, const void* A
 int gemm_dispatch(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, int64_t K,
                   const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
                   const void* R, int64_t ldr, void* C, int64_t ldc, hipStream_t s) {
+  return gemm_dispatch_ex(dtype_in, dtype_out, epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc,
+                          EpiArgs{0, 0, 1.f}, s);
+}
+
+int gemm_dispatch_ex(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, int64_t K,
+                     const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+                     const void* R, int64_t ldr, void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
   NR_CHECK_ARG(dtype_in == NR_F32 || dtype_in == NR_BF16, "nr_gemm: bad dtype_in %d", dtype_in);
   NR_CHECK_ARG(dtype_out == NR_F32 || dtype_out == NR_BF16, "nr_gemm: bad dtype_out %d", dtype_out);
   NR_CHECK_ARG(M >= 0 && N > 0 && K > 0, "nr_gemm: bad shape M=%lld N=%lld K=%lld", (long long)M, (long long)N, (long long)K);
@@ -456,9 +489,10 @@ int gemm_dispatch(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, in
     return NR_ERR_UNSUPPORTED;
   }
   NR_CHECK_ARG(A && W && C, "nr_gemm: null operand");
-  NR_CHECK_ARG(epi != NR_EPI_RESADD || R, "nr_gemm: RESADD needs R");
-  const int64_t ea = dtype_in == NR_F32 ? 4 : 8;  // elements per 16 B
-  NR_CHECK_ARG(lda >= K && ldw >= K && lda % ea == 0 && ldw % ea == 0 &&
+  NR_CHECK_ARG((epi != NR_EPI_RESADD && epi != NR_EPI_DRELU) || R, "nr_gemm: RESADD/DRELU need R");
+  NR_CHECK_ARG(epi >= NR_EPI_NONE && epi <= NR_EPI_DRELU, "nr_gemm: bad epilogue %d", epi);
+  const int64_t e16 = dtype_in == NR_F32 ? 4 : 8;  // elements per 16 B
+  NR_CHECK_ARG(lda >= K && ldw >= K && lda % e16 == 0 && ldw % e16 == 0 &&
                    ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0,
                "nr_gemm: A/W must be 16-byte aligned with 16-byte row strides");
   const int64_t ncols = epi == NR_EPI_GEGLU ? N / 2 : N;
@@ -469,25 +503,44 @@ int gemm_dispatch(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, in
   static const bool force_small = getenv("NR_GEMM_SMALL_TILE") != nullptr;  // A/B switch for profiling
   const int64_t vo = dtype_out == NR_F32 ? 4 : 8;  // the LDS-staged epilogue stores 16 B per lane
   const bool aligned_out = ((uintptr_t)C & 15) == 0 && ldc % vo == 0 &&
-                           (epi != NR_EPI_RESADD || (((uintptr_t)R & 15) == 0 && ldr % vo == 0));
+                           ((epi != NR_EPI_RESADD && epi != NR_EPI_DRELU) || (((uintptr_t)R & 15) == 0 && ldr % vo == 0));
   const bool big = (N % G2BN == 0) && aligned_out && !force_small;
   if (dtype_in == NR_F32) {
     if (big) {
-      if (dtype_out == NR_F32) return launch_gemm256<float, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
-      return launch_gemm256<float, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
+      if (dtype_out == NR_F32) return launch_gemm256<float, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
+      return launch_gemm256<float, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
     }
-    if (dtype_out == NR_F32) return launch_gemm_t<float, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
-    return launch_gemm_t<float, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
+    if (dtype_out == NR_F32) return launch_gemm_t<float, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
+    return launch_gemm_t<float, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
   }
   if (big) {
-    if (dtype_out == NR_F32) return launch_gemm256<__bf16, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
-    return launch_gemm256<__bf16, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
+    if (dtype_out == NR_F32) return launch_gemm256<__bf16, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
+    return launch_gemm256<__bf16, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
   }
-  if (dtype_out == NR_F32) return launch_gemm_t<__bf16, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
-  return launch_gemm_t<__bf16, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, s);
+  if (dtype_out == NR_F32) return launch_gemm_t<__bf16, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
+  return launch_gemm_t<__bf16, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
 }
 
 }  // namespace nr
+
+extern "C" int nr_gemm_relu_dropout(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K,
+                                    const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+                                    void* C, int64_t ldc, uint64_t seed, float p, void* stream) {
+  nr::clear_error();
+  NR_CHECK_ARG(p >= 0.f && p < 1.f, "nr_gemm_relu_dropout: p must be in [0, 1)");
+  const double t = (double)p * 4294967296.0;
+  const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  return nr::gemm_dispatch_ex(dtype_in, dtype_out, NR_EPI_RELU_DROPOUT, M, N, K, A, lda, W, ldw, bias, nullptr, 0,
+                              C, ldc, nr::EpiArgs{seed, thr, 1.0f / (1.0f - p)}, (hipStream_t)stream);
+}
+
+extern "C" int nr_gemm_drelu(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K, const void* A,
+                             int64_t lda, const void* W, int64_t ldw, const void* Y, int64_t ldy, void* C,
+                             int64_t ldc, float scale, void* stream) {
+  nr::clear_error();
+  return nr::gemm_dispatch_ex(dtype_in, dtype_out, NR_EPI_DRELU, M, N, K, A, lda, W, ldw, nullptr, Y, ldy, C, ldc,
+                              nr::EpiArgs{0, 0, scale}, (hipStream_t)stream);
+}
 
 extern "C" int nr_gemm(int dtype_in, int dtype_out, int epilogue, int64_t M, int64_t N, int64_t K,
                        const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,

@@ -22,6 +22,10 @@ void clear_error();
 int gemm_dispatch(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, int64_t K,
                   const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
                   const void* R, int64_t ldr, void* C, int64_t ldc, hipStream_t s);
+struct EpiArgs;
+int gemm_dispatch_ex(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, int64_t K,
+                     const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+                     const void* R, int64_t ldr, void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s);
 int layernorm_dispatch(int dti, int dto, int64_t rows, int64_t dim, const void* x, int64_t ldx,
                        const float* g, const float* b, float eps, void* y, int64_t ldy,
                        hipStream_t s);
@@ -36,6 +40,17 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// Counter-based dropout stream (splitmix64 finaliser of seed + (idx+1) * golden
+// ratio, upper 32 bits).  oracle/train_ref.py restates it in numpy so the CPU
+// checker draws exactly the same masks.
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

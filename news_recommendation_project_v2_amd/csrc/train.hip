@@ -1,0 +1,465 @@
+// Training-step kernels of config 5 (reference scripts/train_v3.py ->
+// AttentionAttentionTrainer.train_one_epoch, trainer.py:1030-1117):
+//   token model (g_mlp_layernorm of the last valid token) -> history gather ->
+//   FinalAttention per valid history slot (GEMMs in gemm.hip, dropout fused in
+//   the ReLU epilogue) -> per-dimension softmax pooling -> cosine vs the
+//   positive / negative news -> MarginRankingLoss(2) -> backward ->
+//   clip_grad_norm_(0.5) -> AdamW.
+// The GEMMs (forward, data-grad and weight-grad) all run on the C = A·Wᵀ MFMA
+// kernel; the weight-grad and data-grad operands are produced by the LDS
+// transpose below.  Everything here is HBM-bound row / reduction work.
+#include "nr_common.h"
+
+namespace nr {
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p) {
+  if constexpr (sizeof(T) == 4) return *p; else return (float)*p;
+}
+template <typename T>
+__device__ __forceinline__ void stf(T* p, float v) {
+  if constexpr (sizeof(T) == 4) *p = v; else *p = (T)v;
+}
+
+// ----------------------------------------------------------------- gather rows
+// dst[i] = src[idx[i]] (idx < 0 -> zero row), with dtype conversion.
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void gather_rows_kernel(int64_t n, int64_t dim, const TI* __restrict__ src,
+                                                          int64_t lds, const int32_t* __restrict__ idx,
+                                                          TO* __restrict__ dst, int64_t ldd) {
+  const int64_t i = (int64_t)blockIdx.x;
+  if (i >= n) return;
+  const int64_t r = idx ? idx[i] : i;
+  for (int64_t c = threadIdx.x; c < dim; c += 256) stf<TO>(dst + i * ldd + c, r < 0 ? 0.f : ldf<TI>(src + r * lds + c));
+}
+
+// ----------------------------------------------------------------- transpose
+// dst[c][r] = src[r][c] through a 64x65 f32 LDS tile (256 threads).
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void transpose_kernel(int64_t rows, int64_t cols, const TI* __restrict__ src,
+                                                        int64_t lds, TO* __restrict__ dst, int64_t ldd) {
+  __shared__ float tile[64][65];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int rr = ty + 4 * k;
+    const int64_t r = r0 + rr, c = c0 + tx;
+    tile[rr][tx] = (r < rows && c < cols) ? ldf<TI>(src + r * lds + c) : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int cc = ty + 4 * k;
+    const int64_t c = c0 + cc, r = r0 + tx;
+    if (c < cols && r < rows) stf<TO>(dst + c * ldd + r, tile[tx][cc]);
+  }
+}
+
+// ----------------------------------------------------------------- pooling fwd
+// FinalAttention pooling (modeling_utils.py:224-228) over consecutive slot rows:
+// xp row = [x | p] (p = exp(w)); u_d = sum x p / (sum p + 1e-10), z_d = sum p + 1e-10.
+// One workgroup (4 waves x 256 dims) per segment.
+template <typename T>
+__global__ __launch_bounds__(256) void final_pool_fwd_kernel(int64_t n_seg, const int64_t* __restrict__ off,
+                                                             const T* __restrict__ xp, int64_t ld,
+                                                             float* __restrict__ users, float* __restrict__ z) {
+  constexpr int D = 1024;
+  const int64_t b = blockIdx.x;
+  if (b >= n_seg) return;
+  const int d = threadIdx.x * 4;
+  float num[4] = {0.f, 0.f, 0.f, 0.f}, den[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t i = off[b]; i < off[b + 1]; ++i) {
+    const T* row = xp + i * ld;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float x = ldf<T>(row + d + t), p = ldf<T>(row + D + d + t);
+      num[t] = fmaf(x, p, num[t]);
+      den[t] += p;
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float zz = den[t] + 1e-10f;
+    z[b * D + d + t] = zz;
+    users[b * D + d + t] = num[t] / zz;
+  }
+}
+
+// ----------------------------------------------------------------- pooling bwd
+// dx_i = du * p_i / z ;  dlogit_i = du * (x_i - u) / z * p_i  (d p_i / d w_i = p_i).
+// Rows of no segment (padding up to n_rows) get zeros.
+template <typename T>
+__global__ __launch_bounds__(256) void final_pool_bwd_kernel(int64_t n_seg, const int64_t* __restrict__ off,
+                                                             int64_t n_rows, const T* __restrict__ xp, int64_t ld,
+                                                             const float* __restrict__ users,
+                                                             const float* __restrict__ z,
+                                                             const float* __restrict__ du, T* __restrict__ dx,
+                                                             int64_t lddx, T* __restrict__ dl, int64_t lddl) {
+  constexpr int D = 1024;
+  const int64_t b = blockIdx.x;
+  const int d = threadIdx.x * 4;
+  if (b >= n_seg) {  // trailing blocks zero the padding rows
+    for (int64_t i = off[n_seg] + (b - n_seg); i < n_rows; i += gridDim.x - n_seg)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { stf<T>(dx + i * lddx + d + t, 0.f); stf<T>(dl + i * lddl + d + t, 0.f); }
+    return;
+  }
+  float g[4], u[4], iz[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    g[t] = du[b * D + d + t];
+    u[t] = users[b * D + d + t];
+    iz[t] = 1.0f / z[b * D + d + t];
+  }
+  for (int64_t i = off[b]; i < off[b + 1]; ++i) {
+    const T* row = xp + i * ld;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float x = ldf<T>(row + d + t), p = ldf<T>(row + D + d + t);
+      const float gp = g[t] * p * iz[t];
+      stf<T>(dx + i * lddx + d + t, gp);
+      stf<T>(dl + i * lddl + d + t, gp * (x - u[t]));
+    }
+  }
+}
+
+// ----------------------------------------------------------------- cosine + margin loss
+// F.cosine_similarity(u, e) = (u / max(|u|, 1e-8)) . (e / max(|e|, 1e-8))
+// (data_model_helper.py / trainer.py:1058-1061), MarginRankingLoss(margin)(s_pos,
+// s_neg, y=1) = mean(clamp_min(margin - (s_pos - s_neg), 0)) (trainer.py:1063-1066).
+// One wave per batch row; du written, dE rows (pos / neg) accumulated with atomics.
+__global__ __launch_bounds__(256) void cosine_margin_kernel(int64_t B, const float* __restrict__ users,
+                                                            const float* __restrict__ E, int64_t lde,
+                                                            const int32_t* __restrict__ pos,
+                                                            const int32_t* __restrict__ neg, float margin,
+                                                            float* __restrict__ s_out, float* __restrict__ loss,
+                                                            float* __restrict__ du, float* __restrict__ dE) {
+  constexpr int D = 1024, NJ = D / 256;
+  constexpr float EPS = 1e-8f;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float u[NJ][4], ep[NJ][4], en[NJ][4];
+  float uu = 0.f, pp = 0.f, nn = 0.f, up = 0.f, un = 0.f;
+  const float* ur = users + b * D;
+  const float* pr = E + (int64_t)pos[b] * lde;
+  const float* nr_ = E + (int64_t)neg[b] * lde;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int e = j * 256 + lane * 4;
+    const float4 a = *reinterpret_cast<const float4*>(ur + e);
+    const float4 p = *reinterpret_cast<const float4*>(pr + e);
+    const float4 q = *reinterpret_cast<const float4*>(nr_ + e);
+    u[j][0] = a.x; u[j][1] = a.y; u[j][2] = a.z; u[j][3] = a.w;
+    ep[j][0] = p.x; ep[j][1] = p.y; ep[j][2] = p.z; ep[j][3] = p.w;
+    en[j][0] = q.x; en[j][1] = q.y; en[j][2] = q.z; en[j][3] = q.w;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      uu = fmaf(u[j][t], u[j][t], uu);
+      pp = fmaf(ep[j][t], ep[j][t], pp);
+      nn = fmaf(en[j][t], en[j][t], nn);
+      up = fmaf(u[j][t], ep[j][t], up);
+      un = fmaf(u[j][t], en[j][t], un);
+    }
+  }
+  uu = wave_sum(uu); pp = wave_sum(pp); nn = wave_sum(nn); up = wave_sum(up); un = wave_sum(un);
+  const float nu = sqrtf(uu), np_ = sqrtf(pp), nq = sqrtf(nn);
+  const float iu = 1.0f / fmaxf(nu, EPS), ip = 1.0f / fmaxf(np_, EPS), iq = 1.0f / fmaxf(nq, EPS);
+  const float sp = up * iu * ip, sn = un * iu * iq;
+  const float v = margin - (sp - sn);
+  const float act = v >= 0.f ? 1.0f : 0.0f;  // clamp_min backward passes where input >= min
+  const float gsp = -act / (float)B, gsn = act / (float)B;
+  if (lane == 0) {
+    if (s_out) { s_out[b] = sp; s_out[B + b] = sn; }
+    atomicAdd(loss, fmaxf(v, 0.f) / (float)B);
+  }
+  // d cos(u, e) / du = (ê - [|u| > eps] cos û) / max(|u|, eps)   (û = u / max(|u|, eps))
+  const float cu = nu > EPS ? 1.f : 0.f, cp = np_ > EPS ? 1.f : 0.f, cq = nq > EPS ? 1.f : 0.f;
+  float* dp = dE + (int64_t)pos[b] * lde;
+  float* dn = dE + (int64_t)neg[b] * lde;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int e = j * 256 + lane * 4;
+    float g[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float uh = u[j][t] * iu, ph = ep[j][t] * ip, qh = en[j][t] * iq;
+      g[t] = gsp * (ph - cu * sp * uh) * iu + gsn * (qh - cu * sn * uh) * iu;
+      atomicAdd(dp + e + t, gsp * (uh - cp * sp * ph) * ip);
+      atomicAdd(dn + e + t, gsn * (uh - cq * sn * qh) * iq);
+    }
+    *reinterpret_cast<float4*>(du + b * D + e) = make_float4(g[0], g[1], g[2], g[3]);
+  }
+}
+
+// ----------------------------------------------------------------- scatter add
+template <typename T>
+__global__ __launch_bounds__(256) void scatter_add_rows_kernel(int64_t n, int64_t dim, const T* __restrict__ src,
+                                                               int64_t lds, const int32_t* __restrict__ idx,
+                                                               float* __restrict__ dst, int64_t ldd) {
+  const int64_t i = blockIdx.x;
+  if (i >= n) return;
+  const int32_t r = idx[i];
+  if (r < 0) return;
+  for (int64_t c = threadIdx.x; c < dim; c += 256) atomicAdd(dst + (int64_t)r * ldd + c, ldf<T>(src + i * lds + c));
+}
+
+// ----------------------------------------------------------------- column sums
+// out[c] += sum_r src[r][c]; 64 rows x 256 columns per workgroup, atomics per column.
+template <typename T>
+__global__ __launch_bounds__(256) void col_sum_kernel(int64_t rows, int64_t cols, const T* __restrict__ src,
+                                                      int64_t lds, float* __restrict__ out) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int64_t r0 = (int64_t)blockIdx.y * 256;
+  const int64_t r1 = min(rows, r0 + 256);
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) s += ldf<T>(src + r * lds + c);
+  atomicAdd(out + c, s);
+}
+
+// ----------------------------------------------------------------- LN param grads
+// E = LN(x) * g + b  ->  dg += dE * xhat, db += dE (rows gathered by row_idx).
+// One wave per row; per-row partials folded into per-block LDS sums first.
+template <typename TI>
+__global__ __launch_bounds__(256) void ln_param_grad_kernel(int64_t n, const TI* __restrict__ x, int64_t ldx,
+                                                            const int64_t* __restrict__ row_idx, float eps,
+                                                            const float* __restrict__ dy, int64_t lddy,
+                                                            float* __restrict__ dg, float* __restrict__ db) {
+  constexpr int D = 1024, NJ = D / 256;
+  __shared__ float sg[D], sb[D];
+  for (int c = threadIdx.x; c < D; c += 256) { sg[c] = 0.f; sb[c] = 0.f; }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + wave; i < n; i += (int64_t)gridDim.x * 4) {
+    const int64_t row = row_idx ? row_idx[i] : i;
+    float v[NJ][4];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        v[j][t] = ldf<TI>(x + row * ldx + j * 256 + lane * 4 + t);
+        s += v[j][t];
+      }
+    const float mean = wave_sum(s) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { const float dd = v[j][t] - mean; q = fmaf(dd, dd, q); }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int e = j * 256 + lane * 4 + t;
+        const float g = dy[i * lddy + e];
+        atomicAdd(&sg[e], g * (v[j][t] - mean) * rstd);
+        atomicAdd(&sb[e], g);
+      }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    atomicAdd(dg + c, sg[c]);
+    atomicAdd(db + c, sb[c]);
+  }
+}
+
+// ----------------------------------------------------------------- grad norm + AdamW
+__global__ __launch_bounds__(256) void sumsq_kernel(int64_t n, const float* __restrict__ x, float* __restrict__ out) {
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) s = fmaf(x[i], x[i], s);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, s);
+}
+
+// torch.nn.utils.clip_grad_norm_(max_norm): coef = min(max_norm / (norm + 1e-6), 1)
+// torch.optim.AdamW (weight decay decoupled, bias-corrected):
+//   p *= 1 - lr wd;  m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2
+//   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+__global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    __bf16* __restrict__ p16, float lr, float b1, float b2,
+                                                    float eps, float wd, float bc1, float bc2s, float max_norm,
+                                                    const float* __restrict__ sumsq) {
+  float coef = 1.f;
+  if (sumsq) coef = fminf(max_norm / (sqrtf(*sumsq) + 1e-6f), 1.f);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float gi = g[i] * coef;
+    float pi = p[i] * (1.f - lr * wd);
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    pi -= (lr / bc1) * mi / (sqrtf(vi) / bc2s + eps);
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi;
+    if (p16) p16[i] = (__bf16)pi;
+  }
+}
+
+static int grid_for(int64_t n) { const int64_t g = (n + 255) / 256; return (int)(g < 4096 ? g : 4096); }
+
+}  // namespace nr
+
+using namespace nr;
+
+#define NR_DT2(dti, dto, ...)                                                              \
+  do {                                                                                     \
+    if (dti == NR_F32 && dto == NR_F32) { typedef float TI; typedef float TO; __VA_ARGS__; } \
+    else if (dti == NR_F32) { typedef float TI; typedef __bf16 TO; __VA_ARGS__; }           \
+    else if (dto == NR_F32) { typedef __bf16 TI; typedef float TO; __VA_ARGS__; }           \
+    else { typedef __bf16 TI; typedef __bf16 TO; __VA_ARGS__; }                            \
+  } while (0)
+#define NR_DT1(dt, ...)                                       \
+  do {                                                        \
+    if (dt == NR_F32) { typedef float T; __VA_ARGS__; }       \
+    else { typedef __bf16 T; __VA_ARGS__; }                   \
+  } while (0)
+#define NR_OKDT(d) ((d) == NR_F32 || (d) == NR_BF16)
+
+extern "C" int nr_gather_rows(int dtype_in, int dtype_out, int64_t n, int64_t dim, const void* src, int64_t lds,
+                              const int32_t* idx, void* dst, int64_t ldd, void* stream) {
+  clear_error();
+  NR_CHECK_ARG(NR_OKDT(dtype_in) && NR_OKDT(dtype_out), "nr_gather_rows: bad dtype");
+  NR_CHECK_ARG(n >= 0 && dim > 0 && lds >= dim && ldd >= dim, "nr_gather_rows: bad shape");
+  if (n == 0) return NR_OK;
+  NR_CHECK_ARG(src && dst, "nr_gather_rows: null pointer");
+  NR_DT2(dtype_in, dtype_out,
+         hipLaunchKernelGGL((gather_rows_kernel<TI, TO>), dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream, n,
+                            dim, (const TI*)src, lds, idx, (TO*)dst, ldd));
+  NR_CHECK_LAUNCH("nr_gather_rows");
+  return NR_OK;
+}
+
+extern "C" int nr_transpose(int dtype_in, int dtype_out, int64_t rows, int64_t cols, const void* src, int64_t lds,
+                            void* dst, int64_t ldd, void* stream) {
+  clear_error();
+  NR_CHECK_ARG(NR_OKDT(dtype_in) && NR_OKDT(dtype_out), "nr_transpose: bad dtype");
+  NR_CHECK_ARG(rows >= 0 && cols >= 0 && lds >= cols && ldd >= rows, "nr_transpose: bad shape");
+  if (rows == 0 || cols == 0) return NR_OK;
+  NR_CHECK_ARG(src && dst, "nr_transpose: null pointer");
+  NR_CHECK_ARG((rows + 63) / 64 <= 65535, "nr_transpose: too many rows");
+  const dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
+  NR_DT2(dtype_in, dtype_out,
+         hipLaunchKernelGGL((transpose_kernel<TI, TO>), grid, dim3(256), 0, (hipStream_t)stream, rows, cols,
+                            (const TI*)src, lds, (TO*)dst, ldd));
+  NR_CHECK_LAUNCH("nr_transpose");
+  return NR_OK;
+}
+
+extern "C" int nr_final_pool_fwd(int dtype, int64_t n_seg, const int64_t* off, const void* xp, int64_t ld,
+                                 float* users, float* z, void* stream) {
+  clear_error();
+  NR_CHECK_ARG(NR_OKDT(dtype) && n_seg >= 0 && ld >= 2048, "nr_final_pool_fwd: bad args");
+  if (n_seg == 0) return NR_OK;
+  NR_CHECK_ARG(off && xp && users && z, "nr_final_pool_fwd: null pointer");
+  NR_DT1(dtype, hipLaunchKernelGGL((final_pool_fwd_kernel<T>), dim3((unsigned)n_seg), dim3(256), 0,
+                                   (hipStream_t)stream, n_seg, off, (const T*)xp, ld, users, z));
+  NR_CHECK_LAUNCH("nr_final_pool_fwd");
+  return NR_OK;
+}
+
+extern "C" int nr_final_pool_bwd(int dtype, int64_t n_seg, const int64_t* off, int64_t n_rows, const void* xp,
+                                 int64_t ld, const float* users, const float* z, const float* du, void* dx,
+                                 int64_t lddx, void* dl, int64_t lddl, void* stream) {
+  clear_error();
+  NR_CHECK_ARG(NR_OKDT(dtype) && n_seg >= 0 && n_rows >= 0 && ld >= 2048 && lddx >= 1024 && lddl >= 1024,
+               "nr_final_pool_bwd: bad args");
+  if (n_seg == 0 && n_rows == 0) return NR_OK;
+  NR_CHECK_ARG(off && xp && users && z && du && dx && dl, "nr_final_pool_bwd: null pointer");
+  const unsigned grid = (unsigned)(n_seg + 64);  // 64 trailing blocks zero the padding rows
+  NR_DT1(dtype, hipLaunchKernelGGL((final_pool_bwd_kernel<T>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                                   n_seg, off, n_rows, (const T*)xp, ld, users, z, du, (T*)dx, lddx, (T*)dl, lddl));
+  NR_CHECK_LAUNCH("nr_final_pool_bwd");
+  return NR_OK;
+}
+
+extern "C" int nr_cosine_margin(int64_t B, const float* users, const float* E, int64_t lde, const int32_t* pos,
+                                const int32_t* neg, float margin, float* s_out, float* loss, float* du, float* dE,
+                                void* stream) {
+  clear_error();
+  NR_CHECK_ARG(B >= 0 && lde >= 1024 && lde % 4 == 0, "nr_cosine_margin: bad args");
+  if (B == 0) return NR_OK;
+  NR_CHECK_ARG(users && E && pos && neg && loss && du && dE, "nr_cosine_margin: null pointer");
+  hipLaunchKernelGGL(cosine_margin_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream, B,
+                     users, E, lde, pos, neg, margin, s_out, loss, du, dE);
+  NR_CHECK_LAUNCH("nr_cosine_margin");
+  return NR_OK;
+}
+
+extern "C" int nr_scatter_add_rows(int dtype, int64_t n, int64_t dim, const void* src, int64_t lds,
+                                   const int32_t* idx, float* dst, int64_t ldd, void* stream) {
+  clear_error();
+  NR_CHECK_ARG(NR_OKDT(dtype) && n >= 0 && dim > 0 && lds >= dim && ldd >= dim, "nr_scatter_add_rows: bad args");
+  if (n == 0) return NR_OK;
+  NR_CHECK_ARG(src && idx && dst, "nr_scatter_add_rows: null pointer");
+  NR_DT1(dtype, hipLaunchKernelGGL((scatter_add_rows_kernel<T>), dim3((unsigned)n), dim3(256), 0,
+                                   (hipStream_t)stream, n, dim, (const T*)src, lds, idx, dst, ldd));
+  NR_CHECK_LAUNCH("nr_scatter_add_rows");
+  return NR_OK;
+}
+
+extern "C" int nr_col_sum(int dtype, int64_t rows, int64_t cols, const void* src, int64_t lds, float* out,
+                          void* stream) {
+  clear_error();
+  NR_CHECK_ARG(NR_OKDT(dtype) && rows >= 0 && cols > 0 && lds >= cols, "nr_col_sum: bad args");
+  if (rows == 0) return NR_OK;
+  NR_CHECK_ARG(src && out, "nr_col_sum: null pointer");
+  NR_CHECK_ARG((rows + 255) / 256 <= 65535, "nr_col_sum: too many rows");
+  const dim3 grid((unsigned)((cols + 255) / 256), (unsigned)((rows + 255) / 256));
+  NR_DT1(dtype, hipLaunchKernelGGL((col_sum_kernel<T>), grid, dim3(256), 0, (hipStream_t)stream, rows, cols,
+                                   (const T*)src, lds, out));
+  NR_CHECK_LAUNCH("nr_col_sum");
+  return NR_OK;
+}
+
+extern "C" int nr_ln_param_grad(int dtype_in, int64_t n, int64_t dim, const void* x, int64_t ldx,
+                                const int64_t* row_idx, float eps, const float* dy, int64_t lddy, float* dgamma,
+                                float* dbeta, void* stream) {
+  clear_error();
+  NR_CHECK_ARG(dim == 1024, "nr_ln_param_grad: dim %lld unsupported", (long long)dim);
+  NR_CHECK_ARG(n >= 0 && ldx >= dim && lddy >= dim, "nr_ln_param_grad: bad args");
+  NR_CHECK_ARG(dtype_in == NR_F32 || dtype_in == NR_BF16 || dtype_in == NR_F16, "nr_ln_param_grad: bad dtype");
+  if (n == 0) return NR_OK;
+  NR_CHECK_ARG(x && dy && dgamma && dbeta, "nr_ln_param_grad: null pointer");
+  const unsigned grid = (unsigned)((n + 3) / 4 < 1024 ? (n + 3) / 4 : 1024);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_in == NR_F32)
+    hipLaunchKernelGGL((ln_param_grad_kernel<float>), dim3(grid), dim3(256), 0, s, n, (const float*)x, ldx, row_idx,
+                       eps, dy, lddy, dgamma, dbeta);
+  else if (dtype_in == NR_BF16)
+    hipLaunchKernelGGL((ln_param_grad_kernel<__bf16>), dim3(grid), dim3(256), 0, s, n, (const __bf16*)x, ldx,
+                       row_idx, eps, dy, lddy, dgamma, dbeta);
+  else
+    hipLaunchKernelGGL((ln_param_grad_kernel<_Float16>), dim3(grid), dim3(256), 0, s, n, (const _Float16*)x, ldx,
+                       row_idx, eps, dy, lddy, dgamma, dbeta);
+  NR_CHECK_LAUNCH("nr_ln_param_grad");
+  return NR_OK;
+}
+
+extern "C" int nr_sumsq(int64_t n, const float* x, float* out, void* stream) {
+  clear_error();
+  NR_CHECK_ARG(n >= 0, "nr_sumsq: bad n");
+  if (n == 0) return NR_OK;
+  NR_CHECK_ARG(x && out, "nr_sumsq: null pointer");
+  hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, x, out);
+  NR_CHECK_LAUNCH("nr_sumsq");
+  return NR_OK;
+}
+
+extern "C" int nr_adamw(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf16, int64_t step,
+                        float lr, float beta1, float beta2, float eps, float weight_decay, float max_norm,
+                        const float* sumsq, void* stream) {
+  clear_error();
+  NR_CHECK_ARG(n >= 0 && step >= 1, "nr_adamw: bad args");
+  if (n == 0) return NR_OK;
+  NR_CHECK_ARG(p && g && m && v, "nr_adamw: null pointer");
+  const float bc1 = (float)(1.0 - pow((double)beta1, (double)step));
+  const float bc2s = (float)sqrt(1.0 - pow((double)beta2, (double)step));
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v,
+                     (__bf16*)p_bf16, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, max_norm, sumsq);
+  NR_CHECK_LAUNCH("nr_adamw");
+  return NR_OK;
+}

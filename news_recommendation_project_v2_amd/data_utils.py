@@ -268,3 +268,131 @@ def token_attention_eval_collate_fn(input, conn):
     """(f32 token states [B, L, D], int32 mask [B, L]) of a batch of news (data_utils.py:929-933)."""
     res = get_embeds_from_db(conn, input)
     return res["embeddings"].to(dtype=torch.float32), res["attention_mask"].to(dtype=torch.int32)
+
+
+# --------------------------------------------------------------- training data (config 5)
+def split_impressions_pos_neg(rng: np.random.Generator, grouped_news_rev_index, labels,
+                              max_neg_ratio: Optional[float] = None, max_pos_ratio: Optional[float] = None) -> np.ndarray:
+    """Balanced (positive, negative, row) triples per impression (data_utils.py:337-388).
+
+    Per impression, with P positives and Q negatives, k = max(P, Q) (or the
+    ratio-capped value): the larger side is sampled without replacement down
+    to k, the smaller side is topped up to k by sampling with replacement and
+    shuffled.  The generator calls (choice / permutation, same arguments, same
+    order) are the reference's, so a shared ``rng`` yields identical triples.
+    Returns int32 [3, sum k]: positive news, negative news, impression row.
+    """
+    pos_all, neg_all, counts = [], [], []
+    for i, row in enumerate(labels):
+        lab = np.asarray(row)
+        cand = np.asarray(grouped_news_rev_index[i])
+        n_pos = int(lab.sum())
+        n_neg = len(lab) - n_pos
+        k = max(n_pos, n_neg)
+        if max_neg_ratio or max_pos_ratio:
+            if max_neg_ratio and n_neg * max_neg_ratio > n_pos:
+                k = int(n_pos / max_neg_ratio)
+            elif max_pos_ratio and n_pos * max_pos_ratio > n_neg:
+                k = int(n_neg / max_pos_ratio)
+        pos = [cand[j] for j in range(len(lab)) if lab[j] != 0]
+        neg = [cand[j] for j in range(len(lab)) if lab[j] == 0]
+        if n_neg >= k:
+            neg = rng.choice(neg, size=k, replace=False)
+            pos = rng.permutation(np.append(pos, rng.choice(pos, k - n_pos)))
+        else:
+            pos = rng.choice(pos, size=k, replace=False)
+            neg = rng.permutation(np.append(neg, rng.choice(neg, k - n_neg)))
+        pos_all.extend(np.asarray(pos).tolist())
+        neg_all.extend(np.asarray(neg).tolist())
+        counts.append(k)
+    rows = np.repeat(np.arange(len(counts)), counts).astype(np.int32)
+    return np.stack([np.array(pos_all, dtype=np.int32), np.array(neg_all, dtype=np.int32), rows])
+
+
+class FinalAttentionTrainDataset(Dataset):
+    """(history group, positive, negative) training rows (data_utils.py:581-645).
+
+    ``reset`` (called once per epoch) permutes impressions, draws the balanced
+    pairs, and permutes whole batches except the last (ragged) one, with the
+    reference's generator call order."""
+
+    def __init__(self, history_rev_index, history_len_list, news_rev_index, impression_len_list, labels,
+                 batch_size: int, max_neg_raio: Optional[float] = None, max_pos_ratio: Optional[float] = None,
+                 rng=None):
+        assert len(history_len_list) == len(impression_len_list), "Number of rows should match between history and news"
+        assert sum(impression_len_list) == len(news_rev_index), \
+            "Number of impressions should match length of impression list"
+        self.group_history = group_items(history_rev_index, history_len_list)
+        self.batch_size = batch_size
+        self.labels = labels
+        self.news_rev_index = news_rev_index
+        self.impression_len_list = impression_len_list
+        self.rng = rng if rng is not None else np.random.default_rng(1234)
+        self.max_neg_ratio = max_neg_raio
+        self.max_pos_ratio = max_pos_ratio
+        self.reset()
+
+    def __len__(self):
+        return len(self.pos_neg_indices)
+
+    def __getitem__(self, idx):
+        p, n, r = self.pos_neg_indices[idx]
+        return self.group_history[r], p, n
+
+    def reset(self):
+        perm = self.rng.permutation(len(self.labels))
+        trip = split_impressions_pos_neg(self.rng, group_items(self.news_rev_index, self.impression_len_list)[perm],
+                                         self.labels[perm], self.max_neg_ratio, self.max_pos_ratio)
+        trip[2] = perm[trip[2]]
+        total = trip.shape[1]
+        n_batches = -(total // -self.batch_size)
+        order = self.rng.permutation(n_batches - 1).tolist() + [n_batches - 1]
+        sel = (np.asarray(order, dtype=np.int64)[:, None] * self.batch_size
+               + np.arange(self.batch_size)[None, :]).ravel()[:total]
+        self.pos_neg_indices = trip[:, sel].T
+
+    def batches(self):
+        """Row ranges of the DataLoader batches (shuffle=False, in order)."""
+        n = len(self)
+        return [(s, min(n, s + self.batch_size)) for s in range(0, n, self.batch_size)]
+
+
+def attention_attention_train_collate_fn(input, conn):
+    """Batch -> (token states, token mask, padded history indices, history mask,
+    pos ‖ neg indices), all indices into the batch's sorted unique news
+    (data_utils.py:893-915)."""
+    from .config import NEWS_TEXT_MAXLEN
+    grouped_history, pos, neg = zip(*input)
+    lens = [len(h) for h in grouped_history]
+    allidx = np.concatenate(list(grouped_history) + [np.asarray(pos), np.asarray(neg)])
+    uniq, rev = np.unique(allidx, return_inverse=True)
+    states = get_embeds_from_db(conn, uniq)
+    cuts = np.cumsum(lens)
+    hist_rev = np.split(rev[:cuts[-1]] if len(cuts) else rev[:0], cuts[:-1])
+    padded = pad_to_maxlen(hist_rev)
+    return (states["embeddings"].to(dtype=torch.float32)[:, :NEWS_TEXT_MAXLEN],
+            states["attention_mask"].to(dtype=torch.int32)[:, :NEWS_TEXT_MAXLEN],
+            torch.tensor(padded["indices"], dtype=torch.int32),
+            torch.tensor(padded["attention_mask"], dtype=torch.int32),
+            torch.tensor(rev[len(rev) - 2 * len(pos):], dtype=torch.int32))
+
+
+def train_batch_csr(conn, rows, maxlen: Optional[int] = None):
+    """Same batch in the device-friendly CSR form of train_step.TrainBatch:
+    (last valid token row per unique news [U, D] (fp16 as stored), history
+    indices int32 [Hs], offsets int64 [B+1], pos int32 [B], neg int32 [B]).
+    Only the last valid token matters to the token model (attention.py:193 +
+    last_token_pool), truncated at NEWS_TEXT_MAXLEN like the reference collate."""
+    from .config import NEWS_TEXT_MAXLEN
+    maxlen = maxlen or NEWS_TEXT_MAXLEN
+    grouped_history, pos, neg = zip(*rows)
+    lens = np.array([len(h) for h in grouped_history], dtype=np.int64)
+    allidx = np.concatenate(list(grouped_history) + [np.asarray(pos), np.asarray(neg)])
+    uniq, rev = np.unique(allidx, return_inverse=True)
+    ids = ",".join(str(int(i) + 1) for i in uniq)
+    res = conn.execute(f"SELECT data FROM tensors WHERE id IN ({ids}) ORDER BY id;").fetchall()
+    last = torch.stack([t[min(len(t), maxlen) - 1] for t in (read_token_blob(r[0]) for r in res)])
+    Hs = int(lens.sum())
+    B = len(pos)
+    return (last, rev[:Hs].astype(np.int32), lengths_to_offsets(lens), rev[Hs:Hs + B].astype(np.int32),
+            rev[Hs + B:].astype(np.int32))

@@ -296,3 +296,122 @@ def attention_varlen(qkv: torch.Tensor, cu_seqlens: torch.Tensor, qblock_off: to
     _lib.call("nr_attention_varlen", _dtype(qkv, "qkv"), cu_seqlens.numel() - 1, n_qblocks, _ptr(qkv),
               _ptr(cu_seqlens), _ptr(qblock_off), _ptr(out), _stream(dev))
     return out
+
+
+# ------------------------------------------------------------------ training step (config 5)
+def _dt(t: torch.Tensor, name: str) -> int:
+    return _dtype(t, name)
+
+
+def gemm_relu_dropout(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], seed: int, p: float,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = relu(a @ w.T + bias) * keep / (1 - p), keep from the (seed, row, col) hash stream."""
+    dev = _dev(a, w, bias, out)
+    M, K = a.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=a.dtype, device=dev)
+    _lib.call("nr_gemm_relu_dropout", _dt(a, "a"), _dt(out, "out"), M, N, K, _ptr(a), _rowmajor(a, "a"), _ptr(w),
+              _rowmajor(w, "w"), _ptr(bias), _ptr(out), _rowmajor(out, "out"), ctypes.c_uint64(seed & (2**64 - 1)),
+              ctypes.c_float(p), _stream(dev))
+    return out
+
+
+def gemm_drelu(a: torch.Tensor, w: torch.Tensor, y: torch.Tensor, scale: float,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = (y > 0) ? (a @ w.T) * scale : 0 (backward of relu + dropout, y = forward output)."""
+    dev = _dev(a, w, y, out)
+    M, K = a.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=y.dtype, device=dev)
+    _lib.call("nr_gemm_drelu", _dt(a, "a"), _dt(out, "out"), M, N, K, _ptr(a), _rowmajor(a, "a"), _ptr(w),
+              _rowmajor(w, "w"), _ptr(y), _rowmajor(y, "y"), _ptr(out), _rowmajor(out, "out"), ctypes.c_float(scale),
+              _stream(dev))
+    return out
+
+
+def gather_rows(src: torch.Tensor, idx: Optional[torch.Tensor], n: Optional[int] = None,
+                out_dtype: Optional[torch.dtype] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    dev = _dev(src, idx, out)
+    n = idx.numel() if idx is not None else (n if n is not None else src.shape[0])
+    if idx is not None and (idx.dtype != torch.int32 or not idx.is_contiguous()):
+        raise _lib.NewsRecHIPError("gather_rows: idx must be contiguous int32")
+    dim = src.shape[1]
+    if out is None:
+        out = torch.empty((n, dim), dtype=out_dtype or src.dtype, device=dev)
+    _lib.call("nr_gather_rows", _dt(src, "src"), _dt(out, "out"), n, dim, _ptr(src), _rowmajor(src, "src"), _ptr(idx),
+              _ptr(out), _rowmajor(out, "out"), _stream(dev))
+    return out
+
+
+def transpose(src: torch.Tensor, out_dtype: Optional[torch.dtype] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    dev = _dev(src, out)
+    rows, cols = src.shape
+    if out is None:
+        out = torch.empty((cols, rows), dtype=out_dtype or src.dtype, device=dev)
+    _lib.call("nr_transpose", _dt(src, "src"), _dt(out, "out"), rows, cols, _ptr(src), _rowmajor(src, "src"),
+              _ptr(out), _rowmajor(out, "out"), _stream(dev))
+    return out
+
+
+def final_pool_fwd(xp: torch.Tensor, off: torch.Tensor):
+    dev = _dev(xp, off)
+    n_seg = off.numel() - 1
+    users = torch.empty((n_seg, 1024), dtype=torch.float32, device=dev)
+    z = torch.empty_like(users)
+    _lib.call("nr_final_pool_fwd", _dt(xp, "xp"), n_seg, _ptr(off), _ptr(xp), _rowmajor(xp, "xp"), _ptr(users),
+              _ptr(z), _stream(dev))
+    return users, z
+
+
+def final_pool_bwd(xp: torch.Tensor, off: torch.Tensor, users: torch.Tensor, z: torch.Tensor, du: torch.Tensor,
+                   dx: torch.Tensor, dw: torch.Tensor) -> None:
+    dev = _dev(xp, off, users, z, du, dx, dw)
+    _lib.call("nr_final_pool_bwd", _dt(xp, "xp"), off.numel() - 1, _ptr(off), dx.shape[0], _ptr(xp),
+              _rowmajor(xp, "xp"), _ptr(users), _ptr(z), _ptr(du), _ptr(dx), _rowmajor(dx, "dx"), _ptr(dw),
+              _rowmajor(dw, "dw"), _stream(dev))
+
+
+def cosine_margin(users: torch.Tensor, E: torch.Tensor, pos: torch.Tensor, neg: torch.Tensor, margin: float,
+                  loss: torch.Tensor, du: torch.Tensor, dE: torch.Tensor,
+                  s_out: Optional[torch.Tensor] = None) -> None:
+    dev = _dev(users, E, pos, neg, loss, du, dE, s_out)
+    _lib.call("nr_cosine_margin", users.shape[0], _ptr(users), _ptr(E), _rowmajor(E, "E"), _ptr(pos), _ptr(neg),
+              ctypes.c_float(margin), _ptr(s_out), _ptr(loss), _ptr(du), _ptr(dE), _stream(dev))
+
+
+def scatter_add_rows(src: torch.Tensor, idx: torch.Tensor, dst: torch.Tensor) -> None:
+    dev = _dev(src, idx, dst)
+    _lib.call("nr_scatter_add_rows", _dt(src, "src"), idx.numel(), src.shape[1], _ptr(src), _rowmajor(src, "src"),
+              _ptr(idx), _ptr(dst), _rowmajor(dst, "dst"), _stream(dev))
+
+
+def col_sum(src: torch.Tensor, out: torch.Tensor) -> None:
+    dev = _dev(src, out)
+    _lib.call("nr_col_sum", _dt(src, "src"), src.shape[0], src.shape[1], _ptr(src), _rowmajor(src, "src"), _ptr(out),
+              _stream(dev))
+
+
+def ln_param_grad(x: torch.Tensor, row_idx: Optional[torch.Tensor], eps: float, dy: torch.Tensor,
+                  dgamma: torch.Tensor, dbeta: torch.Tensor) -> None:
+    dev = _dev(x, row_idx, dy, dgamma, dbeta)
+    dt = {torch.float32: _lib.NR_F32, torch.bfloat16: _lib.NR_BF16, torch.float16: _lib.NR_F16}[x.dtype]
+    n = row_idx.numel() if row_idx is not None else x.shape[0]
+    _lib.call("nr_ln_param_grad", dt, n, x.shape[1], _ptr(x), _rowmajor(x, "x"), _ptr(row_idx), ctypes.c_float(eps),
+              _ptr(dy), _rowmajor(dy, "dy"), _ptr(dgamma), _ptr(dbeta), _stream(dev))
+
+
+def sumsq(x: torch.Tensor, out: torch.Tensor) -> None:
+    dev = _dev(x, out)
+    _lib.call("nr_sumsq", x.numel(), _ptr(x), _ptr(out), _stream(dev))
+
+
+def adamw(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, step: int, lr: float,
+          betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.01, max_norm: float = 0.0,
+          sumsq_t: Optional[torch.Tensor] = None, p_bf16: Optional[torch.Tensor] = None) -> None:
+    dev = _dev(p, g, m, v, sumsq_t, p_bf16)
+    _lib.call("nr_adamw", p.numel(), _ptr(p), _ptr(g), _ptr(m), _ptr(v), _ptr(p_bf16), step, ctypes.c_float(lr),
+              ctypes.c_float(betas[0]), ctypes.c_float(betas[1]), ctypes.c_float(eps), ctypes.c_float(weight_decay),
+              ctypes.c_float(max_norm), _ptr(sumsq_t), _stream(dev))

@@ -1,0 +1,248 @@
+"""One training step of config 5 on the MI355X.
+
+Replaces the body of ``AttentionAttentionTrainer.train_one_epoch``
+(trainer.py:1030-1071) for one batch:
+
+  first_res  = token_model(tok, mask)                  # = g_mlp_LN(last valid token)
+  second_res = first_res[hist] * hist_mask             # padded [B, h_max, D]
+  outputs    = final_attention(second_res, hist_mask)  # train mode: dropout p = 0.1
+  res        = cosine(outputs.repeat(2, 1), first_res[pos ‖ neg])
+  loss       = MarginRankingLoss(2)(res[:B], res[B:], 1)
+  loss.backward(); clip_grad_norm_(0.5); AdamW(lr 1e-6).step()
+
+as a fixed kernel sequence (no autograd):
+  * the token model is ``nr_gather_layernorm`` of the U unique news' last rows;
+  * FinalAttention runs once per VALID history slot (Hs = sum h_i rows packed in
+    CSR order, zero-padded to a multiple of 64): the reference's padded slots
+    are masked to zero weight, so they carry no gradient and skipping them is
+    exact; dropout is fused into the ReLU GEMM epilogues with a counter-hash
+    stream (``nr_gemm_relu_dropout``), its backward into the data-grad GEMMs
+    (``nr_gemm_drelu``: the mask is recovered from the saved outputs);
+  * data-grad GEMMs use transposed weights, weight-grad GEMMs transposed
+    activations / grads, all on the C = A·Wᵀ MFMA kernel (bf16 or exact f32);
+  * pooling forward / backward, cosine + margin loss, scatter-add of the
+    history gradient, bias and LayerNorm-parameter reductions, the global grad
+    norm and AdamW (with the clip coefficient folded in) are HIP kernels.
+
+Parameters live in ONE flat f32 buffer (master weights; the torch modules'
+parameters are re-pointed at views of it, so ``state_dict()`` is always
+current), with a flat bf16 mirror for the bf16 compute dtype.  Only the
+parameters that receive gradients are in it — exactly the set torch's AdamW
+updates (the token model's attention / g_mlp weights and attn_layernorm get no
+gradient because MyLayer discards them, attention.py:193).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import ops
+from ._lib import NewsRecHIPError
+
+D = 1024
+H = 4096
+DROP_P = 0.1
+MARGIN = 2.0  # MarginRankingLoss(2), trainer.py:985
+
+
+def _pad64(n: int) -> int:
+    return max(64, (n + 63) // 64 * 64)
+
+
+@dataclass
+class TrainBatch:
+    """Device-side batch: the output of ``attention_attention_train_collate_fn``
+    in CSR form (data_utils.py:893-915).
+
+    tok_last  [U, D] f32/f16  each unique news' last valid token state
+    hist_idx  [Hs] int32      history slots, indices into the U rows
+    hist_off  [B+1] int64     CSR offsets of the B batch rows
+    pos, neg  [B] int32       positive / negative news, indices into the U rows
+    """
+    tok_last: torch.Tensor
+    hist_idx: torch.Tensor
+    hist_off: torch.Tensor
+    pos: torch.Tensor
+    neg: torch.Tensor
+
+    @property
+    def B(self) -> int:
+        return self.pos.numel()
+
+
+class FinalAttentionTrainStep:
+    """Owns the flat parameters, AdamW state and scratch of the config-5 step."""
+
+    def __init__(self, token_model, final_attention, dtype: torch.dtype = torch.bfloat16, lr: float = 1e-6,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.01, max_norm: float = 0.5,
+                 dropout: float = DROP_P, seed: int = 1234, device=None):
+        if dtype not in (torch.float32, torch.bfloat16):
+            raise NewsRecHIPError("train step dtype must be float32 or bfloat16")
+        layers = list(token_model.encoder.layer)
+        if len(layers) != 1:
+            raise NewsRecHIPError("training supports NUM_HIDDEN_LAYERS == 1 (config.py:35)")
+        self.device = device or torch.device("cuda")
+        self.dtype = dtype
+        self.lr, self.betas, self.eps, self.wd, self.max_norm = lr, betas, eps, weight_decay, max_norm
+        self.p = dropout
+        self.seed = seed
+        self.step_count = 0
+        self.ln = layers[0].g_mlp_layernorm
+        self.ln_eps = float(self.ln.eps)
+        fa = final_attention
+        self.names = ["ln.weight", "ln.bias"]
+        params = [self.ln.weight, self.ln.bias]
+        for i in range(1, 6):
+            lin = getattr(fa, f"linear{i}")
+            self.names.append(f"linear{i}.weight")
+            params.append(lin.weight)
+            if lin.bias is not None:
+                self.names.append(f"linear{i}.bias")
+                params.append(lin.bias)
+        sizes = [p.numel() for p in params]
+        # 16-B aligned slices (64 floats) so every view is a valid GEMM operand
+        offs, o = [], 0
+        for n in sizes:
+            offs.append(o)
+            o += (n + 63) // 64 * 64
+        self.n_flat = o
+        dev = self.device
+        self.flat = torch.zeros(o, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros_like(self.flat)
+        self.m = torch.zeros_like(self.flat)
+        self.v = torch.zeros_like(self.flat)
+        self.flat16 = torch.zeros(o, dtype=torch.bfloat16, device=dev) if dtype == torch.bfloat16 else None
+        self.views, self.gviews, self.cviews = {}, {}, {}
+        with torch.no_grad():
+            for name, prm, off, n in zip(self.names, params, offs, sizes):
+                v = self.flat[off:off + n].view(prm.shape)
+                v.copy_(prm.detach().to(dev, torch.float32))
+                prm.data = v  # the module now reads the master weights
+                self.views[name] = v
+                self.gviews[name] = self.grad[off:off + n].view(prm.shape)
+                self.cviews[name] = (self.flat16[off:off + n].view(prm.shape) if self.flat16 is not None else v)
+            if self.flat16 is not None:
+                self.flat16.copy_(self.flat)
+        self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._ws = {}
+
+    # ------------------------------------------------------------------ helpers
+    def _buf(self, name: str, shape, dtype) -> torch.Tensor:
+        t = self._ws.get(name)
+        n = int(np.prod(shape))
+        if t is None or t.numel() < n or t.dtype != dtype:
+            t = torch.empty(max(n, 1), dtype=dtype, device=self.device)
+            self._ws[name] = t
+        return t[:n].view(shape)
+
+    def W(self, i: int) -> torch.Tensor:
+        return self.cviews[f"linear{i}.weight"]
+
+    def b(self, i: int) -> Optional[torch.Tensor]:
+        return self.views.get(f"linear{i}.bias")
+
+    def layer_seed(self, layer: int) -> int:
+        """Dropout stream of one forward layer in the current step."""
+        return (self.seed * 1_000_003 + self.step_count * 7919 + layer * 104_729) & (2**64 - 1)
+
+    # ------------------------------------------------------------------ step
+    def forward_backward(self, batch: TrainBatch):
+        """Loss (device scalar) and gradients into ``self.grad`` (zeroed first).
+        Returns (loss, users, E) for inspection."""
+        dt, dev = self.dtype, self.device
+        U = batch.tok_last.shape[0]
+        B = batch.B
+        Hs = batch.hist_idx.numel()
+        Hp = _pad64(Hs)
+        scale = 1.0 / (1.0 - self.p)
+        self.grad.zero_()
+        self.loss.zero_()
+        # ---- forward
+        gam = self.views["ln.weight"].view(1, D)
+        bet = self.views["ln.bias"].view(1, D)
+        E = ops.gather_layernorm(batch.tok_last, None, gam, bet, self.ln_eps, out=self._buf("E", (U, D), torch.float32))
+        idx = self._buf("idx", (Hp,), torch.int32)
+        idx.fill_(-1)
+        idx[:Hs].copy_(batch.hist_idx)
+        S = ops.gather_rows(E, idx, out_dtype=dt, out=self._buf("S", (Hp, D), dt))
+        X1 = ops.gemm_relu_dropout(S, self.W(1), self.b(1), self.layer_seed(1), self.p, out=self._buf("X1", (Hp, H), dt))
+        X2 = ops.gemm_relu_dropout(X1, self.W(2), self.b(2), self.layer_seed(2), self.p,
+                                   out=self._buf("X2", (Hp, H), dt))
+        XP = self._buf("XP", (Hp, 2 * D), dt)
+        X = XP[:, :D]
+        ops.gemm(X2, self.W(3), self.b(3), out=X)
+        Y = ops.gemm_relu_dropout(X, self.W(4), self.b(4), self.layer_seed(3), self.p, out=self._buf("Y", (Hp, H), dt))
+        ops.gemm(Y, self.W(5), None, epilogue="exp", out=XP[:, D:])
+        users, z = ops.final_pool_fwd(XP, batch.hist_off)
+        # ---- loss + backward
+        du = self._buf("du", (B, D), torch.float32)
+        dE = self._buf("dE", (U, D), torch.float32)
+        dE.zero_()
+        ops.cosine_margin(users, E, batch.pos, batch.neg, MARGIN, self.loss, du, dE)
+        dXp = self._buf("dXp", (Hp, D), dt)
+        dL = self._buf("dL", (Hp, D), dt)
+        ops.final_pool_bwd(XP, batch.hist_off, users, z, du, dXp, dL)
+        T = lambda src, name: ops.transpose(src, out=self._buf(name, (src.shape[1], src.shape[0]), dt))
+        # linear5 (no bias): logits = Y W5ᵀ
+        W5t = T(self.W(5), "W5t")
+        dY = ops.gemm_drelu(dL, W5t, Y, scale, out=self._buf("dY", (Hp, H), dt))     # = dZ4
+        self._wgrad(dL, Y, "linear5.weight")
+        # linear4: Y = dropout(relu(X W4ᵀ + b4))
+        W4t = T(self.W(4), "W4t")
+        dX = ops.gemm(dY, W4t, None, epilogue="resadd", residual=dXp, out=self._buf("dX", (Hp, D), dt))
+        self._wgrad(dY, X, "linear4.weight")
+        ops.col_sum(dY, self.gviews["linear4.bias"])
+        # linear3: X = X2 W3ᵀ + b3
+        W3t = T(self.W(3), "W3t")
+        dZ2 = ops.gemm_drelu(dX, W3t, X2, scale, out=self._buf("dZ2", (Hp, H), dt))
+        self._wgrad(dX, X2, "linear3.weight")
+        ops.col_sum(dX, self.gviews["linear3.bias"])
+        # linear2
+        W2t = T(self.W(2), "W2t")
+        dZ1 = ops.gemm_drelu(dZ2, W2t, X1, scale, out=self._buf("dZ1", (Hp, H), dt))
+        self._wgrad(dZ2, X1, "linear2.weight")
+        ops.col_sum(dZ2, self.gviews["linear2.bias"])
+        # linear1
+        W1t = T(self.W(1), "W1t")
+        dS = ops.gemm(dZ1, W1t, None, out=self._buf("dS", (Hp, D), dt))
+        self._wgrad(dZ1, S, "linear1.weight")
+        ops.col_sum(dZ1, self.gviews["linear1.bias"])
+        # history gather -> unique news rows -> token LayerNorm params
+        ops.scatter_add_rows(dS[:Hs], batch.hist_idx, dE)
+        ops.ln_param_grad(batch.tok_last, None, self.ln_eps, dE, self.gviews["ln.weight"], self.gviews["ln.bias"])
+        return self.loss, users, E
+
+    def _wgrad(self, dOut: torch.Tensor, Xin: torch.Tensor, name: str) -> None:
+        """grad[name] = dOutᵀ · Xin  ([N_out, Hp] x [Hp, K_in])."""
+        dt = self.dtype
+        dOt = ops.transpose(dOut, out=self._buf("wg_a", (dOut.shape[1], dOut.shape[0]), dt))
+        Xt = ops.transpose(Xin, out=self._buf("wg_b", (Xin.shape[1], Xin.shape[0]), dt))
+        ops.gemm(dOt, Xt, None, out=self.gviews[name])
+
+    def optimizer_step(self) -> None:
+        """clip_grad_norm_(max_norm) + AdamW, one launch each (trainer.py:1067-1069)."""
+        self.step_count += 1
+        self.sumsq.zero_()
+        ops.sumsq(self.grad, self.sumsq)
+        ops.adamw(self.flat, self.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps, self.wd,
+                  self.max_norm, self.sumsq if self.max_norm > 0 else None, self.flat16)
+
+    def step(self, batch: TrainBatch) -> torch.Tensor:
+        """One full step; returns this step's loss as its own device scalar."""
+        loss, _, _ = self.forward_backward(batch)
+        out = loss.clone()
+        self.optimizer_step()
+        return out
+
+    def grad_dict(self) -> dict:
+        return {k: v for k, v in self.gviews.items()}
+
+    def flops_per_step(self, Hs: int) -> float:
+        """MFMA FLOPs of one step (forward + data-grad + weight-grad GEMMs)."""
+        Hp = _pad64(Hs)
+        fwd = 2.0 * Hp * (D * H + H * H + H * D + D * H + H * D)
+        return 3.0 * fwd

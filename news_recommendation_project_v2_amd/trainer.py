@@ -1,0 +1,109 @@
+"""Config-5 trainer (reference trainer.py:952-1206, ``AttentionAttentionTrainer``).
+
+Same constructor arguments and the same epoch loop: the training set is
+``FinalAttentionTrainDataset`` (balanced positive / negative pairs per
+impression, re-drawn every epoch with the shared ``rng``), batches come in
+DataLoader order (shuffle=False, the dataset already permutes batches), token
+states are read from the sqlite store, and every batch runs one
+forward + backward + clip + AdamW step — here ``train_step.FinalAttentionTrainStep``
+on the MI355X instead of torch autograd.  Per epoch the mean loss (weighted by
+batch rows, trainer.py:1073-1074) is appended to
+``{log_dir}/train_final_history_score.jsonl`` and the two state dicts are
+saved as ``{ckpt_dir}/Epoch_{i}.pt`` (locally: the Azure blob upload of
+trainer.py:1172-1197 is out of scope).
+
+The reference sizes the batch with a GPU OOM probe
+(batch_size_finder.get_attention_attention_train_batch_size); here it is an
+argument (HBM is not the constraint at these shapes).
+"""
+from __future__ import annotations
+
+import json
+import math
+import sqlite3
+from datetime import datetime
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .config import DEVICE
+from .data_utils import FinalAttentionTrainDataset, lengths_to_offsets, train_batch_csr
+from .train_step import FinalAttentionTrainStep, TrainBatch
+
+DEFAULT_TRAIN_BATCH = 256
+
+
+class AttentionAttentionTrainer:
+    def __init__(self, db_name: str, token_attention_model: torch.nn.Module, final_attention_model: torch.nn.Module,
+                 train_history_rev_index: np.ndarray, train_history_len_list: np.ndarray,
+                 train_news_rev_index: np.ndarray, train_impression_len_list: np.ndarray, train_labels: np.ndarray,
+                 log_dir: Optional[Path] = None, token_ckpt_dir: Optional[Path] = None,
+                 final_attn_ckpt_dir: Optional[Path] = None, exp_name: str = "",
+                 max_neg_ratio: Optional[float] = None, max_pos_ratio: Optional[float] = None,
+                 rng: Optional[np.random.Generator] = None, batch_size: int = DEFAULT_TRAIN_BATCH,
+                 dtype: torch.dtype = torch.float32, lr: float = 1e-6, dropout: float = 0.1, seed: int = 1234):
+        self.rng = rng if rng is not None else np.random.default_rng(1234)
+        self.log_dir = log_dir
+        self.exp_name = exp_name
+        self.token_ckpt_dir = token_ckpt_dir
+        self.final_attn_ckpt_dir = final_attn_ckpt_dir
+        self.token_attention_model = token_attention_model
+        self.final_attention_model = final_attention_model
+        self.train_batch_size = batch_size
+        self.engine = FinalAttentionTrainStep(token_attention_model, final_attention_model, dtype=dtype, lr=lr,
+                                              dropout=dropout, seed=seed, device=DEVICE)
+        self.train_dataset = FinalAttentionTrainDataset(
+            history_rev_index=train_history_rev_index, history_len_list=train_history_len_list,
+            news_rev_index=train_news_rev_index, impression_len_list=train_impression_len_list,
+            labels=train_labels, batch_size=batch_size, max_neg_raio=max_neg_ratio, max_pos_ratio=max_pos_ratio,
+            rng=self.rng)
+        self.connection = sqlite3.connect(str(db_name))
+
+    def device_batch(self, lo: int, hi: int) -> TrainBatch:
+        rows = [self.train_dataset[i] for i in range(lo, hi)]
+        last, hidx, hoff, pos, neg = train_batch_csr(self.connection, rows)
+        d = DEVICE
+        return TrainBatch(tok_last=last.to(d).contiguous(), hist_idx=torch.as_tensor(hidx).to(d),
+                          hist_off=torch.as_tensor(hoff).to(d), pos=torch.as_tensor(pos).to(d),
+                          neg=torch.as_tensor(neg).to(d))
+
+    def train_one_epoch(self) -> float:
+        self.token_attention_model.train()
+        self.final_attention_model.train()
+        running_loss, running_count = 0.0, 0
+        losses = []
+        for lo, hi in self.train_dataset.batches():
+            batch = self.device_batch(lo, hi)
+            losses.append((self.engine.step(batch), hi - lo))
+        for loss, n in losses:  # one sync at the end of the epoch
+            v = float(loss.item()) if not isinstance(loss, float) else loss
+            if math.isnan(v):
+                print("Nan loss found. Please check")
+                break
+            running_loss += v * n
+            running_count += n
+        self._invalidate_eval_cache()
+        return running_loss / max(running_count, 1)
+
+    def _invalidate_eval_cache(self):
+        if hasattr(self.final_attention_model, "_hip_cache"):
+            self.final_attention_model._hip_cache = {}
+
+    def train(self, num_epochs: int):
+        for i in range(num_epochs):
+            loss = self.train_one_epoch()
+            print(i + 1, loss)
+            if self.log_dir:
+                Path(self.log_dir).mkdir(parents=True, exist_ok=True)
+                with open(Path(self.log_dir) / "train_final_history_score.jsonl", "a") as f:
+                    f.write(json.dumps({"timestamp": datetime.now().isoformat(), "exp_name": self.exp_name,
+                                        "epoch": i + 1, "loss": loss}) + "\n")
+            for d, m in ((self.token_ckpt_dir, self.token_attention_model),
+                         (self.final_attn_ckpt_dir, self.final_attention_model)):
+                if d:
+                    Path(d).mkdir(parents=True, exist_ok=True)
+                    torch.save({k: v.detach().cpu() for k, v in m.state_dict().items()}, Path(d) / f"Epoch_{i + 1}.pt")
+            self.train_dataset.reset()
+        self.connection.close()

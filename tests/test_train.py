@@ -1,0 +1,275 @@
+"""Config 5 training (scripts/train_v3.py ->
+AttentionAttentionTrainer, trainer.py:952-1206).
+
+Golden vectors (tests/golden/train_step.npz, tests/golden/make_golden.py train)
+come from the real reference with dropout p = 0: its FinalAttentionTrainDataset
+batching, its collate fn, one hand-run step of the train_one_epoch body and a
+full train_one_epoch.  Parameter tensors are pinned through 2048 sampled
+elements each (the fixture must stay small).
+
+Tolerances: f32 loss 1e-5 relative; f32 gradients 1e-3 relative to each
+tensor's max |g| (MFMA f32 vs CPU summation order over 4096-long dots);
+AdamW-updated parameters 3e-8 absolute (the lr = 1e-6 update is ~1e-6 per
+element); bf16 step: loss within 2e-2 relative and gradient cosine > 0.99 of f32.
+"""
+import io
+import sqlite3
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from news_recommendation_project_v2_amd import data_utils
+from news_recommendation_project_v2_amd import weights as W
+
+
+def _setup():
+    g = golden("train_step")
+    lens = g["tok_lens"]
+    states = [(W.normal_tensor(91, f"train_tok_{i}", (int(n), 1024)) * 2.0 + 0.3).half() for i, n in enumerate(lens)]
+    labels = np.empty(len(g["cand_len"]), dtype=object)
+    s = 0
+    flat = g["labels_flat"]
+    labels[:] = [tuple(int(x) for x in flat[s0:s0 + n]) for s0, n in
+                 zip(np.concatenate([[0], np.cumsum(g["cand_len"])[:-1]]), g["cand_len"])]
+    return g, states, labels
+
+
+def _db(path, states):
+    with sqlite3.connect(path) as conn:
+        conn.execute("CREATE TABLE tensors (id INTEGER PRIMARY KEY, data BLOB)")
+        for t in states:
+            buf = io.BytesIO()
+            torch.save(t, buf)
+            conn.execute("INSERT INTO tensors (data) VALUES (?)", (buf.getvalue(),))
+
+
+def _dataset(g, labels):
+    return data_utils.FinalAttentionTrainDataset(g["hist"], g["hist_len"], g["cand"], g["cand_len"], labels,
+                                                 batch_size=int(g["batch_size"]), rng=np.random.default_rng(1234))
+
+
+def _params():
+    sd = W.final_attention_state_dict(1234)
+    tok = W.token_attn_state_dict(1234)
+    p = {"ln.weight": tok["encoder.layer.0.g_mlp_layernorm.weight"],
+         "ln.bias": tok["encoder.layer.0.g_mlp_layernorm.bias"]}
+    p.update(sd)
+    return p
+
+
+def _oracle_batch(ds, states, lo, hi):
+    rows = [ds[i] for i in range(lo, hi)]
+    groups, pos, neg = zip(*rows)
+    allidx = np.concatenate(list(groups) + [np.asarray(pos), np.asarray(neg)])
+    uniq, rev = np.unique(allidx, return_inverse=True)
+    last = torch.stack([states[int(u)][-1].float() for u in uniq])
+    lens = [len(x) for x in groups]
+    cuts = np.cumsum(lens)
+    hg = np.split(rev[:cuts[-1]], cuts[:-1])
+    B = len(pos)
+    return last, hg, rev[cuts[-1]:cuts[-1] + B], rev[cuts[-1] + B:], B
+
+
+def test_train_dataset_and_collate_match_reference(tmp_path):
+    g, states, labels = _setup()
+    ds = _dataset(g, labels)
+    np.testing.assert_array_equal(ds.pos_neg_indices, g["pos_neg_indices"])
+    db = tmp_path / "t.db"
+    _db(db, states)
+    B = int(g["batch_size"])
+    rows = [ds[i] for i in range(B)]
+    with sqlite3.connect(db) as conn:
+        tok, tmask, hidx, hmask, pn = data_utils.attention_attention_train_collate_fn(rows, conn)
+        last, hi, ho, pos, neg = data_utils.train_batch_csr(conn, rows)
+    np.testing.assert_array_equal(hidx.numpy(), g["b0_hidx"])
+    np.testing.assert_array_equal(hmask.numpy(), g["b0_hmask"])
+    np.testing.assert_array_equal(pn.numpy(), g["b0_pn"])
+    np.testing.assert_array_equal(tmask.numpy(), g["b0_tmask"])
+    # CSR form == padded form
+    np.testing.assert_array_equal(np.concatenate([pos, neg]), g["b0_pn"])
+    np.testing.assert_array_equal(hi, g["b0_hidx"][g["b0_hmask"] == 1])
+    np.testing.assert_array_equal(np.diff(ho), g["b0_hmask"].sum(1))
+    lastpos = tmask.sum(1) - 1
+    assert torch.equal(last.float(), tok[torch.arange(tok.shape[0]), lastpos])
+
+
+def _check_grads(got: dict, g, rtol_max=1e-3, prefix="grad"):
+    for k in g["step_grad_names"]:
+        k = str(k)
+        idx = g[f"{prefix}_idx:{k}"]
+        want = g[f"{prefix}_val:{k}"]
+        have = got[k].detach().reshape(-1).cpu().double().numpy()
+        scale = max(np.abs(want).max(), 1e-12)
+        assert np.abs(have[idx] - want).max() <= rtol_max * scale, k
+        np.testing.assert_allclose(have.sum(), float(g[f"grad_sum:{k}"]), rtol=1e-3, atol=1e-3 * scale, err_msg=k)
+
+
+def test_train_oracle_step_matches_reference():
+    from oracle import train_ref
+    g, states, labels = _setup()
+    ds = _dataset(g, labels)
+    last, hg, pos, neg, _ = _oracle_batch(ds, states, 0, int(g["batch_size"]))
+    params = _params()
+    res = train_ref.train_step(params, last, hg, pos, neg)
+    assert abs(res["loss"] - float(g["step_loss"])) <= 1e-6 * abs(float(g["step_loss"]))
+    assert abs(res["total_norm"] - float(g["step_total_norm"])) <= 1e-5 * float(g["step_total_norm"])
+    _check_grads(res["grads"], g, rtol_max=1e-5)
+    for k in g["step_grad_names"]:
+        k = str(k)
+        have = res["params_after"][k].reshape(-1).numpy()[g[f"grad_idx:{k}"]]
+        np.testing.assert_allclose(have, g[f"step_param_val:{k}"], rtol=0, atol=1e-9, err_msg=k)
+
+
+def test_train_oracle_epoch_matches_reference():
+    from oracle import train_ref
+    g, states, labels = _setup()
+    ds = _dataset(g, labels)
+    batches = [_oracle_batch(ds, states, lo, hi) for lo, hi in ds.batches()]
+    loss, after = train_ref.train_epoch(_params(), batches)
+    assert abs(loss - float(g["epoch_loss"])) <= 1e-6 * abs(float(g["epoch_loss"]))
+    for k in g["step_grad_names"]:
+        k = str(k)
+        have = after[k].reshape(-1).numpy()[g[f"grad_idx:{k}"]]
+        np.testing.assert_allclose(have, g[f"epoch_param_val:{k}"], rtol=0, atol=1e-8, err_msg=k)
+
+
+def test_drop_hash_stream_is_uniform():
+    from oracle import train_ref
+    m = train_ref.keep_mask(99, np.arange(512), 4096, 0.1)
+    assert abs(float(m.mean()) - 0.9) < 2e-3
+
+
+# ---------------------------------------------------------------- GPU
+def _engine(dtype, p, dev):
+    from news_recommendation_project_v2_amd.modeling_utils import FinalAttention, get_token_attn_model
+    from news_recommendation_project_v2_amd.train_step import FinalAttentionTrainStep
+    tm = get_token_attn_model()
+    tm.load_state_dict(W.token_attn_state_dict(1234))
+    fa = FinalAttention(1024, 4096)
+    fa.load_state_dict(W.final_attention_state_dict(1234))
+    fa = fa.to(dev)
+    return FinalAttentionTrainStep(tm, fa, dtype=dtype, dropout=p, device=dev), tm, fa
+
+
+def _device_batch(ds, states, lo, hi, dev, tmp_path):
+    from news_recommendation_project_v2_amd.train_step import TrainBatch
+    db = tmp_path / f"b{lo}.db"
+    _db(db, states)
+    with sqlite3.connect(db) as conn:
+        last, hi_, ho, pos, neg = data_utils.train_batch_csr(conn, [ds[i] for i in range(lo, hi)])
+    return TrainBatch(last.to(dev), torch.as_tensor(hi_).to(dev), torch.as_tensor(ho).to(dev),
+                      torch.as_tensor(pos).to(dev), torch.as_tensor(neg).to(dev))
+
+
+@pytest.mark.gpu
+def test_gpu_train_step_f32_matches_reference(gpu_device, tmp_path):
+    g, states, labels = _setup()
+    ds = _dataset(g, labels)
+    eng, _, _ = _engine(torch.float32, 0.0, gpu_device)
+    batch = _device_batch(ds, states, 0, int(g["batch_size"]), gpu_device, tmp_path)
+    loss, _, _ = eng.forward_backward(batch)
+    torch.cuda.synchronize()
+    assert abs(float(loss) - float(g["step_loss"])) <= 1e-5 * abs(float(g["step_loss"]))
+    _check_grads(eng.grad_dict(), g)
+    eng.optimizer_step()
+    norm = float(eng.sumsq.sqrt())
+    assert abs(norm - float(g["step_total_norm"])) <= 1e-3 * float(g["step_total_norm"])
+    for k in g["step_grad_names"]:
+        k = str(k)
+        have = eng.views[k].reshape(-1).cpu().numpy()[g[f"grad_idx:{k}"]]
+        np.testing.assert_allclose(have, g[f"step_param_val:{k}"], rtol=0, atol=3e-8, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_gpu_train_step_dropout_matches_oracle(gpu_device, tmp_path):
+    from oracle import train_ref
+    g, states, labels = _setup()
+    ds = _dataset(g, labels)
+    eng, _, _ = _engine(torch.float32, 0.1, gpu_device)
+    batch = _device_batch(ds, states, 8, 16, gpu_device, tmp_path)
+    seeds = tuple(eng.layer_seed(i) for i in (1, 2, 3))
+    loss, _, _ = eng.forward_backward(batch)
+    torch.cuda.synchronize()
+    last, hg, pos, neg, _ = _oracle_batch(ds, states, 8, 16)
+    ref = train_ref.train_step(_params(), last, hg, pos, neg, p=0.1, seeds=seeds, do_step=False)
+    assert abs(float(loss) - ref["loss"]) <= 1e-5 * abs(ref["loss"])
+    for k, want in ref["grads"].items():
+        have = eng.grad_dict()[k].cpu()
+        scale = float(want.abs().max())
+        assert float((have - want).abs().max()) <= 1e-3 * scale, k
+
+
+@pytest.mark.gpu
+def test_gpu_trainer_epoch_matches_reference(gpu_device, tmp_path):
+    from news_recommendation_project_v2_amd.trainer import AttentionAttentionTrainer
+    g, states, labels = _setup()
+    db = tmp_path / "train.db"
+    _db(db, states)
+    from news_recommendation_project_v2_amd.modeling_utils import FinalAttention, get_token_attn_model
+    tm = get_token_attn_model()
+    tm.load_state_dict(W.token_attn_state_dict(1234))
+    fa = FinalAttention(1024, 4096)
+    fa.load_state_dict(W.final_attention_state_dict(1234))
+    fa = fa.to(gpu_device)
+    tr = AttentionAttentionTrainer(str(db), tm, fa, g["hist"], g["hist_len"], g["cand"], g["cand_len"], labels,
+                                   rng=np.random.default_rng(1234), batch_size=int(g["batch_size"]),
+                                   dtype=torch.float32, dropout=0.0, log_dir=tmp_path / "logs",
+                                   final_attn_ckpt_dir=tmp_path / "ckpt")
+    np.testing.assert_array_equal(tr.train_dataset.pos_neg_indices, g["pos_neg_indices"])
+    loss = tr.train_one_epoch()
+    assert abs(loss - float(g["epoch_loss"])) <= 1e-5 * abs(float(g["epoch_loss"]))
+    sd = {**{"ln." + k.split(".")[-1]: v for k, v in tm.state_dict().items() if "g_mlp_layernorm" in k},
+          **fa.state_dict()}
+    for k in g["step_grad_names"]:
+        k = str(k)
+        have = sd[k].reshape(-1).cpu().numpy()[g[f"grad_idx:{k}"]]
+        np.testing.assert_allclose(have, g[f"epoch_param_val:{k}"], rtol=0, atol=5e-8, err_msg=k)
+    tr.train(1)  # second epoch: log + checkpoint written
+    assert (tmp_path / "logs" / "train_final_history_score.jsonl").is_file()
+    assert (tmp_path / "ckpt" / "Epoch_1.pt").is_file()
+
+
+@pytest.mark.gpu
+def test_gpu_train_step_bf16_close_to_f32(gpu_device, tmp_path):
+    g, states, labels = _setup()
+    ds = _dataset(g, labels)
+    batch = _device_batch(ds, states, 0, int(g["batch_size"]), gpu_device, tmp_path)
+    e32, _, _ = _engine(torch.float32, 0.0, gpu_device)
+    l32, _, _ = e32.forward_backward(batch)
+    e16, _, _ = _engine(torch.bfloat16, 0.0, gpu_device)
+    l16, _, _ = e16.forward_backward(batch)
+    torch.cuda.synchronize()
+    assert abs(float(l16) - float(l32)) <= 2e-2 * abs(float(l32))
+    for k in e32.names:
+        a, b = e32.gviews[k].double().flatten(), e16.gviews[k].double().flatten()
+        cos = float((a @ b) / (a.norm() * b.norm() + 1e-30))
+        assert cos > 0.99, (k, cos)
+
+
+@pytest.mark.gpu
+def test_gpu_train_kernels(gpu_device):
+    from news_recommendation_project_v2_amd import ops
+    x = torch.randn(300, 200, device=gpu_device)
+    t = ops.transpose(x)
+    assert torch.equal(t, x.T)
+    tb = ops.transpose(x, out_dtype=torch.bfloat16)
+    assert torch.equal(tb, x.T.to(torch.bfloat16))
+    cs = torch.zeros(200, device=gpu_device)
+    ops.col_sum(x, cs)
+    torch.testing.assert_close(cs, x.sum(0), rtol=1e-5, atol=1e-4)
+    idx = torch.tensor([3, -1, 0, 299], dtype=torch.int32, device=gpu_device)
+    gr = ops.gather_rows(x, idx)
+    assert torch.equal(gr[0], x[3]) and torch.equal(gr[1], torch.zeros(200, device=gpu_device))
+    # AdamW vs torch
+    p = torch.randn(1000, device=gpu_device)
+    gg = torch.randn(1000, device=gpu_device)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    ref = p.clone().requires_grad_(True)
+    ref.grad = gg.clone()
+    opt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=0.01)
+    for step in (1, 2):
+        ops.adamw(p, gg, m, v, step, 1e-3)
+        opt.step()
+    torch.testing.assert_close(p, ref.detach(), rtol=0, atol=1e-6)
