@@ -185,6 +185,20 @@ int nr_dense_rank(const float* scores, const int64_t* cand_off, int64_t n_imp, i
                   int32_t* status, void* stream);
 
 /*
+ * MIND metrics per impression from dense ranks (nr_dense_rank) and 0/1 labels
+ * (replaces evaluation.score_row, evaluation.py:34-54, run per
+ * impression by score(), :57-98).  metrics [n_imp][4] f64 = (AUC, MRR, nDCG@5,
+ * nDCG@10); AUC = Mann-Whitney U / (P N) on 1 / rank (sklearn's ROC AUC, NaN for
+ * single-class impressions).  MRR / nDCG are exact when the impression has no
+ * tied ranks; tie_flag[i] = 1 marks impressions with ties (the reference's
+ * positions then follow numpy's unstable argsort: evaluate those on the host).
+ * status (caller-zeroed device int32): |1 if an impression has > 2048
+ * candidates, |2 for a non-0/1 label or out-of-range rank (row set to NaN, flagged).
+ */
+int nr_impression_metrics(const int32_t* ranks, const float* labels, const int64_t* cand_off, int64_t n_imp,
+                          double* metrics, int32_t* tie_flag, int32_t* status, void* stream);
+
+/*
  * FinalAttention per-news transform for n news rows of `emb`:
  *   x = W3·relu(W2·relu(W1·e + b1) + b2) + b3 ;  p = exp(W5·relu(W4·x + b4))
  * written as table[n][2][1024] = (x, p) in `dtype` (modeling_utils.py:218-224,

@@ -3,11 +3,12 @@
 Kept: TransformData (45-114), EmbeddingsComponent (117-175),
 SaveEmbeddingComponent (178-223), LoadEmbeddingComponent (226-258),
 TokenEmbeddingsComponent (955-977), FinalAttentionComponent (980-1027,
-transform only), plus
+transform only), StoreEmbeddingsComponent (858-880),
+AttentionAttentionComponent (883-952, config-5 training), plus
 LatentAttentionComponent — the same scoring with the latent pooler, which the
 reference can only reach through get_latent_attention_model
-(modeling_utils.py:151-155).  Training components and the Azure upload are out
-of scope.
+(modeling_utils.py:151-155).  The other experiments' components and the Azure
+upload are out of scope.
 """
 from __future__ import annotations
 
@@ -17,9 +18,9 @@ from typing import Any, Optional
 import numpy as np
 import torch
 
-from .data_model_helper import apply_token_attn, get_embeddings, get_final_second_attention_score
+from .data_model_helper import apply_token_attn, get_embeddings, get_final_second_attention_score, store_embeddings
 from .data_utils import split_impressions_and_history
-from .modeling_utils import get_final_attention_model, get_latent_attention_model
+from .modeling_utils import get_final_attention_model, get_latent_attention_model, get_token_attn_model
 from .pipeline import PipelineComponent, check_req_keys
 
 
@@ -107,6 +108,74 @@ class LoadEmbeddingComponent(PipelineComponent):
         if q.exists():
             context_dict["query_news_embeddings"] = torch.load(q, weights_only=True)
         return context_dict
+
+
+class StoreEmbeddingsComponent(PipelineComponent):
+    """Per-token title hidden states -> sqlite token DB (components.py:858-880)."""
+
+    required_keys = {"news_list", "news_text_dict"}
+
+    def __init__(self, model_path: str, db_name: str):
+        self.model_path = model_path
+        self.db_name = db_name
+
+    def transform(self, context_dict):
+        check_req_keys(self.required_keys, context_dict)
+        new = context_dict.copy()
+        store_embeddings(self.model_path, new["news_list"], new["news_text_dict"], self.db_name)
+        del new["news_text_dict"]
+        return new
+
+
+class AttentionAttentionComponent(PipelineComponent):
+    """Config-5 training of the token-attention model + FinalAttention
+    (components.py:883-952): ``train`` builds an AttentionAttentionTrainer on the
+    impressions that have a history and runs ``num_epochs``; ``transform`` is the
+    identity.  Extra keyword arguments (batch_size, dtype, lr, dropout, seed) go
+    to the trainer."""
+
+    required_keys = {"impression_rev_ind_array", "impression_len_list", "history_rev_ind_array",
+                     "history_len_list", "history_bool"}
+    train_required_keys = required_keys | {"labels"}
+
+    def __init__(self, db_name: str, token_attention_model_path: Optional[Path] = None,
+                 final_attention_model_path: Optional[Path] = None, log_dir: Optional[Path] = None,
+                 token_ckpt_dir: Optional[Path] = None, final_attn_ckpt_dir: Optional[Path] = None, num_epochs=5,
+                 exp_name: str = "", max_neg_ratio: Optional[float] = None, max_pos_ratio: Optional[float] = None,
+                 rng=None, **trainer_kw):
+        self.db_name = db_name
+        self.token_attention = get_token_attn_model(token_attention_model_path)
+        self.final_attention = get_final_attention_model(final_attention_model_path)
+        self.num_epochs = num_epochs
+        self.exp_name = exp_name
+        self.rng = rng if rng is not None else np.random.default_rng(1234)
+        self.log_dir = log_dir
+        self.token_ckpt_dir = token_ckpt_dir
+        self.final_attn_ckpt_dir = final_attn_ckpt_dir
+        self.max_neg_ratio = max_neg_ratio
+        self.max_pos_ratio = max_pos_ratio
+        self.trainer_kw = trainer_kw
+        self.trainer = None
+
+    def transform(self, context_dict):
+        return context_dict
+
+    def train(self, context_dict, val_context_dict=None):
+        from .trainer import AttentionAttentionTrainer
+        check_req_keys(self.train_required_keys, context_dict)
+        hb = np.asarray(context_dict["history_bool"], dtype=bool)
+        imp_len = np.asarray(context_dict["impression_len_list"])
+        self.trainer = AttentionAttentionTrainer(
+            db_name=self.db_name, token_attention_model=self.token_attention,
+            final_attention_model=self.final_attention,
+            train_history_rev_index=context_dict["history_rev_ind_array"][0],
+            train_history_len_list=context_dict["history_len_list"],
+            train_news_rev_index=context_dict["impression_rev_ind_array"][0][np.repeat(hb, imp_len)],
+            train_impression_len_list=imp_len[hb], train_labels=np.asarray(context_dict["labels"])[hb],
+            log_dir=self.log_dir, token_ckpt_dir=self.token_ckpt_dir, final_attn_ckpt_dir=self.final_attn_ckpt_dir,
+            exp_name=self.exp_name, max_neg_ratio=self.max_neg_ratio, max_pos_ratio=self.max_pos_ratio,
+            rng=self.rng, **self.trainer_kw)
+        self.trainer.train(self.num_epochs)
 
 
 class TokenEmbeddingsComponent(PipelineComponent):

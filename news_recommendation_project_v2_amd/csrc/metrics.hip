@@ -1,0 +1,126 @@
+// MIND metrics per impression on the device, from the dense
+// ranks of nr_dense_rank and 0/1 labels.  Replaces evaluation.score_row
+// (evaluation.py:34-54: roc_auc_score(labels, 1 / rank), mrr_score,
+// ndcg_score @5 / @10) run per impression in a ProcessPoolExecutor.
+//
+// One wave per impression, a 2048-bin LDS histogram of its dense ranks:
+//   AUC  = (sum over positives of the tie-averaged ascending rank - P(P+1)/2) / (P N)
+//          (Mann-Whitney U == sklearn's trapezoidal ROC AUC on 1/rank; NaN when
+//          P == 0 or N == 0, like sklearn 1.7's undefined-AUC result)
+//   MRR  = sum_pos 1 / rank / P ;  nDCG@k = sum_{pos, rank <= k} 1 / log2(rank + 1)
+//          / sum_{j < min(P, k)} 1 / log2(j + 2)
+// MRR / nDCG use np.argsort(1 / rank)[::-1] positions in the reference, which
+// equal rank - 1 only when no two candidates tie; impressions with ties are
+// flagged (tie_flag = 1) for the host to evaluate with numpy's own tie order.
+#include "nr_common.h"
+
+namespace nr {
+
+constexpr int kMaxCand = 2048;
+
+__global__ __launch_bounds__(256) void metrics_kernel(const int32_t* __restrict__ ranks, const float* __restrict__ labels,
+                                                      const int64_t* __restrict__ off, int64_t n_imp,
+                                                      double* __restrict__ out, int32_t* __restrict__ tie_flag,
+                                                      int32_t* __restrict__ status) {
+  __shared__ int cnt[4][kMaxCand + 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t imp = (int64_t)blockIdx.x * 4 + w;
+  if (imp >= n_imp) return;
+  const int64_t a = off[imp];
+  const int c = (int)(off[imp + 1] - a);
+  double* o = out + imp * 4;
+  if (c > kMaxCand) {
+    if (lane == 0) { atomicOr(status, 1); o[0] = o[1] = o[2] = o[3] = __builtin_nan(""); tie_flag[imp] = 1; }
+    return;
+  }
+  int* h = cnt[w];
+  for (int v = lane; v <= c; v += 64) h[v] = 0;
+  __builtin_amdgcn_wave_barrier();
+  // histogram of dense ranks (1..c), label sums, binary-label check
+  int P = 0, maxr = 0, bad = 0;
+  for (int i = lane; i < c; i += 64) {
+    const int r = ranks[a + i];
+    const float y = labels[a + i];
+    if (r < 1 || r > c) bad = 1;
+    else atomicAdd(&h[r], 1);
+    if (y != 0.f && y != 1.f) bad = 1;
+    P += y != 0.f;
+    maxr = max(maxr, r);
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int m = 32; m >= 1; m >>= 1) {
+    P += __shfl_xor(P, m, 64);
+    maxr = max(maxr, __shfl_xor(maxr, m, 64));
+    bad |= __shfl_xor(bad, m, 64);
+  }
+  if (bad) {
+    if (lane == 0) { atomicOr(status, 2); o[0] = o[1] = o[2] = o[3] = __builtin_nan(""); tie_flag[imp] = 1; }
+    return;
+  }
+  // h[v] <- number of candidates with dense rank > v (lower score): suffix sum
+  // over 1..c, 32 bins per lane, then a wave scan of the lane totals.
+  const int per = (c + 63) / 64;
+  const int lo = 1 + lane * per, hi = min(c, lo + per - 1);
+  int tot = 0;
+  for (int v = lo; v <= hi; ++v) tot += h[v];
+  int suf = tot;  // inclusive suffix over lanes >= lane
+  for (int m = 1; m < 64; m <<= 1) {
+    const int t = __shfl_down(suf, m, 64);
+    if (lane + m < 64) suf += t;
+  }
+  int run = suf - tot;  // candidates in bins above this lane's range
+  // rewrite bins high -> low: keep the count in the upper 16 bits
+  for (int v = hi; v >= lo; --v) {
+    const int k = h[v];
+    h[v] = (run << 12) | k;  // run <= 2048 (12 bits), k <= 2048 needs 12 bits
+    run += k;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int N = c - P;
+  double S = 0.0, rr = 0.0, d5 = 0.0, d10 = 0.0;
+  for (int i = lane; i < c; i += 64) {
+    if (labels[a + i] == 0.f) continue;
+    const int r = ranks[a + i];
+    const int e = h[r];
+    const int below = e >> 12, k = e & 4095;
+    S += (double)below + 0.5 * (double)(k + 1);
+    rr += 1.0 / (double)r;
+    const double disc = 1.0 / log2((double)r + 1.0);
+    if (r <= 5) d5 += disc;
+    if (r <= 10) d10 += disc;
+  }
+  for (int m = 32; m >= 1; m >>= 1) {
+    S += __shfl_xor(S, m, 64);
+    rr += __shfl_xor(rr, m, 64);
+    d5 += __shfl_xor(d5, m, 64);
+    d10 += __shfl_xor(d10, m, 64);
+  }
+  if (lane == 0) {
+    const double nan = __builtin_nan("");
+    o[0] = (P == 0 || N == 0) ? nan : (S - 0.5 * (double)P * (double)(P + 1)) / ((double)P * (double)N);
+    double i5 = 0.0, i10 = 0.0;
+    for (int j = 0; j < min(P, 10); ++j) {
+      const double disc = 1.0 / log2((double)j + 2.0);
+      if (j < 5) i5 += disc;
+      i10 += disc;
+    }
+    o[1] = rr / (double)P;  // P == 0 -> NaN like 0 / 0 in numpy
+    o[2] = d5 / i5;
+    o[3] = d10 / i10;
+    tie_flag[imp] = maxr < c ? 1 : 0;
+  }
+}
+
+}  // namespace nr
+
+extern "C" int nr_impression_metrics(const int32_t* ranks, const float* labels, const int64_t* cand_off, int64_t n_imp,
+                                     double* metrics, int32_t* tie_flag, int32_t* status, void* stream) {
+  nr::clear_error();
+  NR_CHECK_ARG(n_imp >= 0, "nr_impression_metrics: n_imp < 0");
+  if (n_imp == 0) return NR_OK;
+  NR_CHECK_ARG(ranks && labels && cand_off && metrics && tie_flag && status, "nr_impression_metrics: null pointer");
+  hipLaunchKernelGGL(nr::metrics_kernel, dim3((unsigned)((n_imp + 3) / 4)), dim3(256), 0, (hipStream_t)stream, ranks,
+                     labels, cand_off, n_imp, metrics, tie_flag, status);
+  NR_CHECK_LAUNCH("nr_impression_metrics");
+  return NR_OK;
+}

@@ -158,3 +158,30 @@ def score(preds_input: Sequence[Sequence[int]] | np.ndarray, labels_input: Seque
         "ndcg10": np.mean(n10).item(),
         "num_samples": len(preds_input),
     }
+
+
+def score_device(ranks, labels, offsets) -> dict:
+    """``score`` over flat dense ranks / 0/1 labels with CSR offsets, on the MI355X
+    (nr_impression_metrics): one wave per impression instead of sklearn per row
+    in a process pool (evaluation.py:57-98).  Impressions with tied ranks get
+    MRR / nDCG from the host with the reference's numpy calls (their positions
+    depend on np.argsort's tie order).  Accepts device or host arrays."""
+    import torch
+
+    from . import ops
+    from .config import DEVICE
+    dev = DEVICE
+    r = torch.as_tensor(np.asarray(ranks, dtype=np.int32) if not isinstance(ranks, torch.Tensor) else ranks)
+    y = torch.as_tensor(np.asarray(labels, dtype=np.float32) if not isinstance(labels, torch.Tensor) else labels)
+    o = torch.as_tensor(np.asarray(offsets, dtype=np.int64) if not isinstance(offsets, torch.Tensor) else offsets)
+    r, y, o = r.to(dev, torch.int32), y.to(dev, torch.float32), o.to(dev, torch.int64)
+    m, tie = ops.impression_metrics(r, y, o)
+    m = m.cpu().numpy()
+    ties = np.nonzero(tie.cpu().numpy())[0]
+    if len(ties):
+        rh, yh, oh = r.cpu().numpy(), y.cpu().numpy(), o.cpu().numpy()
+        for i in ties:
+            a, b = oh[i], oh[i + 1]
+            _, m[i, 1], m[i, 2], m[i, 3] = _row_metrics(yh[a:b], rh[a:b])
+    return {"auc": np.mean(m[:, 0]).item(), "mrr": np.mean(m[:, 1]).item(), "ndcg5": np.mean(m[:, 2]).item(),
+            "ndcg10": np.mean(m[:, 3]).item(), "num_samples": int(len(m))}

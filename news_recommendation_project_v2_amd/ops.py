@@ -220,6 +220,27 @@ def dense_rank(scores: torch.Tensor, cand_off: torch.Tensor, check: bool = True)
     return ranks
 
 
+def impression_metrics(ranks: torch.Tensor, labels: torch.Tensor, cand_off: torch.Tensor):
+    """Per-impression (AUC, MRR, nDCG@5, nDCG@10) f64 [n, 4] + tie flags int32 [n]
+    from dense ranks (int32) and 0/1 labels (f32); raises on >2048 candidates or
+    non-binary labels."""
+    dev = _dev(ranks, labels, cand_off)
+    if ranks.dtype != torch.int32 or labels.dtype != torch.float32 or cand_off.dtype != torch.int64:
+        raise _lib.NewsRecHIPError("impression_metrics: ranks int32, labels f32, cand_off int64")
+    n = cand_off.numel() - 1
+    out = torch.empty((n, 4), dtype=torch.float64, device=dev)
+    tie = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("nr_impression_metrics", _ptr(ranks), _ptr(labels), _ptr(cand_off), n, _ptr(out), _ptr(tie),
+              _ptr(status), _stream(dev))
+    st = int(status.item())
+    if st & 1:
+        raise _lib.NewsRecHIPError("impression_metrics: an impression has more than 2048 candidates")
+    if st & 2:
+        raise _lib.NewsRecHIPError("impression_metrics: labels must be 0/1 and ranks in 1..c")
+    return out, tie
+
+
 def final_attn_transform(emb: torch.Tensor, w: dict, out: Optional[torch.Tensor] = None,
                          workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Per-news FinalAttention table [n, 2*1024] = (x, exp(w)) in emb.dtype.

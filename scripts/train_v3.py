@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Config-5 training entry point (reference scripts/train_v3.py:23-161):
+TransformData -> [StoreEmbeddingsComponent] -> AttentionAttentionComponent.train
+(token-attention LayerNorm + FinalAttention, MarginRankingLoss(2), AdamW lr 1e-6,
+clip 0.5, 5 epochs), checkpoints models/{token_attn,final_attn}/Epoch_{i}.pt and
+logs/train_final_history_score.jsonl.
+
+Flags (the reference hard-codes them): --data-dir --db-name --log-dir --ckpt-dir
+--epochs --batch-size --dtype {fp32,bf16} --num-impressions --store-db
+(--model-path) to (re)build the sqlite token-state DB with the title encoder
+first.  --synthetic: seeded MIND-shaped behaviours and a synthetic token DB
+(fp16 N(0,1) states, 20 +- 6 tokens per title), no data or checkpoints needed.
+"""
+from __future__ import annotations
+
+import argparse
+import io
+import sqlite3
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+from news_recommendation_project_v2_amd.components import (AttentionAttentionComponent,  # noqa: E402
+                                                           StoreEmbeddingsComponent, TransformData)
+from news_recommendation_project_v2_amd.config import MODEL_PATH, DataSubset, NewsDataset  # noqa: E402
+from news_recommendation_project_v2_amd.pipeline import Pipeline  # noqa: E402
+
+
+def synthetic_token_db(path: Path, n_news: int, seed: int = 1234) -> None:
+    rng = np.random.default_rng(seed)
+    lens = np.clip(np.rint(rng.normal(20, 6, n_news)), 1, 512).astype(np.int64)
+    g = torch.Generator().manual_seed(seed)
+    with sqlite3.connect(path) as conn:
+        conn.execute("DROP TABLE IF EXISTS tensors;")
+        conn.execute("CREATE TABLE tensors (id INTEGER PRIMARY KEY, data BLOB)")
+        for n in lens:
+            buf = io.BytesIO()
+            torch.save(torch.randn((int(n), 1024), generator=g).half(), buf)
+            conn.execute("INSERT INTO tensors (data) VALUES (?)", (buf.getvalue(),))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--data-dir", type=Path, default=Path("data"))
+    ap.add_argument("--db-name", type=Path, default=Path("mydb_train.sqlite"))
+    ap.add_argument("--log-dir", type=Path, default=Path("logs"))
+    ap.add_argument("--ckpt-dir", type=Path, default=Path("models"))
+    ap.add_argument("--epochs", type=int, default=5)
+    ap.add_argument("--batch-size", type=int, default=256)
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="bf16")
+    ap.add_argument("--num-impressions", type=int, default=None)
+    ap.add_argument("--store-db", action="store_true")
+    ap.add_argument("--model-path", default=MODEL_PATH)
+    ap.add_argument("--exp-name", default="attn_attn")
+    ap.add_argument("--synthetic", action="store_true")
+    args = ap.parse_args()
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    rng = np.random.default_rng(1234)
+
+    if args.synthetic:
+        sys.path.insert(0, str(Path(__file__).resolve().parent))
+        from eval import synthetic_context
+        ctx = synthetic_context(NewsDataset.MINDsmall_train, args.num_impressions or 2000, seed=1234)
+        n_news = len(TransformData().transform(dict(ctx))["news_list"])
+        synthetic_token_db(args.db_name, n_news)
+    else:
+        from news_recommendation_project_v2_amd.data_utils import load_dataset
+        beh, feats = load_dataset(args.data_dir, NewsDataset.MINDsmall_train, num_samples=args.num_impressions,
+                                  data_subset=DataSubset.WITH_HISTORY, random_state=rng)
+        ctx = {"news_dataset": NewsDataset.MINDsmall_train, "behaviors": beh, **feats}
+
+    steps = [("init_transform", TransformData())]
+    if args.store_db and not args.synthetic:
+        steps.append(("store_comp", StoreEmbeddingsComponent(args.model_path, db_name=str(args.db_name))))
+    comp = AttentionAttentionComponent(db_name=str(args.db_name), log_dir=args.log_dir,
+                                       token_ckpt_dir=args.ckpt_dir / "token_attn",
+                                       final_attn_ckpt_dir=args.ckpt_dir / "final_attn", exp_name=args.exp_name,
+                                       num_epochs=args.epochs, rng=rng, batch_size=args.batch_size, dtype=dtype)
+    steps.append(("attn_attn", comp))
+    t0 = time.time()
+    Pipeline("train_subset", steps).train(ctx)
+    n = len(comp.trainer.train_dataset) * args.epochs
+    print(f"[train_v3] {args.epochs} epochs, {n} training rows in {time.time() - t0:.1f}s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
