@@ -75,6 +75,18 @@ def split_impressions_and_history(impressions: Sequence[str], history: Sequence[
     history_rev_ind_array [2, H], history_len_list [I'], labels.
     """
     assert len(impressions) > 0, "No Impressions given"
+    from .native import split_behaviors
+    res = split_behaviors(impressions, history)  # C++ parser (libnewsrec_host.so)
+    if res is not None:
+        return res
+    return split_impressions_and_history_py(impressions, history)
+
+
+def split_impressions_and_history_py(impressions: Sequence[str], history: Sequence[Optional[str]]) -> dict[str, Any]:
+    """Pure-Python restatement of the same parse; used when the native parser
+    declines an input (non-ASCII text, malformed labels) so that outputs and
+    exceptions stay the reference's."""
+    assert len(impressions) > 0, "No Impressions given"
     imps = list(impressions)
     hists = list(history)
     label_present = "-" in imps[0]
