@@ -57,6 +57,10 @@ extern "C" {
                                  forward only: use nr_gemm_relu_dropout      */
 #define NR_EPI_DRELU 7  /* C = R > 0 ? acc * scale : 0 (backward of relu+dropout
                            given its forward output R): nr_gemm_drelu       */
+#define NR_EPI_SOFTMAX64 8 /* C = softmax over each aligned run of 64 columns of
+                           (acc + bias): SDPA's softmax over the 64 latents of
+                           latent_attention.py:72 fused into the score GEMM
+                           (needs N % 256 == 0, 16-byte aligned C rows)      */
 
 /* Library version (major*100 + minor). */
 int nr_version(void);

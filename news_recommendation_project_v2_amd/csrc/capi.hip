@@ -92,7 +92,7 @@ extern "C" int64_t nr_latent_workspace_bytes(int dtype, int64_t n) {
 }
 
 // latent_attention.py:157-163 with the 64 latents' K/V folded into A and Bt:
-//   y = LN_q(e); P = softmax64(y Aᵀ); h1 = e + P Btᵀ;
+//   y = LN_q(e); P = softmax64(y Aᵀ) (fused epilogue); h1 = e + P Btᵀ;
 //   h = h1 + GEGLU(LN_f(h1) W1iᵀ + b1i) W2ᵀ + b2     -> table[n][1024]
 extern "C" int nr_latent_transform(int dtype, int64_t n, const void* emb, int64_t emb_ld,
                                    const float* lnq_g, const float* lnq_b, const void* A,
@@ -114,7 +114,7 @@ extern "C" int nr_latent_transform(int dtype, int64_t n, const void* emb, int64_
   hipStream_t st = (hipStream_t)stream;
   char* wy = (char*)ws;
   char* wsc = wy + mc * D * es;
-  char* wp = wsc + mc * S * 4;
+  char* wp = wsc + mc * S * 4;  // (wsc: f32 scores of the unfused path, kept for the ABI's workspace size)
   char* wf = wp + mc * S * es;
   for (int64_t r0 = 0; r0 < n; r0 += nr::kChunk) {
     const int64_t m = (n - r0) < nr::kChunk ? (n - r0) : nr::kChunk;
@@ -122,8 +122,8 @@ extern "C" int nr_latent_transform(int dtype, int64_t n, const void* emb, int64_
     char* h = (char*)table + r0 * D * es;
     int rc;
     if ((rc = nr::layernorm_dispatch(dtype, dtype, m, D, e, emb_ld, lnq_g, lnq_b, 1e-5f, wy, D, st))) return rc;
-    if ((rc = nr::gemm_dispatch(dtype, NR_F32, NR_EPI_NONE, m, S, D, wy, D, A, D, nullptr, nullptr, 0, wsc, S, st))) return rc;
-    if ((rc = nr::softmax64_dispatch(m, S / 64, (const float*)wsc, S, dtype, wp, S, st))) return rc;
+    // scores + the per-head 64-latent softmax fused in the GEMM epilogue
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_SOFTMAX64, m, S, D, wy, D, A, D, nullptr, nullptr, 0, wp, S, st))) return rc;
     if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RESADD, m, D, S, wp, S, Bt, S, nullptr, e, emb_ld, h, D, st))) return rc;
     if ((rc = nr::layernorm_dispatch(dtype, dtype, m, D, h, D, lnf_g, lnf_b, 1e-5f, wy, D, st))) return rc;
     if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_GEGLU, m, 2 * F, D, wy, D, W1i, D, b1i, nullptr, 0, wf, F, st))) return rc;

@@ -230,6 +230,111 @@ constexpr int G2_STAGE = (G2BM + G2BN) * 128;  // bytes per stage (A + B, 128-B 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void g_void;
 
+// Epilogue of the 256x256 kernels (acc[4][2] per wave: rows wm*128 + 32 mi,
+// cols wn*64 + 32 ni), staged through the kernel's LDS (caller has finished
+// with the operand stages and passed a barrier).
+template <int EPI, typename TO>
+__device__ __forceinline__ void gemm256_store(const f32x16 (&acc)[4][2], unsigned char* smem, int wave, int lane,
+                                              int wm, int wn, int64_t m0, int64_t n0, int64_t M, int64_t N,
+                                              const float* __restrict__ bias, const TO* R, int64_t ldr, TO* C,
+                                              int64_t ldc, const EpiArgs& ea) {
+  // Epilogue, staged through LDS so global stores are whole 16-byte row
+  // segments (the 32x32 C/D map would give 2-4-byte scattered stores).  Two
+  // passes of 64 rows per wave; bias and activation are applied in registers,
+  // the f32 results parked in the wave's private 16 KiB LDS slab
+  // ([64 rows][COLS] f32), then read back row-wise, residual added, stored.
+  constexpr int COLS = (EPI == NR_EPI_GEGLU) ? 32 : 64;  // output columns per wave
+  constexpr int VEC = 16 / (int)sizeof(TO);               // elements per 16-B store
+  constexpr int LPR = COLS / VEC;                          // lanes per output row
+  constexpr int RPI = 64 / LPR;                            // rows per wave instruction
+  const int cl = lane & 31, rh = 4 * (lane >> 5);
+  float* slab = reinterpret_cast<float*>(smem + wave * 16384);
+  const int64_t wcol = n0 + wn * 64;
+  const int64_t ocol0 = (EPI == NR_EPI_GEGLU) ? wcol / 2 : wcol;
+  float ba = 0.f, bg = 0.f;
+  if (bias) { ba = bias[wcol + cl]; bg = bias[wcol + 32 + cl]; }
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int mi = 2 * pass + h;
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int lr = 32 * h + (reg & 3) + 8 * (reg >> 2) + rh;
+        if constexpr (EPI == NR_EPI_GEGLU) {
+          slab[lr * COLS + cl] = (acc[mi][0][reg] + ba) * gelu_erf(acc[mi][1][reg] + bg);
+        } else {
+          float v0 = acc[mi][0][reg] + ba, v1 = acc[mi][1][reg] + bg;
+          if constexpr (EPI == NR_EPI_RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
+          if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
+            const uint64_t gi = (uint64_t)((m0 + wm * 128 + pass * 64 + lr) * N + wcol + cl);
+            v0 = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(v0, 0.f) * ea.scale;
+            v1 = drop_hash(ea.seed, gi + 32) < ea.thr ? 0.f : fmaxf(v1, 0.f) * ea.scale;
+          }
+          if constexpr (EPI == NR_EPI_EXP) { v0 = expf(v0); v1 = expf(v1); }
+          if constexpr (EPI == NR_EPI_GELU) { v0 = gelu_erf(v0); v1 = gelu_erf(v1); }
+          slab[lr * COLS + cl] = v0;
+          slab[lr * COLS + 32 + cl] = v1;
+        }
+      }
+    }
+    __syncthreads();
+    const int rr = lane / LPR, cc = (lane % LPR) * VEC;
+#pragma unroll
+    for (int it = 0; it < 64 / RPI; ++it) {
+      const int lr = it * RPI + rr;
+      const int64_t row = m0 + wm * 128 + pass * 64 + lr;
+      float v[VEC];
+#pragma unroll
+      for (int q = 0; q < VEC; q += 4) {
+        const float4 f = *reinterpret_cast<const float4*>(slab + lr * COLS + cc + q);
+        v[q] = f.x; v[q + 1] = f.y; v[q + 2] = f.z; v[q + 3] = f.w;
+      }
+      if constexpr (EPI == NR_EPI_SOFTMAX64) {
+        // the wave's 64 columns are one 64-wide softmax group (column block
+        // wn * 64); a row's values sit on LPR consecutive lanes
+        float m = v[0];
+#pragma unroll
+        for (int q = 1; q < VEC; ++q) m = fmaxf(m, v[q]);
+#pragma unroll
+        for (int o = 1; o < LPR; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        float sum = 0.f;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) { v[q] = expf(v[q] - m); sum += v[q]; }
+#pragma unroll
+        for (int o = 1; o < LPR; o <<= 1) sum += __shfl_xor(sum, o, 64);
+        const float inv = 1.0f / sum;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) v[q] *= inv;
+      }
+      if (row < M) {
+        if constexpr (EPI == NR_EPI_RESADD || EPI == NR_EPI_DRELU) {
+          const uint4 rv = *reinterpret_cast<const uint4*>(R + row * ldr + ocol0 + cc);
+          float r[VEC];
+          if constexpr (sizeof(TO) == 4) {
+            r[0] = __uint_as_float(rv.x); r[1] = __uint_as_float(rv.y);
+            r[2] = __uint_as_float(rv.z); r[3] = __uint_as_float(rv.w);
+          } else {
+            const uint32_t w4[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { r[2 * q] = bf16_lo(w4[q]); r[2 * q + 1] = bf16_hi(w4[q]); }
+          }
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) {
+            if constexpr (EPI == NR_EPI_RESADD) v[q] += r[q];
+            else v[q] = r[q] > 0.f ? v[q] * ea.scale : 0.f;
+          }
+        }
+        TO o[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) o[q] = to_out<TO>(v[q]);
+        *reinterpret_cast<uint4*>(C + row * ldc + ocol0 + cc) = *reinterpret_cast<const uint4*>(o);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <typename TI, int EPI, typename TO>
 __global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, int64_t K,
                                                              const TI* __restrict__ A, int64_t lda,
@@ -341,88 +446,190 @@ __global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, i
     __syncthreads();
   }
 
-  // Epilogue, staged through LDS so global stores are whole 16-byte row
-  // segments (the 32x32 C/D map would give 2-4-byte scattered stores).  Two
-  // passes of 64 rows per wave; bias and activation are applied in registers,
-  // the f32 results parked in the wave's private 16 KiB LDS slab
-  // ([64 rows][COLS] f32), then read back row-wise, residual added, stored.
-  constexpr int COLS = (EPI == NR_EPI_GEGLU) ? 32 : 64;  // output columns per wave
-  constexpr int VEC = 16 / (int)sizeof(TO);               // elements per 16-B store
-  constexpr int LPR = COLS / VEC;                          // lanes per output row
-  constexpr int RPI = 64 / LPR;                            // rows per wave instruction
-  const int cl = lane & 31, rh = 4 * (lane >> 5);
-  float* slab = reinterpret_cast<float*>(smem + wave * 16384);
-  const int64_t wcol = n0 + wn * 64;
-  const int64_t ocol0 = (EPI == NR_EPI_GEGLU) ? wcol / 2 : wcol;
-  float ba = 0.f, bg = 0.f;
-  if (bias) { ba = bias[wcol + cl]; bg = bias[wcol + 32 + cl]; }
+  gemm256_store<EPI, TO>(acc, smem, wave, lane, wm, wn, m0, n0, M, N, bias, R, ldr, C, ldc, ea);
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined 256x256 variant: each K tile is computed in 4 phases, one output
+// quadrant (64 rows x 32 cols per wave) each, with the half-tile LDS-DMA
+// prefetches spread over the phases and kept in flight ACROSS raw s_barriers
+// (counted vmcnt, never a drained queue in steady state):
+//   P1: read A(m0) + B(n0) frags, DMA A-half 0 of tile t+1 -> MFMA q(m0,n0)
+//   P2: read B(n1) frags,         DMA A-half 1 of tile t+1 -> MFMA q(m0,n1)
+//   P3: read A(m1) frags,         DMA B-half 0 of tile t+2 -> MFMA q(m1,n1)
+//   P4: (frags in registers),     DMA B-half 1 of tile t+2 -> MFMA q(m1,n0)
+//       (vmcnt(2) before P4's first barrier: tile t+1 has landed)
+// A stage's B halves are last read in P2 and its A halves in P3, so the
+// prefetch into a stage never overwrites data a wave can still read (each
+// phase ends lgkmcnt(0) + barrier).  Block ids are remapped XCD-aware so the
+// N-tiles that share an A panel run on one XCD (its L2 holds the panel).
+// Same LDS images, swizzle and epilogue as gemm256_kernel.
+template <typename TI, int EPI, typename TO>
+__global__ __launch_bounds__(512, 2) void gemm256p_kernel(int64_t M, int64_t N, int64_t K,
+                                                          const TI* __restrict__ A, int64_t lda,
+                                                          const TI* __restrict__ W, int64_t ldw,
+                                                          const float* __restrict__ bias, const TO* R,
+                                                          int64_t ldr, TO* C, int64_t ldc, EpiArgs ea) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nx = (int)gridDim.x, nwg = nx * (int)gridDim.y;
+  const int orig = (int)blockIdx.y * nx + (int)blockIdx.x;
+  const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+  const int64_t n0 = (int64_t)(wg % nx) * G2BN;
+  const int64_t m0 = (int64_t)(wg / nx) * G2BM;
+
+  constexpr int BK = 128 / (int)sizeof(TI), CE = 16 / (int)sizeof(TI);
+  // half-tile DMA sources: wave covers rows 128h + 16 wave + 8 j + lane / 8
+  const TI* asrc[2][2];
+  const TI* bsrc[2][2];
+  int hoff[2][2];
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int mi = 2 * pass + h;
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int lr = 32 * h + (reg & 3) + 8 * (reg >> 2) + rh;
-        if constexpr (EPI == NR_EPI_GEGLU) {
-          slab[lr * COLS + cl] = (acc[mi][0][reg] + ba) * gelu_erf(acc[mi][1][reg] + bg);
-        } else {
-          float v0 = acc[mi][0][reg] + ba, v1 = acc[mi][1][reg] + bg;
-          if constexpr (EPI == NR_EPI_RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
-          if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
-            const uint64_t gi = (uint64_t)((m0 + wm * 128 + pass * 64 + lr) * N + wcol + cl);
-            v0 = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(v0, 0.f) * ea.scale;
-            v1 = drop_hash(ea.seed, gi + 32) < ea.thr ? 0.f : fmaxf(v1, 0.f) * ea.scale;
-          }
-          if constexpr (EPI == NR_EPI_EXP) { v0 = expf(v0); v1 = expf(v1); }
-          if constexpr (EPI == NR_EPI_GELU) { v0 = gelu_erf(v0); v1 = gelu_erf(v1); }
-          slab[lr * COLS + cl] = v0;
-          slab[lr * COLS + 32 + cl] = v1;
-        }
-      }
+    for (int j = 0; j < 2; ++j) {
+      const int r0 = 128 * h + (wave * 2 + j) * 8;
+      const int row = r0 + (lane >> 3);
+      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+      asrc[h][j] = A + min(m0 + row, M - 1) * lda + chunk * CE;
+      bsrc[h][j] = W + (n0 + row) * ldw + chunk * CE;
+      hoff[h][j] = r0 * 128;
     }
-    __syncthreads();
-    const int rr = lane / LPR, cc = (lane % LPR) * VEC;
+  auto dmaA = [&](int h, int stage, int64_t kt) {
+    unsigned char* sa = smem + stage * G2_STAGE;
 #pragma unroll
-    for (int it = 0; it < 64 / RPI; ++it) {
-      const int lr = it * RPI + rr;
-      const int64_t row = m0 + wm * 128 + pass * 64 + lr;
-      float v[VEC];
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((g_void*)(asrc[h][j] + kt * BK), (lds_void*)(sa + hoff[h][j]), 16, 0, 0);
+  };
+  auto dmaB = [&](int h, int stage, int64_t kt) {
+    unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128;
 #pragma unroll
-      for (int q = 0; q < VEC; q += 4) {
-        const float4 f = *reinterpret_cast<const float4*>(slab + lr * COLS + cc + q);
-        v[q] = f.x; v[q + 1] = f.y; v[q + 2] = f.z; v[q + 3] = f.w;
-      }
-      if (row < M) {
-        if constexpr (EPI == NR_EPI_RESADD || EPI == NR_EPI_DRELU) {
-          const uint4 rv = *reinterpret_cast<const uint4*>(R + row * ldr + ocol0 + cc);
-          float r[VEC];
-          if constexpr (sizeof(TO) == 4) {
-            r[0] = __uint_as_float(rv.x); r[1] = __uint_as_float(rv.y);
-            r[2] = __uint_as_float(rv.z); r[3] = __uint_as_float(rv.w);
-          } else {
-            const uint32_t w4[4] = {rv.x, rv.y, rv.z, rv.w};
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((g_void*)(bsrc[h][j] + kt * BK), (lds_void*)(sb + hoff[h][j]), 16, 0, 0);
+  };
+
+  f32x16 acc[4][2];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) { r[2 * q] = bf16_lo(w4[q]); r[2 * q + 1] = bf16_hi(w4[q]); }
-          }
+  for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-          for (int q = 0; q < VEC; ++q) {
-            if constexpr (EPI == NR_EPI_RESADD) v[q] += r[q];
-            else v[q] = r[q] > 0.f ? v[q] * ea.scale : 0.f;
-          }
-        }
-        TO o[VEC];
+    for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) o[q] = to_out<TO>(v[q]);
-        *reinterpret_cast<uint4*>(C + row * ldc + ocol0 + cc) = *reinterpret_cast<const uint4*>(o);
-      }
-    }
-    __syncthreads();
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+  int aoff[4], boff[2], asw[4], bsw[2];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int row = wm * 128 + mi * 32 + fr;
+    aoff[mi] = row * 128;
+    asw[mi] = (row >> 1) & 7;
   }
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const int row = wn * 64 + ni * 32 + fr;
+    boff[ni] = G2BM * 128 + row * 128;
+    bsw[ni] = (row >> 1) & 7;
+  }
+  // fragment f (0..3) of a 128-byte row slice: bf16 32x32x16 k-step f -> chunk
+  // 2f + h;  f32 32x32x2 group f (4 k-steps) -> chunk 4h + f
+  auto chunk_of = [&](int f) { return sizeof(TI) == 2 ? 2 * f + fh : 4 * fh + f; };
+  typedef f32x4 frag_t;  // 16 bytes: 8 bf16 or 4 f32
+  frag_t fa[2][4], fb0[4], fb1[4];
+  auto readA = [&](int stage, int qm) {
+    const unsigned char* s = smem + stage * G2_STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        fa[i][f] = *reinterpret_cast<const frag_t*>(s + aoff[2 * qm + i] + ((chunk_of(f) ^ asw[2 * qm + i]) << 4));
+  };
+  auto readB = [&](int stage, int ni, frag_t (&fb)[4]) {
+    const unsigned char* s = smem + stage * G2_STAGE;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) fb[f] = *reinterpret_cast<const frag_t*>(s + boff[ni] + ((chunk_of(f) ^ bsw[ni]) << 4));
+  };
+  auto mma = [&](int qm, int ni, const frag_t (&fb)[4]) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if constexpr (sizeof(TI) == 2) {
+          acc[2 * qm + i][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              __builtin_bit_cast(bf16x8, fa[i][f]), __builtin_bit_cast(bf16x8, fb[f]), acc[2 * qm + i][ni], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            acc[2 * qm + i][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][f][t], fb[f][t], acc[2 * qm + i][ni], 0, 0, 0);
+        }
+      }
+  };
+// Phase tail: retire this phase's fragment reads BEFORE the barrier (so the
+// other wave group may re-stage what was read), then the MFMA cluster.
+#define NR_PHASE_SYNC_MMA(QM, NI, FB)                   \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
+  __builtin_amdgcn_sched_barrier(0);                   \
+  __builtin_amdgcn_s_barrier();                        \
+  __builtin_amdgcn_s_setprio(1);                       \
+  mma(QM, NI, FB);                                     \
+  __builtin_amdgcn_s_setprio(0);                       \
+  __builtin_amdgcn_s_barrier();
+
+  // The two wave groups (wm = 0: waves 0-3, wm = 1: waves 4-7; one of each per
+  // SIMD) run one barrier apart, so one group's MFMA cluster overlaps the
+  // other's fragment reads.  Hazard bookkeeping for that stagger: reads are
+  // retired before each phase's first barrier; the tile t+1 landing wait
+  // (vmcnt) sits before P4's FIRST barrier so that the leading group, which
+  // starts reading tile t+1 one barrier after that, sees the lagging group's
+  // DMAs landed too.
+  const int wmu = __builtin_amdgcn_readfirstlane(wm);
+  const int64_t nk = K / BK;
+  dmaB(0, 0, 0);
+  dmaB(1, 0, 0);
+  dmaA(0, 0, 0);
+  dmaA(1, 0, 0);
+  if (nk > 1) {
+    dmaB(0, 1, 1);
+    dmaB(1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wmu == 1) __builtin_amdgcn_s_barrier();  // stagger
+  for (int64_t kt = 0; kt < nk; ++kt) {
+    const int st = (int)(kt & 1), ns = st ^ 1;
+    const bool pre1 = kt + 1 < nk, pre2 = kt + 2 < nk;
+    // P1
+    readA(st, 0);
+    readB(st, 0, fb0);
+    if (pre1) dmaA(0, ns, kt + 1);
+    NR_PHASE_SYNC_MMA(0, 0, fb0)
+    // P2
+    readB(st, 1, fb1);
+    if (pre1) dmaA(1, ns, kt + 1);
+    NR_PHASE_SYNC_MMA(0, 1, fb1)
+    // P3
+    readA(st, 1);
+    if (pre2) dmaB(0, st, kt + 2);
+    NR_PHASE_SYNC_MMA(1, 1, fb1)
+    // P4: tile t+1 must have landed (B0 of t+2 may still fly)
+    if (pre2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (pre2) dmaB(1, st, kt + 2);
+    __builtin_amdgcn_s_setprio(1);
+    mma(1, 0, fb0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (wmu == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+#undef NR_PHASE_SYNC_MMA
+  gemm256_store<EPI, TO>(acc, smem, wave, lane, wm, wn, m0, n0, M, N, bias, R, ldr, C, ldc, ea);
 }
 
 template <typename TI, typename TO>
-static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+static int launch_gemm256_v1(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                           const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
                           void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
   dim3 grid((unsigned)(N / G2BN), (unsigned)((M + G2BM - 1) / G2BM));
@@ -439,10 +646,45 @@ static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* 
     case NR_EPI_GELU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_GELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
     case NR_EPI_RELU_DROPOUT: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_RELU_DROPOUT, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
     case NR_EPI_DRELU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_DRELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_SOFTMAX64: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_SOFTMAX64, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
     default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
   }
   NR_CHECK_LAUNCH("nr_gemm");
   return NR_OK;
+}
+
+template <typename TI, typename TO>
+static int launch_gemm256_p(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                          const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
+                          void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
+  dim3 grid((unsigned)(N / G2BN), (unsigned)((M + G2BM - 1) / G2BM));
+  const TI* a = (const TI*)A;
+  const TI* w = (const TI*)W;
+  const TO* r = (const TO*)R;
+  TO* c = (TO*)C;
+  switch (epi) {
+    case NR_EPI_NONE: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_NONE, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_RELU: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_RELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_EXP: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_EXP, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_GEGLU: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_GEGLU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_RESADD: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_RESADD, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_GELU: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_GELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_RELU_DROPOUT: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_RELU_DROPOUT, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_DRELU: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_DRELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_SOFTMAX64: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_SOFTMAX64, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
+  }
+  NR_CHECK_LAUNCH("nr_gemm");
+  return NR_OK;
+}
+
+template <typename TI, typename TO>
+static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                          const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
+                          void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
+  static const bool v1 = getenv("NR_GEMM_V1") != nullptr;  // A/B switch: the 2-stage glds kernel
+  if (v1) return launch_gemm256_v1<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
+  return launch_gemm256_p<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
 }
 
 template <typename TI, typename TO>
@@ -490,7 +732,7 @@ int gemm_dispatch_ex(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N,
   }
   NR_CHECK_ARG(A && W && C, "nr_gemm: null operand");
   NR_CHECK_ARG((epi != NR_EPI_RESADD && epi != NR_EPI_DRELU) || R, "nr_gemm: RESADD/DRELU need R");
-  NR_CHECK_ARG(epi >= NR_EPI_NONE && epi <= NR_EPI_DRELU, "nr_gemm: bad epilogue %d", epi);
+  NR_CHECK_ARG(epi >= NR_EPI_NONE && epi <= NR_EPI_SOFTMAX64, "nr_gemm: bad epilogue %d", epi);
   const int64_t e16 = dtype_in == NR_F32 ? 4 : 8;  // elements per 16 B
   NR_CHECK_ARG(lda >= K && ldw >= K && lda % e16 == 0 && ldw % e16 == 0 &&
                    ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0,
@@ -505,6 +747,10 @@ int gemm_dispatch_ex(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N,
   const bool aligned_out = ((uintptr_t)C & 15) == 0 && ldc % vo == 0 &&
                            ((epi != NR_EPI_RESADD && epi != NR_EPI_DRELU) || (((uintptr_t)R & 15) == 0 && ldr % vo == 0));
   const bool big = (N % G2BN == 0) && aligned_out && !force_small;
+  if (epi == NR_EPI_SOFTMAX64 && !big) {
+    set_error("nr_gemm: SOFTMAX64 needs N %% 256 == 0 and 16-byte aligned output rows");
+    return NR_ERR_UNSUPPORTED;
+  }
   if (dtype_in == NR_F32) {
     if (big) {
       if (dtype_out == NR_F32) return launch_gemm256<float, float>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);

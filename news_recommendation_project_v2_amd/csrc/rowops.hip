@@ -4,6 +4,8 @@
 // reductions are 64-lane butterflies (no LDS).
 #include "nr_common.h"
 
+#include <stdlib.h>
+
 namespace nr {
 
 // Lane-local load of 4 consecutive elements at element offset `e` (f32 or bf16).
@@ -35,43 +37,97 @@ __device__ __forceinline__ void store4(T* p, const float (&v)[4]) {
   }
 }
 
-// torch.nn.LayerNorm semantics: biased variance, y = (x - mean) * rsqrt(var + eps) * g + b
+// 16-byte lane vectors: E = 16 / sizeof(T) elements.
+template <typename T>
+__device__ __forceinline__ void load16(const T* p, float* v) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  if constexpr (sizeof(T) == 4) {
+    v[0] = __uint_as_float(u.x); v[1] = __uint_as_float(u.y); v[2] = __uint_as_float(u.z); v[3] = __uint_as_float(u.w);
+  } else {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { v[2 * q] = bf16_lo(w[q]); v[2 * q + 1] = bf16_hi(w[q]); }
+  }
+}
+
+template <typename TO, int E>
+__device__ __forceinline__ void storeE(TO* p, const float* v) {
+  if constexpr (sizeof(TO) == 4) {
+#pragma unroll
+    for (int q = 0; q < E; q += 4) *reinterpret_cast<float4*>(p + q) = make_float4(v[q], v[q + 1], v[q + 2], v[q + 3]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < E; q += 8) {
+      __bf16 b8[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) b8[t] = (__bf16)v[q + t];
+      *reinterpret_cast<uint4*>(p + q) = *reinterpret_cast<const uint4*>(b8);
+    }
+  }
+}
+
+// torch.nn.LayerNorm semantics: biased variance, y = (x - mean) * rsqrt(var + eps) * g + b.
+// One wave per row, rows grid-strided over a bounded grid (tiny per-row work
+// would otherwise be dispatch-bound); each lane holds 16-byte chunks, so a
+// wave instruction moves 1 KiB; the whole row stays in registers.
 template <typename TI, typename TO, int DIM>
 __global__ __launch_bounds__(256) void layernorm_kernel(int64_t rows, const TI* __restrict__ x,
                                                         int64_t ldx, const float* __restrict__ g,
                                                         const float* __restrict__ b, float eps,
                                                         TO* __restrict__ y, int64_t ldy) {
-  constexpr int NJ = DIM / 256;
+  constexpr int E = 16 / (int)sizeof(TI);           // elements per lane chunk
+  constexpr int CH = DIM / E;                        // chunks per row
+  constexpr int NJ = (CH + 63) / 64;
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  float v[NJ][4];
-  float s = 0.f;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  // affine parameters of this lane's chunks, loaded once per wave
+  float gv[NJ][E], bv[NJ][E];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    load4<TI>(x + row * ldx + j * 256 + lane * 4, v[j]);
-    s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+    const int c = j * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < E; ++t) {
+      const bool ok = CH % 64 == 0 || c < CH;
+      gv[j][t] = (g && ok) ? g[c * E + t] : 1.f;
+      bv[j][t] = (b && ok) ? b[c * E + t] : 0.f;
+    }
   }
-  const float mean = wave_sum(s) / (float)DIM;
-  float q = 0.f;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += nw) {
+    float v[NJ][E];
+    float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j) {
+      const int c = j * 64 + lane;
+      if (CH % 64 == 0 || c < CH) {
+        load16<TI>(x + row * ldx + c * E, v[j]);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float d = v[j][t] - mean;
-      q = fmaf(d, d, q);
+        for (int t = 0; t < E; ++t) s += v[j][t];
+      }
     }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)DIM + eps);
+    const float mean = wave_sum(s) / (float)DIM;
+    float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int e = j * 256 + lane * 4;
-    float o[4];
+    for (int j = 0; j < NJ; ++j) {
+      const int c = j * 64 + lane;
+      if (CH % 64 == 0 || c < CH) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float gg = g ? g[e + t] : 1.f, bb = b ? b[e + t] : 0.f;
-      o[t] = (v[j][t] - mean) * rstd * gg + bb;
+        for (int t = 0; t < E; ++t) {
+          const float d = v[j][t] - mean;
+          q = fmaf(d, d, q);
+        }
+      }
     }
-    store4<TO>(y + row * ldy + e, o);
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)DIM + eps);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = j * 64 + lane;
+      if (CH % 64 == 0 || c < CH) {
+        float o[E];
+#pragma unroll
+        for (int t = 0; t < E; ++t) o[t] = (v[j][t] - mean) * rstd * gv[j][t] + bv[j][t];
+        storeE<TO, E>(y + row * ldy + c * E, o);
+      }
+    }
   }
 }
 
@@ -115,7 +171,9 @@ __global__ __launch_bounds__(256) void inv_norm_kernel(int64_t rows, const T* __
 template <typename TI, typename TO>
 static int launch_ln(int64_t rows, int64_t dim, const void* x, int64_t ldx, const float* g,
                      const float* b, float eps, void* y, int64_t ldy, hipStream_t s) {
-  const dim3 grid((unsigned)((rows + 3) / 4));
+  const int64_t nb = (rows + 3) / 4;
+  static const int64_t cap = getenv("NR_LN_GRID") ? atoll(getenv("NR_LN_GRID")) : 1024;  // tuning knob (measured best for bf16 at 72k rows)
+  const dim3 grid((unsigned)(cap > 0 && nb > cap ? cap : nb));  // rows grid-strided over <= cap blocks
 #define NR_LN_CASE(D)                                                                      \
   case D:                                                                                  \
     hipLaunchKernelGGL((layernorm_kernel<TI, TO, D>), grid, dim3(256), 0, s, rows,        \
@@ -134,7 +192,10 @@ int layernorm_dispatch(int dti, int dto, int64_t rows, int64_t dim, const void* 
                        const float* g, const float* b, float eps, void* y, int64_t ldy,
                        hipStream_t s) {
   NR_CHECK_ARG((dti == NR_F32 || dti == NR_BF16) && (dto == NR_F32 || dto == NR_BF16), "nr_layernorm: bad dtype");
-  NR_CHECK_ARG(rows >= 0 && ldx >= dim && ldy >= dim && ldx % 4 == 0 && ldy % 4 == 0, "nr_layernorm: bad strides");
+  NR_CHECK_ARG(rows >= 0 && ldx >= dim && ldy >= dim, "nr_layernorm: bad strides");
+  NR_CHECK_ARG((ldx * (dti == NR_F32 ? 4 : 2)) % 16 == 0 && (ldy * (dto == NR_F32 ? 4 : 2)) % 16 == 0 &&
+                   ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0,
+               "nr_layernorm: rows must be 16-byte aligned");
   if (rows == 0) return NR_OK;
   NR_CHECK_ARG(x && y, "nr_layernorm: null pointer");
   if (dti == NR_F32) {

@@ -21,6 +21,7 @@ _EPI = {
     "geglu": _lib.NR_EPI_GEGLU,
     "resadd": _lib.NR_EPI_RESADD,
     "gelu": _lib.NR_EPI_GELU,
+    "softmax64": _lib.NR_EPI_SOFTMAX64,
 }
 POOLERS = {"final": _lib.NR_POOL_FINAL, "latent": _lib.NR_POOL_LATENT}
 

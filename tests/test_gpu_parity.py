@@ -287,3 +287,54 @@ def test_eval_script_synthetic_end_to_end(gpu_device, tmp_path, monkeypatch):
         for k in ("train_scores", "val_scores"):
             s = rec[k]
             assert s["num_samples"] == 300 and 0.0 <= s["auc"] <= 1.0 and 0.0 < s["mrr"] <= 1.0
+
+
+# Race screen for the pipelined 256x256 kernel (staggered wave groups, DMA in
+# flight across barriers): many K-tile counts incl. 1 and 2, ragged M, both
+# dtypes, repeated launches compared against a float64 product of the same
+# (bf16-rounded) operands.
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_gemm256_pipeline_race_screen(gpu_device, dt):
+    bk = 64 if dt == torch.bfloat16 else 32
+    shapes = [(256, 256, bk), (300, 256, 2 * bk), (513, 768, 3 * bk), (1000, 512, 1024), (4099, 1024, 4096),
+              (2048, 4096, 512)]
+    g = torch.Generator(device=gpu_device).manual_seed(7)
+    for M, N, K in shapes:
+        a = torch.randn(M, K, device=gpu_device, generator=g).to(dt)
+        w = torch.randn(N, K, device=gpu_device, generator=g).to(dt)
+        ref = (a.double() @ w.double().T)
+        tol = 2e-5 * K ** 0.5 if dt == torch.float32 else 1e-5 * K ** 0.5
+        for _ in range(3):
+            out = ops.gemm(a, w, out_dtype=torch.float32)
+            torch.cuda.synchronize()
+            err = float((out.double() - ref).abs().max())
+            assert err <= tol * float(ref.abs().max()) + 1e-4, (M, N, K, err)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_softmax64_epilogue(gpu_device, dt):
+    """Score GEMM + per-64-column softmax (latent_attention.py:72's SDPA softmax over
+    the 64 latents) fused in the epilogue vs an fp64 torch restatement."""
+    g = torch.Generator(device=gpu_device).manual_seed(3)
+    M, N, K = 1000, 512, 1024
+    a = (torch.randn(M, K, device=gpu_device, generator=g) * 0.1).to(dt)
+    w = (torch.randn(N, K, device=gpu_device, generator=g) * 0.1).to(dt)
+    b = torch.randn(N, device=gpu_device, generator=g)
+    out = ops.gemm(a, w, b, epilogue="softmax64", out_dtype=torch.float32)
+    ref = torch.softmax((a.double() @ w.double().T + b.double()).reshape(M, N // 64, 64), dim=-1).reshape(M, N)
+    torch.cuda.synchronize()
+    assert float((out.double() - ref).abs().max()) < 1e-5
+    assert torch.allclose(out.double().reshape(M, 8, 64).sum(-1), torch.ones(M, 8, dtype=torch.float64, device=gpu_device), atol=1e-5)
+
+
+@pytest.mark.parametrize("dim", [256, 768, 1024, 2048])
+@pytest.mark.parametrize("dti,dto", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16),
+                                     (torch.float32, torch.bfloat16)])
+def test_layernorm_shapes(gpu_device, dim, dti, dto):
+    x = (torch.randn(3001, dim, device=gpu_device) * 3 + 1).to(dti)
+    gm = torch.rand(dim, device=gpu_device) + 0.5
+    bt = torch.randn(dim, device=gpu_device)
+    out = ops.layernorm(x, gm, bt, 1e-5, out_dtype=dto)
+    ref = torch.nn.functional.layer_norm(x.double(), (dim,), gm.double(), bt.double(), 1e-5)
+    tol = 1e-5 if dto == torch.float32 else 8e-3 * float(ref.abs().max())  # bf16 output rounding
+    assert float((out.double() - ref).abs().max()) < tol
