@@ -141,11 +141,64 @@ def timed(run: Run, steps: int, warmup: int, world: int, dev):
 
 
 def auc_of(run: Run) -> float:
+    """Mean AUC over all impressions: dense ranks + per-impression metrics on the
+    device (nr_dense_rank, nr_impression_metrics; == evaluation.score, tested)."""
     from news_recommendation_project_v2_amd import evaluation
     s, _ = run.step()
-    r = run.eng.rank(s).cpu().numpy()
-    a, _, _, _ = evaluation.score_arrays(r, run.imps.labels, run.imps.cand_off())
-    return float(np.mean(a))
+    r = run.eng.rank(s)
+    return float(evaluation.score_device(r, run.imps.labels, run.imps.cand_off())["auc"])
+
+
+def metrics_ms(run: Run, reps: int = 3) -> float:
+    """Device time of dense ranks + MIND metrics over the whole workload."""
+    from news_recommendation_project_v2_amd import ops
+    s, _ = run.step()
+    y = torch.as_tensor(np.asarray(run.imps.labels, dtype=np.float32)).to(s.device)
+    off = torch.as_tensor(run.imps.cand_off()).to(s.device)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        r = run.eng.rank(s)
+        ops.impression_metrics(r, y, off)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def train_step_ms(dev, batch_rows: int = 256, steps: int = 10) -> dict:
+    """Config 5 (BASELINE configs[4]): one FinalAttentionTrainStep (fwd + bwd +
+    clip + AdamW, bf16 MFMA) on a synthetic MIND-shaped batch."""
+    from news_recommendation_project_v2_amd.modeling_utils import get_token_attn_model
+    from news_recommendation_project_v2_amd.train_step import FinalAttentionTrainStep, TrainBatch
+    rng = np.random.default_rng(1234)
+    h = np.clip(rng.geometric(1 / 33.0, batch_rows), 1, 600)
+    ids = rng.integers(0, 40_000, int(h.sum()) + 2 * batch_rows)
+    uniq, rev = np.unique(ids, return_inverse=True)
+    Hs = int(h.sum())
+    tok = torch.randn((len(uniq), 1024), generator=torch.Generator().manual_seed(1)).half().to(dev)
+    b = TrainBatch(tok, torch.as_tensor(rev[:Hs].astype(np.int32)).to(dev),
+                   torch.as_tensor(np.concatenate([[0], np.cumsum(h)]).astype(np.int64)).to(dev),
+                   torch.as_tensor(rev[Hs:Hs + batch_rows].astype(np.int32)).to(dev),
+                   torch.as_tensor(rev[Hs + batch_rows:].astype(np.int32)).to(dev))
+    tm = get_token_attn_model()
+    tm.load_state_dict(W.token_attn_state_dict(1234))
+    fa = FinalAttention(1024, 4096)
+    fa.load_state_dict(W.final_attention_state_dict(1234))
+    eng = FinalAttentionTrainStep(tm, fa.to(dev), dtype=torch.bfloat16, device=dev)
+    for _ in range(3):
+        eng.step(b)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        eng.step(b)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    return {"batch_rows": batch_rows, "history_slots": Hs, "ms_per_step": round(ms, 3),
+            "rows_per_s": round(batch_rows / ms * 1e3, 1),
+            "gemm_tflops": round(eng.flops_per_step(Hs) / ms / 1e9, 1)}
 
 
 def cpu_baseline(pooler: str, imps, table_cpu: torch.Tensor, budget_s: float):
@@ -254,6 +307,8 @@ def main():
                 extra["auc"]["abs_diff"] = abs(extra["auc"][args.dtype] - extra["auc"][dtype])
             del r
             torch.cuda.empty_cache()
+        extra["metrics_ms"] = round(metrics_ms(head), 3)
+        extra["train_bf16_config5"] = train_step_ms(dev)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
