@@ -24,8 +24,27 @@ namespace nr {
 constexpr int GBM = 128, GBN = 128;
 constexpr int GROW = 36;  // LDS row stride in 32-bit words (128 B data + 16 B pad)
 
-__device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+// Exact-erf GELU, 0.5 g (1 + erf(g / sqrt 2)) (F.gelu default: latent_attention.py:27,
+// XLM-R hidden_act "gelu"), written through erfc(z) = t exp(-z^2 + P(t)),
+// t = 1 / (1 + z / 2) (Numerical Recipes erfcc: fractional error < 1.2e-7
+// everywhere).  Branch-free: ~16 VALU ops instead of the divergent two-range
+// erff, which dominated the GEGLU epilogue.  |gelu - exact| <= 6.1e-7 for
+// |g| <= 12 (checked in float64), i.e. f32 rounding level.
+__device__ __forceinline__ float gelu_erf(float g) {
+  const float x = g * 0.70710678118654752440f;
+  const float z = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  const float ans = t * __expf(fmaf(t, p, fmaf(-z, z, -1.26551223f)));  // erfc(|x|)
+  return x >= 0.f ? g * fmaf(-0.5f, ans, 1.0f) : 0.5f * g * ans;
 }
 
 // Extra epilogue arguments (dropout of the training forward; unused otherwise).
@@ -233,8 +252,17 @@ typedef const __attribute__((address_space(1))) void g_void;
 // Epilogue of the 256x256 kernels (acc[4][2] per wave: rows wm*128 + 32 mi,
 // cols wn*64 + 32 ni), staged through the kernel's LDS (caller has finished
 // with the operand stages and passed a barrier).
-template <int EPI, typename TO>
-__device__ __forceinline__ void gemm256_store(const f32x16 (&acc)[4][2], unsigned char* smem, int wave, int lane,
+template <bool MF16>
+struct Acc256 {  // per-wave 128x64 accumulators: 4x2 tiles of 32x32, or 8x4 tiles of 16x16
+  typedef f32x16 type[4][2];
+};
+template <>
+struct Acc256<true> {
+  typedef f32x4 type[8][4];
+};
+
+template <int EPI, typename TO, bool MF16 = false>
+__device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type& acc, unsigned char* smem, int wave, int lane,
                                               int wm, int wn, int64_t m0, int64_t n0, int64_t M, int64_t N,
                                               const float* __restrict__ bias, const TO* R, int64_t ldr, TO* C,
                                               int64_t ldc, const EpiArgs& ea) {
@@ -252,9 +280,48 @@ __device__ __forceinline__ void gemm256_store(const f32x16 (&acc)[4][2], unsigne
   const int64_t wcol = n0 + wn * 64;
   const int64_t ocol0 = (EPI == NR_EPI_GEGLU) ? wcol / 2 : wcol;
   float ba = 0.f, bg = 0.f;
-  if (bias) { ba = bias[wcol + cl]; bg = bias[wcol + 32 + cl]; }
+  float b16[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (MF16) {
+    if (bias) {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) b16[ni] = bias[wcol + 16 * ni + (lane & 15)];
+    }
+  } else if (bias) {
+    ba = bias[wcol + cl];
+    bg = bias[wcol + 32 + cl];
+  }
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
+    if constexpr (MF16) {
+      // 16x16 C/D map: col = lane & 15, row = 4 * (lane >> 4) + r
+      const int c16 = lane & 15, r16 = 4 * (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int mi = 4 * pass + i;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = 16 * i + r16 + r;
+          if constexpr (EPI == NR_EPI_GEGLU) {
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+              slab[lr * COLS + 16 * ni + c16] = (acc[mi][ni][r] + b16[ni]) * gelu_erf(acc[mi][ni + 2][r] + b16[ni + 2]);
+          } else {
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+              float v = acc[mi][ni][r] + b16[ni];
+              if constexpr (EPI == NR_EPI_RELU) v = fmaxf(v, 0.f);
+              if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
+                const uint64_t gi = (uint64_t)((m0 + wm * 128 + pass * 64 + lr) * N + wcol + 16 * ni + c16);
+                v = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(v, 0.f) * ea.scale;
+              }
+              if constexpr (EPI == NR_EPI_EXP) v = expf(v);
+              if constexpr (EPI == NR_EPI_GELU) v = gelu_erf(v);
+              slab[lr * COLS + 16 * ni + c16] = v;
+            }
+          }
+        }
+      }
+    } else
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int mi = 2 * pass + h;
@@ -464,7 +531,7 @@ __global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, i
 // phase ends lgkmcnt(0) + barrier).  Block ids are remapped XCD-aware so the
 // N-tiles that share an A panel run on one XCD (its L2 holds the panel).
 // Same LDS images, swizzle and epilogue as gemm256_kernel.
-template <typename TI, int EPI, typename TO>
+template <typename TI, int EPI, typename TO, bool MF16 = false>
 __global__ __launch_bounds__(512, 2) void gemm256p_kernel(int64_t M, int64_t N, int64_t K,
                                                           const TI* __restrict__ A, int64_t lda,
                                                           const TI* __restrict__ W, int64_t ldw,
@@ -509,63 +576,93 @@ __global__ __launch_bounds__(512, 2) void gemm256p_kernel(int64_t M, int64_t N, 
       __builtin_amdgcn_global_load_lds((g_void*)(bsrc[h][j] + kt * BK), (lds_void*)(sb + hoff[h][j]), 16, 0, 0);
   };
 
-  f32x16 acc[4][2];
+  typename Acc256<MF16>::type acc;
+  if constexpr (MF16) {
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
+      for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+        for (int r = 0; r < 4; ++r) acc[mi][ni][r] = 0.f;
+  } else {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+  }
 
   const int fr = lane & 31, fh = lane >> 5;
-  int aoff[4], boff[2], asw[4], bsw[2];
+  // 32x32 operand tiles (MF16 = false): 4 A tiles of 32 rows, 2 B tiles of 32 columns
+  // 16x16 operand tiles (MF16 = true):  8 A tiles of 16 rows, 4 B tiles of 16 columns
+  constexpr int TA = MF16 ? 8 : 4, TB = MF16 ? 4 : 2, TR = MF16 ? 16 : 32;
+  const int lr_ = MF16 ? (lane & 15) : fr;
+  int aoff[TA], boff[TB], asw[TA], bsw[TB];
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
-    const int row = wm * 128 + mi * 32 + fr;
+  for (int mi = 0; mi < TA; ++mi) {
+    const int row = wm * 128 + mi * TR + lr_;
     aoff[mi] = row * 128;
     asw[mi] = (row >> 1) & 7;
   }
 #pragma unroll
-  for (int ni = 0; ni < 2; ++ni) {
-    const int row = wn * 64 + ni * 32 + fr;
+  for (int ni = 0; ni < TB; ++ni) {
+    const int row = wn * 64 + ni * TR + lr_;
     boff[ni] = G2BM * 128 + row * 128;
     bsw[ni] = (row >> 1) & 7;
   }
-  // fragment f (0..3) of a 128-byte row slice: bf16 32x32x16 k-step f -> chunk
-  // 2f + h;  f32 32x32x2 group f (4 k-steps) -> chunk 4h + f
-  auto chunk_of = [&](int f) { return sizeof(TI) == 2 ? 2 * f + fh : 4 * fh + f; };
+  // fragment f of a 128-byte row slice:
+  //   bf16 32x32x16 k-step f (4 per tile) -> chunk 2f + (lane >> 5)
+  //   bf16 16x16x32 k-step f (2 per tile) -> chunk 4f + (lane >> 4)
+  //   f32  32x32x2 group f (4 k-steps)    -> chunk 4 (lane >> 5) + f
+  auto chunk_of = [&](int f) {
+    if constexpr (MF16) return 4 * f + (lane >> 4);
+    else return sizeof(TI) == 2 ? 2 * f + fh : 4 * fh + f;
+  };
   typedef f32x4 frag_t;  // 16 bytes: 8 bf16 or 4 f32
-  frag_t fa[2][4], fb0[4], fb1[4];
+  constexpr int QA = MF16 ? 4 : 2;   // A tiles per 64-row quadrant
+  constexpr int QB = MF16 ? 2 : 1;   // B tiles per 32-column quadrant
+  constexpr int NF = MF16 ? 2 : 4;   // fragments (k-steps or groups) per tile per K tile
+  frag_t fa[QA][NF], fb0[QB][NF], fb1[QB][NF];
   auto readA = [&](int stage, int qm) {
     const unsigned char* s = smem + stage * G2_STAGE;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < QA; ++i)
 #pragma unroll
-      for (int f = 0; f < 4; ++f)
-        fa[i][f] = *reinterpret_cast<const frag_t*>(s + aoff[2 * qm + i] + ((chunk_of(f) ^ asw[2 * qm + i]) << 4));
+      for (int f = 0; f < NF; ++f)
+        fa[i][f] = *reinterpret_cast<const frag_t*>(s + aoff[QA * qm + i] + ((chunk_of(f) ^ asw[QA * qm + i]) << 4));
   };
-  auto readB = [&](int stage, int ni, frag_t (&fb)[4]) {
+  auto readB = [&](int stage, int qn, frag_t (&fb)[QB][NF]) {
     const unsigned char* s = smem + stage * G2_STAGE;
 #pragma unroll
-    for (int f = 0; f < 4; ++f) fb[f] = *reinterpret_cast<const frag_t*>(s + boff[ni] + ((chunk_of(f) ^ bsw[ni]) << 4));
+    for (int j = 0; j < QB; ++j)
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+        fb[j][f] = *reinterpret_cast<const frag_t*>(s + boff[QB * qn + j] + ((chunk_of(f) ^ bsw[QB * qn + j]) << 4));
   };
-  auto mma = [&](int qm, int ni, const frag_t (&fb)[4]) {
+  auto mma = [&](int qm, int qn, const frag_t (&fb)[QB][NF]) {
 #pragma unroll
-    for (int f = 0; f < 4; ++f)
+    for (int f = 0; f < NF; ++f)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if constexpr (sizeof(TI) == 2) {
-          acc[2 * qm + i][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              __builtin_bit_cast(bf16x8, fa[i][f]), __builtin_bit_cast(bf16x8, fb[f]), acc[2 * qm + i][ni], 0, 0, 0);
-        } else {
+      for (int i = 0; i < QA; ++i)
 #pragma unroll
-          for (int t = 0; t < 4; ++t)
-            acc[2 * qm + i][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][f][t], fb[f][t], acc[2 * qm + i][ni], 0, 0, 0);
+        for (int j = 0; j < QB; ++j) {
+          if constexpr (MF16) {
+            acc[QA * qm + i][QB * qn + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, fa[i][f]), __builtin_bit_cast(bf16x8, fb[j][f]), acc[QA * qm + i][QB * qn + j],
+                0, 0, 0);
+          } else if constexpr (sizeof(TI) == 2) {
+            acc[QA * qm + i][QB * qn + j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                __builtin_bit_cast(bf16x8, fa[i][f]), __builtin_bit_cast(bf16x8, fb[j][f]), acc[QA * qm + i][QB * qn + j],
+                0, 0, 0);
+          } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+              acc[QA * qm + i][QB * qn + j] =
+                  __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][f][t], fb[j][f][t], acc[QA * qm + i][QB * qn + j], 0, 0, 0);
+          }
         }
-      }
   };
-// Phase tail: retire this phase's fragment reads BEFORE the barrier (so the
-// other wave group may re-stage what was read), then the MFMA cluster.
 #define NR_PHASE_SYNC_MMA(QM, NI, FB)                   \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
   __builtin_amdgcn_sched_barrier(0);                   \
@@ -625,7 +722,330 @@ __global__ __launch_bounds__(512, 2) void gemm256p_kernel(int64_t M, int64_t N, 
   }
   if (wmu == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
 #undef NR_PHASE_SYNC_MMA
-  gemm256_store<EPI, TO>(acc, smem, wave, lane, wm, wn, m0, n0, M, N, bias, R, ldr, C, ldc, ea);
+  gemm256_store<EPI, TO, MF16>(acc, smem, wave, lane, wm, wn, m0, n0, M, N, bias, R, ldr, C, ldc, ea);
+}
+
+// ---------------------------------------------------------------------------
+// Persistent bf16 variant (16x16x32 MFMA tiles): one 512-thread workgroup per
+// CU walks its share of the 256x256 output tiles.  The main loop is
+// gemm256p_kernel's; what changes is the tile boundary: as soon as a tile's K
+// loop ends, the NEXT tile's prologue DMAs (K tile 0, and K tile 1's B halves)
+// are issued into the two operand stages, and the finished tile's epilogue
+// runs from a separate 32 KiB LDS region (a 4 KiB, 16-row slab per wave) while
+// they fly.  With one workgroup per CU (234 VGPRs, 160 KiB LDS) the prologue
+// latency and the epilogue (GEGLU's erf, stores) would otherwise be exposed
+// once per tile: at K = 512-1024 that is 10-20 % of a tile.  Tiles are split
+// into 8 contiguous ranges, one per XCD (workgroups b = x mod 8), so the tiles
+// an XCD runs concurrently share A panels in its L2.
+template <int EPI, typename TO>
+__device__ __forceinline__ void epi16_store(const f32x4 (&acc)[8][4], float* slab, int lane, int wm, int wn,
+                                            int64_t m0, int64_t n0, int64_t M, int64_t N,
+                                            const float* __restrict__ bias, const TO* R, int64_t ldr, TO* C,
+                                            int64_t ldc, const EpiArgs& ea) {
+  constexpr int COLS = (EPI == NR_EPI_GEGLU) ? 32 : 64;
+  constexpr int VEC = 16 / (int)sizeof(TO);
+  constexpr int LPR = COLS / VEC;
+  constexpr int RPI = 64 / LPR;
+  constexpr int ITS = 16 / RPI;
+  const int64_t wcol = n0 + wn * 64;
+  const int64_t ocol0 = (EPI == NR_EPI_GEGLU) ? wcol / 2 : wcol;
+  const int c16 = lane & 15, r16 = 4 * (lane >> 4);
+  float b16[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bias) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) b16[ni] = bias[wcol + 16 * ni + c16];
+  }
+  // slab [16][COLS] f32; column bit 4 flipped on rows 4-7 / 12-15 so the two
+  // 16-lane halves of a 32-lane store group hit different banks
+  auto sidx = [](int row, int col) { return row * COLS + (col ^ ((row & 4) << 2)); };
+  const int rr = lane / LPR, cc = (lane % LPR) * VEC;
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = r16 + r;
+      if constexpr (EPI == NR_EPI_GEGLU) {
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          slab[sidx(row, 16 * ni + c16)] = (acc[mi][ni][r] + b16[ni]) * gelu_erf(acc[mi][ni + 2][r] + b16[ni + 2]);
+      } else {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          float v = acc[mi][ni][r] + b16[ni];
+          if constexpr (EPI == NR_EPI_RELU) v = fmaxf(v, 0.f);
+          if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
+            const uint64_t gi = (uint64_t)((m0 + wm * 128 + mi * 16 + row) * N + wcol + 16 * ni + c16);
+            v = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(v, 0.f) * ea.scale;
+          }
+          if constexpr (EPI == NR_EPI_EXP) v = expf(v);
+          if constexpr (EPI == NR_EPI_GELU) v = gelu_erf(v);
+          slab[sidx(row, 16 * ni + c16)] = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < ITS; ++it) {
+      const int lr = it * RPI + rr;
+      const int64_t row = m0 + wm * 128 + mi * 16 + lr;
+      float v[VEC];
+#pragma unroll
+      for (int q = 0; q < VEC; q += 4) {
+        const float4 f = *reinterpret_cast<const float4*>(slab + sidx(lr, cc + q));
+        v[q] = f.x; v[q + 1] = f.y; v[q + 2] = f.z; v[q + 3] = f.w;
+      }
+      if constexpr (EPI == NR_EPI_SOFTMAX64) {
+        float m = v[0];
+#pragma unroll
+        for (int q = 1; q < VEC; ++q) m = fmaxf(m, v[q]);
+#pragma unroll
+        for (int o = 1; o < LPR; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        float sum = 0.f;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) { v[q] = expf(v[q] - m); sum += v[q]; }
+#pragma unroll
+        for (int o = 1; o < LPR; o <<= 1) sum += __shfl_xor(sum, o, 64);
+        const float inv = 1.0f / sum;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) v[q] *= inv;
+      }
+      if (row < M) {
+        if constexpr (EPI == NR_EPI_RESADD || EPI == NR_EPI_DRELU) {
+          const uint4 rv = *reinterpret_cast<const uint4*>(R + row * ldr + ocol0 + cc);
+          float rf[VEC];
+          if constexpr (sizeof(TO) == 4) {
+            rf[0] = __uint_as_float(rv.x); rf[1] = __uint_as_float(rv.y);
+            rf[2] = __uint_as_float(rv.z); rf[3] = __uint_as_float(rv.w);
+          } else {
+            const uint32_t w4[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { rf[2 * q] = bf16_lo(w4[q]); rf[2 * q + 1] = bf16_hi(w4[q]); }
+          }
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) {
+            if constexpr (EPI == NR_EPI_RESADD) v[q] += rf[q];
+            else v[q] = rf[q] > 0.f ? v[q] * ea.scale : 0.f;
+          }
+        }
+        TO o[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) o[q] = to_out<TO>(v[q]);
+        *reinterpret_cast<uint4*>(C + row * ldc + ocol0 + cc) = *reinterpret_cast<const uint4*>(o);
+      }
+    }
+  }
+}
+
+constexpr int G2_EPI_SLAB = 16 * 64 * 4;  // bytes per wave
+
+template <int EPI, typename TO>
+__global__ __launch_bounds__(512, 2) void gemm256pp_kernel(int64_t M, int64_t N, int64_t K,
+                                                           const __bf16* __restrict__ A, int64_t lda,
+                                                           const __bf16* __restrict__ W, int64_t ldw,
+                                                           const float* __restrict__ bias, const TO* R,
+                                                           int64_t ldr, TO* C, int64_t ldc, EpiArgs ea,
+                                                           int tiles_n, int n_tiles) {
+  typedef __bf16 TI;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE + 8 * G2_EPI_SLAB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int wmu = __builtin_amdgcn_readfirstlane(wm);
+  float* slab = reinterpret_cast<float*>(smem + 2 * G2_STAGE + wave * G2_EPI_SLAB);
+
+  // tile schedule: XCD group x = blockIdx % 8 owns a contiguous range of tiles
+  const int G = (int)gridDim.x;
+  int t, t_end, t_step;
+  if (G % 8 == 0 && G >= 8) {
+    const int x = (int)blockIdx.x & 7, li = (int)blockIdx.x >> 3;
+    const int q = n_tiles >> 3, r = n_tiles & 7;
+    const int lo = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    t = lo + li;
+    t_end = lo + q + (x < r ? 1 : 0);
+    t_step = G >> 3;
+  } else {
+    t = (int)blockIdx.x;
+    t_end = n_tiles;
+    t_step = G;
+  }
+  if (t >= t_end) return;  // workgroup-uniform
+
+  constexpr int BK = 64, CE = 8;
+  // DMA addressing recomputed per issue from tile-uniform m0/n0 and a few
+  // lane constants (keeps ~16 VGPRs of 64-bit pointers out of the persistent
+  // loop).  Lane l of wave w fills row 128h + 16w + 8j + l/8, 16-B chunk
+  // (l & 7) ^ ((4j + l/16) & 7) of the swizzled image (= chunk ^ (row>>1 & 7)).
+  int64_t tm0 = 0, tn0 = 0;
+  const int rl = 16 * wave + (lane >> 3);
+  auto cj = [&](int j) { return (lane & 7) ^ ((4 * j + (lane >> 4)) & 7); };
+  auto dmaA = [&](int h, int stage, int64_t kt) {
+    unsigned char* sa = smem + stage * G2_STAGE;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t row = min(tm0 + 128 * h + 8 * j + rl, M - 1);
+      const TI* src = A + row * lda + cj(j) * CE + kt * BK;
+      __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(sa + (128 * h + 16 * wave + 8 * j) * 128), 16, 0, 0);
+    }
+  };
+  auto dmaB = [&](int h, int stage, int64_t kt) {
+    unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const TI* src = W + (tn0 + 128 * h + 8 * j + rl) * ldw + cj(j) * CE + kt * BK;
+      __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(sb + (128 * h + 16 * wave + 8 * j) * 128), 16, 0, 0);
+    }
+  };
+  auto setup = [&](int tile) {
+    tn0 = (int64_t)(tile % tiles_n) * G2BN;
+    tm0 = (int64_t)(tile / tiles_n) * G2BM;
+  };
+  const int64_t nk = K / BK;
+  auto prologue = [&]() {
+    dmaB(0, 0, 0);
+    dmaB(1, 0, 0);
+    dmaA(0, 0, 0);
+    dmaA(1, 0, 0);
+    if (nk > 1) {
+      dmaB(0, 1, 1);
+      dmaB(1, 1, 1);
+    }
+  };
+
+  // fragment addresses: 16x16x32 tiles; the swizzle term (row >> 1) & 7 is
+  // the same for every tile of a lane (tiles are 16 rows apart)
+  const int c16 = lane & 15;
+  const int sw = (c16 >> 1) & 7;
+  const int abase = (wm * 128 + c16) * 128;
+  const int bbase = G2BM * 128 + (wn * 64 + c16) * 128;
+  const int cf0 = ((0 + (lane >> 4)) ^ sw) << 4, cf1 = ((4 + (lane >> 4)) ^ sw) << 4;
+  typedef f32x4 frag_t;
+  frag_t fa[4][2], fb0[2][2], fb1[2][2];
+  f32x4 acc[8][4];
+  auto readA = [&](int stage, int qm) {
+    const unsigned char* sp = smem + stage * G2_STAGE + abase + qm * 4 * 2048;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[i][0] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf0);
+      fa[i][1] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf1);
+    }
+  };
+  auto readB = [&](int stage, int qn, frag_t (&fb)[2][2]) {
+    const unsigned char* sp = smem + stage * G2_STAGE + bbase + qn * 2 * 2048;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      fb[j][0] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf0);
+      fb[j][1] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf1);
+    }
+  };
+  auto mma = [&](int qm, int qn, const frag_t (&fb)[2][2]) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * qm + i][2 * qn + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, fa[i][f]), __builtin_bit_cast(bf16x8, fb[j][f]), acc[4 * qm + i][2 * qn + j],
+              0, 0, 0);
+  };
+#define NR_PHASE_SYNC_MMA(QM, NI, FB)                   \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
+  __builtin_amdgcn_sched_barrier(0);                   \
+  __builtin_amdgcn_s_barrier();                        \
+  __builtin_amdgcn_s_setprio(1);                       \
+  mma(QM, NI, FB);                                     \
+  __builtin_amdgcn_s_setprio(0);                       \
+  __builtin_amdgcn_s_barrier();
+
+  setup(t);
+  prologue();
+  while (true) {
+    // this tile's prologue DMAs (and the previous tile's epilogue stores) landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wmu == 1) __builtin_amdgcn_s_barrier();  // stagger the wave groups
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[mi][ni][r] = 0.f;
+    for (int64_t kt = 0; kt < nk; ++kt) {
+      const int st = (int)(kt & 1), ns = st ^ 1;
+      const bool pre1 = kt + 1 < nk, pre2 = kt + 2 < nk;
+      readA(st, 0);
+      readB(st, 0, fb0);
+      if (pre1) dmaA(0, ns, kt + 1);
+      NR_PHASE_SYNC_MMA(0, 0, fb0)
+      readB(st, 1, fb1);
+      if (pre1) dmaA(1, ns, kt + 1);
+      NR_PHASE_SYNC_MMA(0, 1, fb1)
+      readA(st, 1);
+      if (pre2) dmaB(0, st, kt + 2);
+      NR_PHASE_SYNC_MMA(1, 1, fb1)
+      if (pre2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (pre2) dmaB(1, st, kt + 2);
+      __builtin_amdgcn_s_setprio(1);
+      mma(1, 0, fb0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+    }
+    if (wmu == 0) __builtin_amdgcn_s_barrier();  // re-align the groups: every stage read is retired
+    const int64_t n0 = tn0, m0 = tm0;
+    const int tn = t + t_step;
+    const bool more = tn < t_end;
+    if (more) {  // next tile's operands fly while this tile's epilogue runs
+      setup(tn);
+      prologue();
+    }
+    epi16_store<EPI, TO>(acc, slab, lane, wm, wn, m0, n0, M, N, bias, R, ldr, C, ldc, ea);
+    if (!more) break;
+    t = tn;
+  }
+#undef NR_PHASE_SYNC_MMA
+}
+
+template <typename TO>
+static int launch_gemm256_pp(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                             const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
+                             void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
+  const int tiles_n = (int)(N / G2BN);
+  const int64_t tiles = (int64_t)tiles_n * ((M + G2BM - 1) / G2BM);
+  if (tiles > (1ll << 30)) {
+    set_error("nr_gemm: too many tiles");
+    return NR_ERR_UNSUPPORTED;
+  }
+  const int nt = (int)tiles;
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    n_cu = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+               ? prop.multiProcessorCount : 256;
+    n_cu = n_cu / 8 * 8;
+    if (n_cu < 8) n_cu = 8;
+  }
+  const dim3 grid((unsigned)(nt < n_cu ? nt : n_cu));
+  const __bf16* a = (const __bf16*)A;
+  const __bf16* w = (const __bf16*)W;
+  const TO* r = (const TO*)R;
+  TO* c = (TO*)C;
+#define NR_PP(E) hipLaunchKernelGGL((gemm256pp_kernel<E, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea, tiles_n, nt)
+  switch (epi) {
+    case NR_EPI_NONE: NR_PP(NR_EPI_NONE); break;
+    case NR_EPI_RELU: NR_PP(NR_EPI_RELU); break;
+    case NR_EPI_EXP: NR_PP(NR_EPI_EXP); break;
+    case NR_EPI_GEGLU: NR_PP(NR_EPI_GEGLU); break;
+    case NR_EPI_RESADD: NR_PP(NR_EPI_RESADD); break;
+    case NR_EPI_GELU: NR_PP(NR_EPI_GELU); break;
+    case NR_EPI_RELU_DROPOUT: NR_PP(NR_EPI_RELU_DROPOUT); break;
+    case NR_EPI_DRELU: NR_PP(NR_EPI_DRELU); break;
+    case NR_EPI_SOFTMAX64: NR_PP(NR_EPI_SOFTMAX64); break;
+    default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
+  }
+#undef NR_PP
+  NR_CHECK_LAUNCH("nr_gemm");
+  return NR_OK;
 }
 
 template <typename TI, typename TO>
@@ -679,11 +1099,44 @@ static int launch_gemm256_p(int epi, int64_t M, int64_t N, int64_t K, const void
 }
 
 template <typename TI, typename TO>
+static int launch_gemm256_p16(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                          const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
+                          void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
+  dim3 grid((unsigned)(N / G2BN), (unsigned)((M + G2BM - 1) / G2BM));
+  const TI* a = (const TI*)A;
+  const TI* w = (const TI*)W;
+  const TO* r = (const TO*)R;
+  TO* c = (TO*)C;
+  switch (epi) {
+    case NR_EPI_NONE: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_NONE, TO, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_RELU: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_RELU, TO, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_EXP: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_EXP, TO, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_GEGLU: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_GEGLU, TO, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_RESADD: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_RESADD, TO, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_GELU: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_GELU, TO, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_RELU_DROPOUT: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_RELU_DROPOUT, TO, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_DRELU: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_DRELU, TO, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    case NR_EPI_SOFTMAX64: hipLaunchKernelGGL((gemm256p_kernel<TI, NR_EPI_SOFTMAX64, TO, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
+    default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
+  }
+  NR_CHECK_LAUNCH("nr_gemm");
+  return NR_OK;
+}
+
+template <typename TI, typename TO>
 static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                           const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
                           void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
   static const bool v1 = getenv("NR_GEMM_V1") != nullptr;  // A/B switch: the 2-stage glds kernel
+  // bf16 default: 16x16x32 MFMA tiles (5-8 % faster than 32x32x16 on the pooler shapes,
+  // profiles/round1/s2/gemm_mf16_vs_mf32.txt); NR_GEMM_MF32=1 selects the 32x32x16 tiles
+  static const bool mf16 = getenv("NR_GEMM_MF32") == nullptr;
   if (v1) return launch_gemm256_v1<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
+  static const bool nopersist = getenv("NR_GEMM_NOPERSIST") != nullptr;  // A/B switch: one tile per workgroup
+  if constexpr (sizeof(TI) == 2) {
+    if (mf16 && !nopersist) return launch_gemm256_pp<TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
+    if (mf16) return launch_gemm256_p16<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
+  }
   return launch_gemm256_p<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
 }
 

@@ -276,12 +276,15 @@ def test_eval_script_synthetic_end_to_end(gpu_device, tmp_path, monkeypatch):
     import sys
     from pathlib import Path
     script = Path(__file__).resolve().parents[1] / "scripts" / "eval.py"
-    for pooler in ("final", "latent"):
+    for pooler, extra in (("final", []), ("latent", []), ("final", ["--host-metrics"])):
         monkeypatch.setattr(sys, "argv", ["eval.py", "--synthetic", "--num-impressions", "300", "--pooler", pooler,
-                                          "--log-dir", str(tmp_path), "--ckpt", str(tmp_path / "none.pt")])
+                                          "--log-dir", str(tmp_path), "--ckpt", str(tmp_path / "none.pt")] + extra)
         runpy.run_path(str(script), run_name="__main__")
     lines = (tmp_path / "final_scores.jsonl").read_text().splitlines()
-    assert len(lines) == 2
+    assert len(lines) == 3
+    dev, host = json.loads(lines[0]), json.loads(lines[2])  # same data and pooler: device == host metrics
+    for k in ("auc", "mrr", "ndcg5", "ndcg10"):
+        assert abs(dev["val_scores"][k] - host["val_scores"][k]) < 1e-12
     for ln in lines:
         rec = json.loads(ln)
         for k in ("train_scores", "val_scores"):
@@ -338,3 +341,29 @@ def test_layernorm_shapes(gpu_device, dim, dti, dto):
     ref = torch.nn.functional.layer_norm(x.double(), (dim,), gm.double(), bt.double(), 1e-5)
     tol = 1e-5 if dto == torch.float32 else 8e-3 * float(ref.abs().max())  # bf16 output rounding
     assert float((out.double() - ref).abs().max()) < tol
+
+
+def test_train_v3_and_save_emb_scripts_synthetic(gpu_device, tmp_path, monkeypatch):
+    """scripts/train_v3.py (config 5) and scripts/save_emb.py run end to end on
+    synthetic data: checkpoints + loss log written, embeddings saved/reloaded."""
+    import json
+    import runpy
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1] / "scripts"
+    monkeypatch.setattr(sys, "argv", ["train_v3.py", "--synthetic", "--num-impressions", "200", "--epochs", "2",
+                                      "--batch-size", "64", "--db-name", str(tmp_path / "tok.db"),
+                                      "--log-dir", str(tmp_path / "logs"), "--ckpt-dir", str(tmp_path / "models")])
+    runpy.run_path(str(root / "train_v3.py"), run_name="__main__")
+    recs = [json.loads(l) for l in (tmp_path / "logs" / "train_final_history_score.jsonl").read_text().splitlines()]
+    assert [r["epoch"] for r in recs] == [1, 2] and all(0.0 < r["loss"] < 4.0 for r in recs)
+    sd = torch.load(tmp_path / "models" / "final_attn" / "Epoch_2.pt", weights_only=True)
+    assert sd["linear1.weight"].shape == (4096, 1024)
+    assert (tmp_path / "models" / "token_attn" / "Epoch_2.pt").is_file()
+    monkeypatch.setattr(sys, "argv", ["save_emb.py", "--synthetic", "--layers", "2", "--vocab", "1000",
+                                      "--num-impressions", "200", "--save-dir", str(tmp_path / "emb")])
+    runpy.run_path(str(root / "save_emb.py"), run_name="__main__")
+    t = torch.load(tmp_path / "emb" / "MINDsmall_dev.pt", weights_only=True)
+    q = torch.load(tmp_path / "emb" / "query_MINDsmall_dev.pt", weights_only=True)
+    assert t.shape == q.shape and t.shape[1] == 1024
+    assert torch.allclose(t.norm(dim=1), torch.ones(t.shape[0]), atol=1e-4)
