@@ -740,7 +740,7 @@ __global__ __launch_bounds__(512, 2) void gemm256p_kernel(int64_t M, int64_t N, 
 template <int EPI, typename TO>
 __device__ __forceinline__ void epi16_store(const f32x4 (&acc)[8][4], float* slab, int lane, int wm, int wn,
                                             int64_t m0, int64_t n0, int64_t M, int64_t N,
-                                            const float* __restrict__ bias, const TO* R, int64_t ldr, TO* C,
+                                            const float (&b16)[4], const TO* R, int64_t ldr, TO* C,
                                             int64_t ldc, const EpiArgs& ea) {
   constexpr int COLS = (EPI == NR_EPI_GEGLU) ? 32 : 64;
   constexpr int VEC = 16 / (int)sizeof(TO);
@@ -750,11 +750,6 @@ __device__ __forceinline__ void epi16_store(const f32x4 (&acc)[8][4], float* sla
   const int64_t wcol = n0 + wn * 64;
   const int64_t ocol0 = (EPI == NR_EPI_GEGLU) ? wcol / 2 : wcol;
   const int c16 = lane & 15, r16 = 4 * (lane >> 4);
-  float b16[4] = {0.f, 0.f, 0.f, 0.f};
-  if (bias) {
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) b16[ni] = bias[wcol + 16 * ni + c16];
-  }
   // slab [16][COLS] f32; column bit 4 flipped on rows 4-7 / 12-15 so the two
   // 16-lane halves of a 32-lane store group hit different banks
   auto sidx = [](int row, int col) { return row * COLS + (col ^ ((row & 4) << 2)); };
@@ -955,11 +950,23 @@ __global__ __launch_bounds__(512, 2) void gemm256pp_kernel(int64_t M, int64_t N,
   __builtin_amdgcn_s_setprio(0);                       \
   __builtin_amdgcn_s_barrier();
 
+  // The epilogue of a full tile issues exactly EPI_STORES 16-byte stores per
+  // wave AFTER the next tile's prologue DMAs; vmcnt retires loads, stores and
+  // LDS-DMA in issue order (MI355X_MICROARCH: one counter, issue order), so
+  // vmcnt(EPI_STORES) means "the prologue has landed" while the previous
+  // tile's stores drain under this tile's MFMAs.  After a ragged (M-tail)
+  // tile fewer stores were issued: drain everything.
+  constexpr int EPI_COLS = (EPI == NR_EPI_GEGLU) ? 32 : 64;
+  constexpr int EPI_STORES = 8 * (16 / (64 / (EPI_COLS / (16 / (int)sizeof(TO)))));
+  static_assert(EPI_STORES == 8 || EPI_STORES == 16 || EPI_STORES == 32, "epilogue store count");
   setup(t);
   prologue();
+  bool drain_all = true;
   while (true) {
-    // this tile's prologue DMAs (and the previous tile's epilogue stores) landed
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (drain_all) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (EPI_STORES == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (EPI_STORES == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (wmu == 1) __builtin_amdgcn_s_barrier();  // stagger the wave groups
 #pragma unroll
@@ -994,12 +1001,21 @@ __global__ __launch_bounds__(512, 2) void gemm256pp_kernel(int64_t M, int64_t N,
     const int64_t n0 = tn0, m0 = tm0;
     const int tn = t + t_step;
     const bool more = tn < t_end;
+    // everything the epilogue reads from memory is loaded BEFORE the next
+    // tile's DMAs: a later load's wait would also wait for the (older) DMAs
+    float b16[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bias) {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) b16[ni] = bias[n0 + wn * 64 + 16 * ni + (lane & 15)];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (more) {  // next tile's operands fly while this tile's epilogue runs
       setup(tn);
       prologue();
     }
-    epi16_store<EPI, TO>(acc, slab, lane, wm, wn, m0, n0, M, N, bias, R, ldr, C, ldc, ea);
+    epi16_store<EPI, TO>(acc, slab, lane, wm, wn, m0, n0, M, N, b16, R, ldr, C, ldc, ea);
     if (!more) break;
+    drain_all = m0 + G2BM > M;  // ragged tile: some stores were skipped
     t = tn;
   }
 #undef NR_PHASE_SYNC_MMA
@@ -1132,9 +1148,11 @@ static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* 
   // profiles/round1/s2/gemm_mf16_vs_mf32.txt); NR_GEMM_MF32=1 selects the 32x32x16 tiles
   static const bool mf16 = getenv("NR_GEMM_MF32") == nullptr;
   if (v1) return launch_gemm256_v1<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
-  static const bool nopersist = getenv("NR_GEMM_NOPERSIST") != nullptr;  // A/B switch: one tile per workgroup
+  // persistent variant: opt-in (NR_GEMM_PERSIST=1) until its register pressure is fixed: its
+  // spill reloads in the epilogue wait on the next tile's DMAs
+  static const bool persist = getenv("NR_GEMM_PERSIST") != nullptr;
   if constexpr (sizeof(TI) == 2) {
-    if (mf16 && !nopersist) return launch_gemm256_pp<TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
+    if (mf16 && persist) return launch_gemm256_pp<TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
     if (mf16) return launch_gemm256_p16<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
   }
   return launch_gemm256_p<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
