@@ -1,6 +1,10 @@
+# Round check on the GPU box: gpu tests, smoke, bench, encoder bench, rocprof trace of the bench.
+# Usage: bash tools/gpu_round_check.sh OUTDIR
 set -o pipefail
-mkdir -p gpurun_out/r1s2
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/r1s2/pytest_gpu.log 2>&1 && \
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" > gpurun_out/r1s2/smoke.log 2>&1 && \
-timeout -k 10 600 python bench.py > gpurun_out/r1s2/bench.json 2> gpurun_out/r1s2/bench.err && \
-timeout -k 10 300 python tools/encoder_bench.py > gpurun_out/r1s2/encoder_bench.log 2>&1
+OUT=${1:-gpurun_out/round}
+mkdir -p "$OUT"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 && \
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" > "$OUT/smoke.log" 2>&1 && \
+timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" && \
+timeout -k 10 300 python tools/encoder_bench.py > "$OUT/encoder_bench.log" 2>&1 && \
+bash tools/prof_trace.sh "$OUT/prof"
