@@ -111,6 +111,20 @@ int nr_gemm_drelu(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K, 
                   void* stream);
 
 /*
+ * n independent C_i[M_i, N_i] = A_i · W_iᵀ (no bias, no epilogue) in ONE launch
+ * over the union of the problems' 256x256 tiles (bf16 or exact-f32 in, f32 or bf16 out).
+ * For problems too small to fill the 256 CUs alone: the config-5 weight-grad
+ * GEMMs dW = dOutᵀ · X of FinalAttention's five linears (trainer.py:1044-1069
+ * backward; four of them are 64 tiles each).  Arrays have n entries,
+ * 1 <= n <= NR_GEMM_MAX_GROUP; each problem needs N % 256 == 0, K % 64 (bf16) / 32 (f32) == 0,
+ * 16-B aligned operands and rows (as nr_gemm's 256x256 path).
+ */
+#define NR_GEMM_MAX_GROUP 8
+int nr_gemm_grouped(int dtype_in, int dtype_out, int n, const int64_t* M, const int64_t* N, const int64_t* K,
+                    const void* const* A, const int64_t* lda, const void* const* W, const int64_t* ldw,
+                    void* const* C, const int64_t* ldc, void* stream);
+
+/*
  * y = LayerNorm(x) * gamma + beta over rows of `dim` (biased variance).
  * Replaces nn.LayerNorm in PreNorm latent_attention.py:10-12,16-19 and
  * MyLayer attention.py:165-166,193.  dim % 256 == 0, dim <= 2048.

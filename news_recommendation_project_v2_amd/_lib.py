@@ -42,6 +42,7 @@ SIGNATURES = {
     "nr_gemm": (_i, [_i, _i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p]),
     "nr_gemm_relu_dropout": (_i, [_i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, ctypes.c_uint64, _f, _p]),
     "nr_gemm_drelu": (_i, [_i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _l, _p, _l, _f, _p]),
+    "nr_gemm_grouped": (_i, [_i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "nr_layernorm": (_i, [_i, _i, _l, _l, _p, _l, _p, _p, _f, _p, _l, _p]),
     "nr_gather_layernorm": (_i, [_i, _l, _l, _p, _l, _p, _i, _p, _p, _f, _p, _l, _p]),
     "nr_softmax64": (_i, [_l, _l, _p, _l, _i, _p, _l, _p]),

@@ -531,21 +531,21 @@ __global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, i
 // phase ends lgkmcnt(0) + barrier).  Block ids are remapped XCD-aware so the
 // N-tiles that share an A panel run on one XCD (its L2 holds the panel).
 // Same LDS images, swizzle and epilogue as gemm256_kernel.
-template <typename TI, int EPI, typename TO, bool MF16 = false>
-__global__ __launch_bounds__(512, 2) void gemm256p_kernel(int64_t M, int64_t N, int64_t K,
-                                                          const TI* __restrict__ A, int64_t lda,
-                                                          const TI* __restrict__ W, int64_t ldw,
-                                                          const float* __restrict__ bias, const TO* R,
-                                                          int64_t ldr, TO* C, int64_t ldc, EpiArgs ea) {
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE];
+// XCD-aware bijective remap of the launch order: dispatch slot `orig` runs on
+// XCD orig % 8; consecutive output tiles (the N tiles sharing an A panel) are
+// given to one XCD so its L2 holds the panel.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+  return (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+}
+
+template <typename TI, int EPI, typename TO, bool MF16>
+__device__ __forceinline__ void gemm256p_body(unsigned char* smem, int64_t m0, int64_t n0, int64_t M, int64_t N,
+                                              int64_t K, const TI* __restrict__ A, int64_t lda,
+                                              const TI* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
+                                              const TO* R, int64_t ldr, TO* C, int64_t ldc, const EpiArgs& ea) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
-  const int nx = (int)gridDim.x, nwg = nx * (int)gridDim.y;
-  const int orig = (int)blockIdx.y * nx + (int)blockIdx.x;
-  const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
-  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
-  const int64_t n0 = (int64_t)(wg % nx) * G2BN;
-  const int64_t m0 = (int64_t)(wg / nx) * G2BM;
 
   constexpr int BK = 128 / (int)sizeof(TI), CE = 16 / (int)sizeof(TI);
   // half-tile DMA sources: wave covers rows 128h + 16 wave + 8 j + lane / 8
@@ -723,6 +723,49 @@ __global__ __launch_bounds__(512, 2) void gemm256p_kernel(int64_t M, int64_t N, 
   if (wmu == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
 #undef NR_PHASE_SYNC_MMA
   gemm256_store<EPI, TO, MF16>(acc, smem, wave, lane, wm, wn, m0, n0, M, N, bias, R, ldr, C, ldc, ea);
+}
+
+template <typename TI, int EPI, typename TO, bool MF16 = false>
+__global__ __launch_bounds__(512, 2) void gemm256p_kernel(int64_t M, int64_t N, int64_t K,
+                                                          const TI* __restrict__ A, int64_t lda,
+                                                          const TI* __restrict__ W, int64_t ldw,
+                                                          const float* __restrict__ bias, const TO* R,
+                                                          int64_t ldr, TO* C, int64_t ldc, EpiArgs ea) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE];
+  const int nx = (int)gridDim.x;
+  const int wg = xcd_remap((int)blockIdx.y * nx + (int)blockIdx.x, nx * (int)gridDim.y);
+  gemm256p_body<TI, EPI, TO, MF16>(smem, (int64_t)(wg / nx) * G2BM, (int64_t)(wg % nx) * G2BN, M, N, K, A, lda, W,
+                                   ldw, bias, R, ldr, C, ldc, ea);
+}
+
+// Grouped launch of up to NR_GEMM_MAX_GROUP independent problems with one
+// dtype / epilogue (no bias, no residual): one grid over all problems' tiles,
+// so small problems (the config-5 weight-grad GEMMs, 64 tiles each) fill the
+// 256 CUs together instead of one after another.  tile_end[p] = prefix sum of
+// the problems' tile counts; tiles are remapped XCD-aware over the whole grid,
+// so one problem's N tiles of an A panel stay on one XCD.
+struct GemmGroup {
+  int n;
+  int tile_end[NR_GEMM_MAX_GROUP];
+  int ntn[NR_GEMM_MAX_GROUP];
+  int64_t M[NR_GEMM_MAX_GROUP], N[NR_GEMM_MAX_GROUP], K[NR_GEMM_MAX_GROUP];
+  const void* A[NR_GEMM_MAX_GROUP];
+  const void* W[NR_GEMM_MAX_GROUP];
+  void* C[NR_GEMM_MAX_GROUP];
+  int64_t lda[NR_GEMM_MAX_GROUP], ldw[NR_GEMM_MAX_GROUP], ldc[NR_GEMM_MAX_GROUP];
+};
+
+template <typename TI, typename TO, bool MF16>
+__global__ __launch_bounds__(512, 2) void gemm256p_group_kernel(GemmGroup g) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE];
+  const int t = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  int p = 0;
+  while (p + 1 < g.n && t >= g.tile_end[p]) ++p;
+  const int local = t - (p ? g.tile_end[p - 1] : 0);
+  const int nx = g.ntn[p];
+  gemm256p_body<TI, NR_EPI_NONE, TO, MF16>(smem, (int64_t)(local / nx) * G2BM, (int64_t)(local % nx) * G2BN, g.M[p],
+                                           g.N[p], g.K[p], (const TI*)g.A[p], g.lda[p], (const TI*)g.W[p], g.ldw[p],
+                                           nullptr, nullptr, 0, (TO*)g.C[p], g.ldc[p], EpiArgs{0, 0, 1.f});
 }
 
 // ---------------------------------------------------------------------------
@@ -1265,4 +1308,50 @@ extern "C" int nr_gemm(int dtype_in, int dtype_out, int epilogue, int64_t M, int
   nr::clear_error();
   return nr::gemm_dispatch(dtype_in, dtype_out, epilogue, M, N, K, A, lda, W, ldw, bias, R, ldr, C,
                            ldc, (hipStream_t)stream);
+}
+
+extern "C" int nr_gemm_grouped(int dtype_in, int dtype_out, int n, const int64_t* M, const int64_t* N,
+                               const int64_t* K, const void* const* A, const int64_t* lda, const void* const* W,
+                               const int64_t* ldw, void* const* C, const int64_t* ldc, void* stream) {
+  nr::clear_error();
+  NR_CHECK_ARG(dtype_in == NR_BF16 || dtype_in == NR_F32, "nr_gemm_grouped: bad dtype_in %d", dtype_in);
+  NR_CHECK_ARG(dtype_out == NR_F32 || dtype_out == NR_BF16, "nr_gemm_grouped: bad dtype_out %d", dtype_out);
+  NR_CHECK_ARG(n >= 1 && n <= NR_GEMM_MAX_GROUP, "nr_gemm_grouped: n=%d outside [1, %d]", n, NR_GEMM_MAX_GROUP);
+  NR_CHECK_ARG(M && N && K && A && lda && W && ldw && C && ldc, "nr_gemm_grouped: null array");
+  nr::GemmGroup g{};
+  g.n = 0;
+  int64_t tiles = 0;
+  const int64_t vo = dtype_out == NR_F32 ? 4 : 8;
+  for (int i = 0; i < n; ++i) {
+    const int64_t bk = dtype_in == NR_F32 ? 32 : 64, e16 = dtype_in == NR_F32 ? 4 : 8;
+    NR_CHECK_ARG(M[i] >= 0 && N[i] > 0 && K[i] > 0 && N[i] % nr::G2BN == 0 && K[i] % bk == 0,
+                 "nr_gemm_grouped: problem %d bad shape M=%lld N=%lld K=%lld (need N %% 256, K %% 64 bf16 / 32 f32)", i,
+                 (long long)M[i], (long long)N[i], (long long)K[i]);
+    if (M[i] == 0) continue;  // empty problem: no operand is read (torch gives a null data pointer)
+    NR_CHECK_ARG(A[i] && W[i] && C[i], "nr_gemm_grouped: problem %d null operand", i);
+    NR_CHECK_ARG(lda[i] >= K[i] && ldw[i] >= K[i] && lda[i] % e16 == 0 && ldw[i] % e16 == 0 && ldc[i] >= N[i] &&
+                     ldc[i] % vo == 0 && ((uintptr_t)A[i] & 15) == 0 && ((uintptr_t)W[i] & 15) == 0 &&
+                     ((uintptr_t)C[i] & 15) == 0,
+                 "nr_gemm_grouped: problem %d operands must be 16-byte aligned with 16-byte row strides", i);
+    const int j = g.n++;
+    g.M[j] = M[i]; g.N[j] = N[i]; g.K[j] = K[i];
+    g.A[j] = A[i]; g.W[j] = W[i]; g.C[j] = C[i];
+    g.lda[j] = lda[i]; g.ldw[j] = ldw[i]; g.ldc[j] = ldc[i];
+    g.ntn[j] = (int)(N[i] / nr::G2BN);
+    tiles += ((M[i] + nr::G2BM - 1) / nr::G2BM) * g.ntn[j];
+    NR_CHECK_ARG(tiles <= 0x7fffffff, "nr_gemm_grouped: too many tiles");
+    g.tile_end[j] = (int)tiles;
+  }
+  if (g.n == 0) return NR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_in == NR_F32 && dtype_out == NR_F32)
+    hipLaunchKernelGGL((nr::gemm256p_group_kernel<float, float, false>), dim3((unsigned)tiles), dim3(512), 0, s, g);
+  else if (dtype_in == NR_F32)
+    hipLaunchKernelGGL((nr::gemm256p_group_kernel<float, __bf16, false>), dim3((unsigned)tiles), dim3(512), 0, s, g);
+  else if (dtype_out == NR_F32)
+    hipLaunchKernelGGL((nr::gemm256p_group_kernel<__bf16, float, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);
+  else
+    hipLaunchKernelGGL((nr::gemm256p_group_kernel<__bf16, __bf16, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);
+  NR_CHECK_LAUNCH("nr_gemm_grouped");
+  return NR_OK;
 }

@@ -56,6 +56,41 @@ __global__ __launch_bounds__(256) void transpose_kernel(int64_t rows, int64_t co
   }
 }
 
+// 16-bit -> 16-bit transpose of a 64x64 tile with 16-B global accesses: each
+// lane loads 8 consecutive columns of a row (2 per lane), the tile sits in LDS
+// as u16 rows of pitch 66 (odd dword pitch: the column reads below are at most
+// 2-way), and each lane writes 8 consecutive source rows of one column as one
+// 16-B store (8 lanes = one 128-B output row segment).  Needs rows, cols,
+// strides multiple of 8 and 16-B aligned bases (checked by the caller).
+__global__ __launch_bounds__(256) void transpose16_kernel(int64_t rows, int64_t cols,
+                                                          const uint16_t* __restrict__ src, int64_t lds,
+                                                          uint16_t* __restrict__ dst, int64_t ldd) {
+  constexpr int P = 66;
+  __shared__ uint16_t tile[64 * P];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int rr = (t >> 3) + 32 * k, ch = t & 7;
+    const int64_t r = r0 + rr, c = c0 + 8 * ch;
+    uint4 u = make_uint4(0, 0, 0, 0);
+    if (r < rows && c < cols) u = *reinterpret_cast<const uint4*>(src + r * lds + c);
+    uint32_t* d = reinterpret_cast<uint32_t*>(tile + rr * P + 8 * ch);  // 4-B aligned (P even)
+    d[0] = u.x; d[1] = u.y; d[2] = u.z; d[3] = u.w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int oc = (t >> 3) + 32 * k, rc = t & 7;
+    const int64_t c = c0 + oc, r = r0 + 8 * rc;
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = (uint32_t)tile[(8 * rc + 2 * j) * P + oc] | ((uint32_t)tile[(8 * rc + 2 * j + 1) * P + oc] << 16);
+    if (c < cols && r < rows) *reinterpret_cast<uint4*>(dst + c * ldd + r) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 // ----------------------------------------------------------------- pooling fwd
 // FinalAttention pooling (modeling_utils.py:224-228) over consecutive slot rows:
 // xp row = [x | p] (p = exp(w)); u_d = sum x p / (sum p + 1e-10), z_d = sum p + 1e-10.
@@ -209,14 +244,46 @@ __global__ __launch_bounds__(256) void scatter_add_rows_kernel(int64_t n, int64_
 // out[c] += sum_r src[r][c]; 64 rows x 256 columns per workgroup, atomics per column.
 template <typename T>
 __global__ __launch_bounds__(256) void col_sum_kernel(int64_t rows, int64_t cols, const T* __restrict__ src,
-                                                      int64_t lds, float* __restrict__ out) {
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  const int64_t r0 = (int64_t)blockIdx.y * 256;
-  const int64_t r1 = min(rows, r0 + 256);
-  float s = 0.f;
-  for (int64_t r = r0; r < r1; ++r) s += ldf<T>(src + r * lds + c);
-  atomicAdd(out + c, s);
+                                                      int64_t lds, int rows_per_block, float* __restrict__ out) {
+  // block = 512 columns (8 per lane, one 16-B (bf16) / 2x16-B (f32) load per
+  // row) x rows_per_block rows, the 4 waves striding the rows; partials
+  // folded in LDS, then one atomic per column per block.
+  __shared__ float part[4][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 512 + lane * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  float s[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = 0.f;
+  const bool vec = c + 8 <= cols && (lds % 8) == 0 && ((uintptr_t)src & 15) == 0;
+  if (vec) {
+    for (int64_t r = r0 + wave; r < r1; r += 4) {
+      const T* p = src + r * lds + c;
+      if constexpr (sizeof(T) == 2) {
+        const uint4 u = *reinterpret_cast<const uint4*>(p);
+        const T* h = reinterpret_cast<const T*>(&u);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += (float)h[e];
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+        s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
+        s[4] += b.x; s[5] += b.y; s[6] += b.z; s[7] += b.w;
+      }
+    }
+  } else if (c < cols) {
+    for (int64_t r = r0 + wave; r < r1; r += 4)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c + e < cols) s[e] += ldf<T>(src + r * lds + c + e);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[wave][lane * 8 + e] = s[e];
+  __syncthreads();
+  for (int j = threadIdx.x; j < 512; j += 256) {
+    const int64_t cc = (int64_t)blockIdx.x * 512 + j;
+    if (cc < cols) atomicAdd(out + cc, (part[0][j] + part[1][j]) + (part[2][j] + part[3][j]));
+  }
 }
 
 // ----------------------------------------------------------------- LN param grads
@@ -268,17 +335,43 @@ __global__ __launch_bounds__(256) void ln_param_grad_kernel(int64_t n, const TI*
 }
 
 // ----------------------------------------------------------------- grad norm + AdamW
+// Sum of squares: 16-B lane loads, grid-stride over <= 1024 blocks, block
+// reduction in LDS, ONE atomic per block (per-wave atomics on a single address
+// serialise at the memory side: MI355X_MICROARCH.md "Global float atomics").
 __global__ __launch_bounds__(256) void sumsq_kernel(int64_t n, const float* __restrict__ x, float* __restrict__ out) {
+  __shared__ float part[4];
   float s = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) s = fmaf(x[i], x[i], s);
+  const int64_t n4 = ((uintptr_t)x & 15) == 0 ? n / 4 : 0;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = x4[i];
+    s = fmaf(v.x, v.x, s);
+    s = fmaf(v.y, v.y, s);
+    s = fmaf(v.z, v.z, s);
+    s = fmaf(v.w, v.w, s);
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    s = fmaf(x[i], x[i], s);
   s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) atomicAdd(out, s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, (part[0] + part[1]) + (part[2] + part[3]));
 }
 
 // torch.nn.utils.clip_grad_norm_(max_norm): coef = min(max_norm / (norm + 1e-6), 1)
 // torch.optim.AdamW (weight decay decoupled, bias-corrected):
 //   p *= 1 - lr wd;  m = b1 m + (1 - b1) g;  v = b2 v + (1 - b2) g^2
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+__device__ __forceinline__ void adamw_one(float& p, float g, float& m, float& v, float lr, float b1, float b2,
+                                          float eps, float wd, float bc1, float bc2s) {
+  p *= 1.f - lr * wd;
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  p -= (lr / bc1) * m / (sqrtf(v) / bc2s + eps);
+}
+
+// 4 parameters per lane (16-B loads / stores of p, g, m, v; 8-B bf16 mirror
+// store) when every array is aligned for it, scalar tail / fallback otherwise.
 __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     __bf16* __restrict__ p16, float lr, float b1, float b2,
@@ -286,12 +379,30 @@ __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* __restrict
                                                     const float* __restrict__ sumsq) {
   float coef = 1.f;
   if (sumsq) coef = fminf(max_norm / (sqrtf(*sumsq) + 1e-6f), 1.f);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float gi = g[i] * coef;
-    float pi = p[i] * (1.f - lr * wd);
-    const float mi = b1 * m[i] + (1.f - b1) * gi;
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
-    pi -= (lr / bc1) * mi / (sqrtf(vi) / bc2s + eps);
+  const bool vec = ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0) &&
+                   (((uintptr_t)p16 & 7) == 0);
+  const int64_t n4 = vec ? n / 4 : 0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adamw_one(pp.x, gg.x * coef, mm.x, vv.x, lr, b1, b2, eps, wd, bc1, bc2s);
+    adamw_one(pp.y, gg.y * coef, mm.y, vv.y, lr, b1, b2, eps, wd, bc1, bc2s);
+    adamw_one(pp.z, gg.z * coef, mm.z, vv.z, lr, b1, b2, eps, wd, bc1, bc2s);
+    adamw_one(pp.w, gg.w * coef, mm.w, vv.w, lr, b1, b2, eps, wd, bc1, bc2s);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (p16) {
+      __bf16 h[4] = {(__bf16)pp.x, (__bf16)pp.y, (__bf16)pp.z, (__bf16)pp.w};
+      *reinterpret_cast<uint2*>(p16 + 4 * i) = *reinterpret_cast<const uint2*>(h);
+    }
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    adamw_one(pi, g[i] * coef, mi, vi, lr, b1, b2, eps, wd, bc1, bc2s);
     m[i] = mi;
     v[i] = vi;
     p[i] = pi;
@@ -342,6 +453,14 @@ extern "C" int nr_transpose(int dtype_in, int dtype_out, int64_t rows, int64_t c
   NR_CHECK_ARG(src && dst, "nr_transpose: null pointer");
   NR_CHECK_ARG((rows + 63) / 64 <= 65535, "nr_transpose: too many rows");
   const dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
+  const bool b16 = dtype_in == dtype_out && dtype_in != NR_F32;
+  if (b16 && rows % 8 == 0 && cols % 8 == 0 && lds % 8 == 0 && ldd % 8 == 0 && ((uintptr_t)src & 15) == 0 &&
+      ((uintptr_t)dst & 15) == 0) {
+    hipLaunchKernelGGL(transpose16_kernel, grid, dim3(256), 0, (hipStream_t)stream, rows, cols,
+                       (const uint16_t*)src, lds, (uint16_t*)dst, ldd);
+    NR_CHECK_LAUNCH("nr_transpose");
+    return NR_OK;
+  }
   NR_DT2(dtype_in, dtype_out,
          hipLaunchKernelGGL((transpose_kernel<TI, TO>), grid, dim3(256), 0, (hipStream_t)stream, rows, cols,
                             (const TI*)src, lds, (TO*)dst, ldd));
@@ -407,10 +526,14 @@ extern "C" int nr_col_sum(int dtype, int64_t rows, int64_t cols, const void* src
   NR_CHECK_ARG(NR_OKDT(dtype) && rows >= 0 && cols > 0 && lds >= cols, "nr_col_sum: bad args");
   if (rows == 0) return NR_OK;
   NR_CHECK_ARG(src && out, "nr_col_sum: null pointer");
-  NR_CHECK_ARG((rows + 255) / 256 <= 65535, "nr_col_sum: too many rows");
-  const dim3 grid((unsigned)((cols + 255) / 256), (unsigned)((rows + 255) / 256));
+  // ~1024 blocks: column groups of 512 x row ranges (multiple of 4 rows, >= 32)
+  const int64_t cgroups = (cols + 511) / 512;
+  int64_t rpb = (rows * cgroups + 1023) / 1024;
+  rpb = rpb < 32 ? 32 : (rpb + 3) / 4 * 4;
+  NR_CHECK_ARG((rows + rpb - 1) / rpb <= 65535 && rpb <= 0x7fffffff, "nr_col_sum: too many rows");
+  const dim3 grid((unsigned)cgroups, (unsigned)((rows + rpb - 1) / rpb));
   NR_DT1(dtype, hipLaunchKernelGGL((col_sum_kernel<T>), grid, dim3(256), 0, (hipStream_t)stream, rows, cols,
-                                   (const T*)src, lds, out));
+                                   (const T*)src, lds, (int)rpb, out));
   NR_CHECK_LAUNCH("nr_col_sum");
   return NR_OK;
 }
@@ -444,7 +567,9 @@ extern "C" int nr_sumsq(int64_t n, const float* x, float* out, void* stream) {
   NR_CHECK_ARG(n >= 0, "nr_sumsq: bad n");
   if (n == 0) return NR_OK;
   NR_CHECK_ARG(x && out, "nr_sumsq: null pointer");
-  hipLaunchKernelGGL(sumsq_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, x, out);
+  const int64_t g = (n / 4 + 255) / 256;
+  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)(g < 1 ? 1 : g < 1024 ? g : 1024)), dim3(256), 0,
+                     (hipStream_t)stream, n, x, out);
   NR_CHECK_LAUNCH("nr_sumsq");
   return NR_OK;
 }
@@ -458,7 +583,7 @@ extern "C" int nr_adamw(int64_t n, float* p, const float* g, float* m, float* v,
   NR_CHECK_ARG(p && g && m && v, "nr_adamw: null pointer");
   const float bc1 = (float)(1.0 - pow((double)beta1, (double)step));
   const float bc2s = (float)sqrt(1.0 - pow((double)beta2, (double)step));
-  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v,
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v,
                      (__bf16*)p_bf16, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, max_norm, sumsq);
   NR_CHECK_LAUNCH("nr_adamw");
   return NR_OK;

@@ -325,6 +325,31 @@ def _dt(t: torch.Tensor, name: str) -> int:
     return _dtype(t, name)
 
 
+def gemm_grouped(problems) -> None:
+    """out_i = a_i @ w_i.T for up to 8 (a, w, out) triples in ONE launch over all
+    their 256x256 tiles (nr_gemm_grouped): small GEMMs that cannot fill the
+    chip alone run side by side.  bf16 or f32 a/w, f32 or bf16 out (one out dtype)."""
+    problems = list(problems)
+    if not 1 <= len(problems) <= 8:
+        raise _lib.NewsRecHIPError("gemm_grouped: 1..8 problems")
+    dev = _dev(*[t for pr in problems for t in pr])
+    n = len(problems)
+    L = ctypes.c_int64 * n
+    P = ctypes.c_void_p * n
+    M, N, K, lda, ldw, ldc = L(), L(), L(), L(), L(), L()
+    A, W, C = P(), P(), P()
+    for i, (a, w, out) in enumerate(problems):
+        if a.dtype != w.dtype or a.shape[1] != w.shape[1] or tuple(out.shape) != (a.shape[0], w.shape[0]):
+            raise _lib.NewsRecHIPError(f"gemm_grouped: problem {i} shape/dtype mismatch")
+        if out.dtype != problems[0][2].dtype:
+            raise _lib.NewsRecHIPError("gemm_grouped: all outputs must share a dtype")
+        M[i], K[i], N[i] = a.shape[0], a.shape[1], w.shape[0]
+        lda[i], ldw[i], ldc[i] = _rowmajor(a, "a"), _rowmajor(w, "w"), _rowmajor(out, "out")
+        A[i], W[i], C[i] = a.data_ptr(), w.data_ptr(), out.data_ptr()
+    _lib.call("nr_gemm_grouped", _dtype(problems[0][0], "a"), _dtype(problems[0][2], "out"), n, M, N, K, A, lda, W,
+              ldw, C, ldc, _stream(dev))
+
+
 def gemm_relu_dropout(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], seed: int, p: float,
                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = relu(a @ w.T + bias) * keep / (1 - p), keep from the (seed, row, col) hash stream."""

@@ -129,6 +129,7 @@ class FinalAttentionTrainStep:
         self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self._ws = {}
+        self._pending = []
 
     # ------------------------------------------------------------------ helpers
     def _buf(self, name: str, shape, dtype) -> torch.Tensor:
@@ -212,16 +213,25 @@ class FinalAttentionTrainStep:
         self._wgrad(dZ1, S, "linear1.weight")
         ops.col_sum(dZ1, self.gviews["linear1.bias"])
         # history gather -> unique news rows -> token LayerNorm params
+        self._flush_wgrads()
         ops.scatter_add_rows(dS[:Hs], batch.hist_idx, dE)
         ops.ln_param_grad(batch.tok_last, None, self.ln_eps, dE, self.gviews["ln.weight"], self.gviews["ln.bias"])
         return self.loss, users, E
 
     def _wgrad(self, dOut: torch.Tensor, Xin: torch.Tensor, name: str) -> None:
-        """grad[name] = dOutᵀ · Xin  ([N_out, Hp] x [Hp, K_in])."""
+        """grad[name] = dOutᵀ · Xin  ([N_out, Hp] x [Hp, K_in]).  bf16: the
+        transposed operands are kept per layer and the five GEMMs run as ONE
+        grouped launch in ``_flush_wgrads`` (four of them are 64 tiles each,
+        a quarter of the chip alone)."""
         dt = self.dtype
-        dOt = ops.transpose(dOut, out=self._buf("wg_a", (dOut.shape[1], dOut.shape[0]), dt))
-        Xt = ops.transpose(Xin, out=self._buf("wg_b", (Xin.shape[1], Xin.shape[0]), dt))
-        ops.gemm(dOt, Xt, None, out=self.gviews[name])
+        dOt = ops.transpose(dOut, out=self._buf("wg_a_" + name, (dOut.shape[1], dOut.shape[0]), dt))
+        Xt = ops.transpose(Xin, out=self._buf("wg_b_" + name, (Xin.shape[1], Xin.shape[0]), dt))
+        self._pending.append((dOt, Xt, self.gviews[name]))
+
+    def _flush_wgrads(self) -> None:
+        if self._pending:
+            ops.gemm_grouped(self._pending)
+            self._pending = []
 
     def optimizer_step(self) -> None:
         """clip_grad_norm_(max_norm) + AdamW, one launch each (trainer.py:1067-1069)."""

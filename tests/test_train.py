@@ -275,3 +275,81 @@ def test_gpu_train_kernels(gpu_device):
         ops.adamw(p, gg, m, v, step, 1e-3)
         opt.step()
     torch.testing.assert_close(p, ref.detach(), rtol=0, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_gpu_train_kernels_vector_paths(gpu_device):
+    """16-bit transpose fast path (rows/cols multiples of 8, strided views),
+    col_sum over several column groups / row blocks (bf16 and f32, ragged tail),
+    sumsq with an unaligned tail, and a weight-grad-shaped GEMM that the
+    dispatcher routes to the 128x128 kernel (256x256 grid under 128 tiles)."""
+    from news_recommendation_project_v2_amd import ops
+    g = torch.Generator(device=gpu_device).manual_seed(3)
+    for dt in (torch.bfloat16,):
+        for rows, cols in ((8320, 4096), (64, 8), (136, 1032), (8, 520)):
+            x = torch.randn(rows, cols, generator=g, device=gpu_device).to(dt)
+            assert torch.equal(ops.transpose(x), x.T.contiguous()), (dt, rows, cols)
+        big = torch.randn(200, 1040, generator=g, device=gpu_device).to(dt)
+        view = big[:, 8:1032]  # 16-B aligned, stride 1040
+        assert torch.equal(ops.transpose(view), view.T.contiguous())
+    for dt in (torch.bfloat16, torch.float32):
+        for rows, cols in ((8320, 4096), (3, 1024), (1000, 1030), (70000, 64)):
+            x = torch.randn(rows, cols, generator=g, device=gpu_device).to(dt)
+            cs = torch.zeros(cols, device=gpu_device)
+            ops.col_sum(x, cs)
+            torch.testing.assert_close(cs, x.float().sum(0), rtol=1e-4, atol=1e-3 * (rows ** 0.5))
+    for n in (1, 1000, 1 << 20, 47_000_003):
+        v = torch.randn(n, generator=g, device=gpu_device)
+        out = torch.zeros(1, device=gpu_device)
+        ops.sumsq(v, out)
+        torch.testing.assert_close(out[0].double(), (v.double() ** 2).sum(), rtol=1e-5, atol=0)
+        out2 = torch.zeros(1, device=gpu_device)
+        ops.sumsq(v[1:], out2)  # 4-B aligned base: scalar path
+        torch.testing.assert_close(out2[0].double(), (v[1:].double() ** 2).sum(), rtol=1e-5, atol=0)
+    a = torch.randn(4096, 2048, generator=g, device=gpu_device).to(torch.bfloat16)
+    w = torch.randn(1024, 2048, generator=g, device=gpu_device).to(torch.bfloat16)
+    c = ops.gemm(a, w, None, out_dtype=torch.float32)
+    torch.testing.assert_close(c, a.float() @ w.float().T, rtol=2e-3, atol=2e-2)
+
+
+@pytest.mark.gpu
+def test_gpu_gemm_grouped(gpu_device):
+    """nr_gemm_grouped: mixed shapes (64-tile and 256-tile problems, a ragged M,
+    an empty problem, a strided output view) in one launch == per-problem f32 matmul."""
+    from news_recommendation_project_v2_amd import ops
+    g = torch.Generator(device=gpu_device).manual_seed(5)
+    r = lambda *s: torch.randn(*s, generator=g, device=gpu_device).to(torch.bfloat16)
+    shapes = [(4096, 1024, 8320), (1024, 4096, 8320), (4096, 4096, 512), (300, 256, 64), (0, 512, 128)]
+    probs = []
+    for M, N, K in shapes:
+        probs.append((r(M, K), r(N, K), torch.full((M, N), float("nan"), device=gpu_device)))
+    wide = torch.full((1024, 1280), float("nan"), device=gpu_device)
+    probs.append((r(1024, 192), r(1024, 192), wide[:, 256:]))
+    ops.gemm_grouped(probs)
+    for a, w, out in probs:
+        if a.shape[0]:
+            ref = a.float() @ w.float().T
+            torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3 * a.shape[1] ** 0.5)
+    assert torch.isnan(wide[:, :256]).all()  # untouched columns of the strided output
+    with pytest.raises(Exception):
+        ops.gemm_grouped([(r(256, 64), r(128, 64), torch.empty(256, 128, device=gpu_device))])  # N % 256
+
+
+@pytest.mark.gpu
+def test_gpu_adamw_vector_and_tail(gpu_device):
+    """AdamW kernel: 4-wide path + scalar tail (n % 4 != 0) + unaligned fallback, vs torch.optim.AdamW."""
+    from news_recommendation_project_v2_amd import ops
+    for n, off in ((1001, 0), (4099, 1)):
+        base = torch.randn(n + off, device=gpu_device)
+        p = base[off:]
+        gg = torch.randn(n, device=gpu_device)
+        m, v = torch.zeros(n, device=gpu_device), torch.zeros(n, device=gpu_device)
+        p16 = torch.zeros(n, dtype=torch.bfloat16, device=gpu_device)
+        ref = p.clone().requires_grad_(True)
+        ref.grad = gg.clone()
+        opt = torch.optim.AdamW([ref], lr=1e-3, weight_decay=0.01)
+        for step in (1, 2, 3):
+            ops.adamw(p, gg, m, v, step, 1e-3, p_bf16=p16)
+            opt.step()
+        torch.testing.assert_close(p, ref.detach(), rtol=0, atol=1e-6)
+        assert torch.equal(p16, p.to(torch.bfloat16))
