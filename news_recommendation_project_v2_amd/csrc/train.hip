@@ -99,12 +99,16 @@ template <typename T>
 __global__ __launch_bounds__(256) void final_pool_fwd_kernel(int64_t n_seg, const int64_t* __restrict__ off,
                                                              const T* __restrict__ xp, int64_t ld,
                                                              float* __restrict__ users, float* __restrict__ z) {
+  // block = (segment, 256-dim quarter); the 4 waves stride the segment's rows,
+  // 4 dims per lane, partial sums folded through LDS (fixed order).
   constexpr int D = 1024;
+  __shared__ float sn[4][256], sd[4][256];
   const int64_t b = blockIdx.x;
   if (b >= n_seg) return;
-  const int d = threadIdx.x * 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int d = (int)blockIdx.y * 256 + lane * 4;
   float num[4] = {0.f, 0.f, 0.f, 0.f}, den[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t i = off[b]; i < off[b + 1]; ++i) {
+  for (int64_t i = off[b] + wave; i < off[b + 1]; i += 4) {
     const T* row = xp + i * ld;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -114,11 +118,12 @@ __global__ __launch_bounds__(256) void final_pool_fwd_kernel(int64_t n_seg, cons
     }
   }
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const float zz = den[t] + 1e-10f;
-    z[b * D + d + t] = zz;
-    users[b * D + d + t] = num[t] / zz;
-  }
+  for (int t = 0; t < 4; ++t) { sn[wave][lane * 4 + t] = num[t]; sd[wave][lane * 4 + t] = den[t]; }
+  __syncthreads();
+  const int c = threadIdx.x, dc = (int)blockIdx.y * 256 + c;
+  const float zz = ((sd[0][c] + sd[1][c]) + (sd[2][c] + sd[3][c])) + 1e-10f;
+  z[b * D + dc] = zz;
+  users[b * D + dc] = ((sn[0][c] + sn[1][c]) + (sn[2][c] + sn[3][c])) / zz;
 }
 
 // ----------------------------------------------------------------- pooling bwd
@@ -131,11 +136,13 @@ __global__ __launch_bounds__(256) void final_pool_bwd_kernel(int64_t n_seg, cons
                                                              const float* __restrict__ z,
                                                              const float* __restrict__ du, T* __restrict__ dx,
                                                              int64_t lddx, T* __restrict__ dl, int64_t lddl) {
+  // block = (segment, 256-dim quarter), waves stride the rows (as the forward)
   constexpr int D = 1024;
   const int64_t b = blockIdx.x;
-  const int d = threadIdx.x * 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int d = (int)blockIdx.y * 256 + lane * 4;
   if (b >= n_seg) {  // trailing blocks zero the padding rows
-    for (int64_t i = off[n_seg] + (b - n_seg); i < n_rows; i += gridDim.x - n_seg)
+    for (int64_t i = off[n_seg] + (b - n_seg) * 4 + wave; i < n_rows; i += (int64_t)(gridDim.x - n_seg) * 4)
 #pragma unroll
       for (int t = 0; t < 4; ++t) { stf<T>(dx + i * lddx + d + t, 0.f); stf<T>(dl + i * lddl + d + t, 0.f); }
     return;
@@ -147,7 +154,7 @@ __global__ __launch_bounds__(256) void final_pool_bwd_kernel(int64_t n_seg, cons
     u[t] = users[b * D + d + t];
     iz[t] = 1.0f / z[b * D + d + t];
   }
-  for (int64_t i = off[b]; i < off[b + 1]; ++i) {
+  for (int64_t i = off[b] + wave; i < off[b + 1]; i += 4) {
     const T* row = xp + i * ld;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -295,10 +302,14 @@ __global__ __launch_bounds__(256) void ln_param_grad_kernel(int64_t n, const TI*
                                                             const float* __restrict__ dy, int64_t lddy,
                                                             float* __restrict__ dg, float* __restrict__ db) {
   constexpr int D = 1024, NJ = D / 256;
-  __shared__ float sg[D], sb[D];
-  for (int c = threadIdx.x; c < D; c += 256) { sg[c] = 0.f; sb[c] = 0.f; }
-  __syncthreads();
+  // per-lane register accumulators for the lane's 16 columns (no LDS atomics)
+  __shared__ float sg[4][D], sb[4][D];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float ag[NJ][4], ab[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { ag[j][t] = 0.f; ab[j][t] = 0.f; }
   for (int64_t i = (int64_t)blockIdx.x * 4 + wave; i < n; i += (int64_t)gridDim.x * 4) {
     const int64_t row = row_idx ? row_idx[i] : i;
     float v[NJ][4];
@@ -318,19 +329,28 @@ __global__ __launch_bounds__(256) void ln_param_grad_kernel(int64_t n, const TI*
       for (int t = 0; t < 4; ++t) { const float dd = v[j][t] - mean; q = fmaf(dd, dd, q); }
     const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j) {
+      const float4 g = *reinterpret_cast<const float4*>(dy + i * lddy + j * 256 + lane * 4);
+      const float gg[4] = {g.x, g.y, g.z, g.w};
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const int e = j * 256 + lane * 4 + t;
-        const float g = dy[i * lddy + e];
-        atomicAdd(&sg[e], g * (v[j][t] - mean) * rstd);
-        atomicAdd(&sb[e], g);
+        ag[j][t] = fmaf(gg[t], (v[j][t] - mean) * rstd, ag[j][t]);
+        ab[j][t] += gg[t];
       }
+    }
   }
+  // fold the 4 waves' register partials in LDS (fixed order), one atomic per column per block
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sg[wave][j * 256 + lane * 4 + t] = ag[j][t];
+      sb[wave][j * 256 + lane * 4 + t] = ab[j][t];
+    }
   __syncthreads();
   for (int c = threadIdx.x; c < D; c += 256) {
-    atomicAdd(dg + c, sg[c]);
-    atomicAdd(db + c, sb[c]);
+    atomicAdd(dg + c, (sg[0][c] + sg[1][c]) + (sg[2][c] + sg[3][c]));
+    atomicAdd(db + c, (sb[0][c] + sb[1][c]) + (sb[2][c] + sb[3][c]));
   }
 }
 
@@ -474,7 +494,7 @@ extern "C" int nr_final_pool_fwd(int dtype, int64_t n_seg, const int64_t* off, c
   NR_CHECK_ARG(NR_OKDT(dtype) && n_seg >= 0 && ld >= 2048, "nr_final_pool_fwd: bad args");
   if (n_seg == 0) return NR_OK;
   NR_CHECK_ARG(off && xp && users && z, "nr_final_pool_fwd: null pointer");
-  NR_DT1(dtype, hipLaunchKernelGGL((final_pool_fwd_kernel<T>), dim3((unsigned)n_seg), dim3(256), 0,
+  NR_DT1(dtype, hipLaunchKernelGGL((final_pool_fwd_kernel<T>), dim3((unsigned)n_seg, 4), dim3(256), 0,
                                    (hipStream_t)stream, n_seg, off, (const T*)xp, ld, users, z));
   NR_CHECK_LAUNCH("nr_final_pool_fwd");
   return NR_OK;
@@ -489,7 +509,7 @@ extern "C" int nr_final_pool_bwd(int dtype, int64_t n_seg, const int64_t* off, i
   if (n_seg == 0 && n_rows == 0) return NR_OK;
   NR_CHECK_ARG(off && xp && users && z && du && dx && dl, "nr_final_pool_bwd: null pointer");
   const unsigned grid = (unsigned)(n_seg + 64);  // 64 trailing blocks zero the padding rows
-  NR_DT1(dtype, hipLaunchKernelGGL((final_pool_bwd_kernel<T>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
+  NR_DT1(dtype, hipLaunchKernelGGL((final_pool_bwd_kernel<T>), dim3(grid, 4), dim3(256), 0, (hipStream_t)stream,
                                    n_seg, off, n_rows, (const T*)xp, ld, users, z, du, (T*)dx, lddx, (T*)dl, lddl));
   NR_CHECK_LAUNCH("nr_final_pool_bwd");
   return NR_OK;
@@ -547,7 +567,9 @@ extern "C" int nr_ln_param_grad(int dtype_in, int64_t n, int64_t dim, const void
   NR_CHECK_ARG(dtype_in == NR_F32 || dtype_in == NR_BF16 || dtype_in == NR_F16, "nr_ln_param_grad: bad dtype");
   if (n == 0) return NR_OK;
   NR_CHECK_ARG(x && dy && dgamma && dbeta, "nr_ln_param_grad: null pointer");
-  const unsigned grid = (unsigned)((n + 3) / 4 < 1024 ? (n + 3) / 4 : 1024);
+  NR_CHECK_ARG(lddy % 4 == 0 && ((uintptr_t)dy & 15) == 0, "nr_ln_param_grad: dy rows must be 16-byte aligned");
+  const int64_t g16 = (n + 15) / 16;  // ~16 rows per block: few enough blocks that the final atomics stay cheap
+  const unsigned grid = (unsigned)(g16 < 256 ? g16 : 256);
   hipStream_t s = (hipStream_t)stream;
   if (dtype_in == NR_F32)
     hipLaunchKernelGGL((ln_param_grad_kernel<float>), dim3(grid), dim3(256), 0, s, n, (const float*)x, ldx, row_idx,
