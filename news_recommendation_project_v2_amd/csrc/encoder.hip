@@ -80,11 +80,18 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = blockIdx.y * 4 + wave;     // head
   const int qb_global = blockIdx.x;        // global query-block index
-  // binary search the sequence owning this query block (qoff: prefix of ceil(L/32))
-  int lo = 0, hi = n_seq;
+  // 64-ary search for the sequence owning this query block (qoff: prefix of
+  // ceil(L/32), qoff[n_seq] = total): each step probes 64 boundaries with one
+  // wave load + ballot, so 20k sequences take 3 dependent loads, not 15.
+  int lo = 0, hi = n_seq;  // invariant: qoff[lo] <= qb_global < qoff[hi]
   while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (qoff[mid] <= qb_global) lo = mid; else hi = mid;
+    const int step = (hi - lo + 63) >> 6;
+    const int idx = lo + lane * step;
+    const bool le = idx < hi && qoff[idx] <= qb_global;
+    const unsigned long long b = __ballot(le);
+    const int last = 63 - __builtin_clzll(b);  // lane 0 (idx = lo) is always set
+    lo = lo + last * step;
+    hi = min(hi, lo + step);
   }
   const int seq = lo;
   const int64_t s0 = cu[seq];
@@ -158,6 +165,11 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
       }
     }
   } else {
+    // Per-wave LDS: the 32-key V tile (rows of 192 B: conflict-free for the
+    // transposed reads below, MI355X guide T10 bank rule), reused for the O tile.
+    __shared__ __attribute__((aligned(16))) unsigned char lds_all[4][32 * 192];
+    unsigned char* lds = lds_all[wave];
+    typedef short s16x4 __attribute__((ext_vector_type(4)));
     bf16x8 qf[4];  // step s: d = 16s + 8lh + j
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -165,17 +177,28 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
 #pragma unroll
       for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)raw[j] * 0.125f);
     }
+    // transposed-read lane roles (T10): group g = lane >> 4 reads a 4-key x 16-d
+    // block; lane 4q + p of the group addresses key row q, d columns 4p..4p+3
+    const int tg = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+    const int tr_off = tq * 192 + 2 * (16 * (tg & 1) + 4 * tp);
     for (int kb = 0; kb < L; kb += 32) {
       const int krow = min(kb + li, L - 1);
       const T* kp = qkv + (s0 + krow) * LD + D + h * HD;
+      bf16x8 kf[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) kf[s] = *reinterpret_cast<const bf16x8*>(kp + 16 * s + 8 * lh);
+      // V tile rows kb + 8i + lane/8 (clamped: those keys get P = 0), 16-B chunk lane % 8
+      uint4 vt[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int vr = min(kb + 8 * i + (lane >> 3), L - 1);
+        vt[i] = *reinterpret_cast<const uint4*>(qkv + (s0 + vr) * LD + vcol + 8 * (lane & 7));
+      }
       f32x16 sacc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kp + 16 * s + 8 * lh);
-        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc, 0, 0, 0);
-      }
+      for (int s = 0; s < 4; ++s) sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s], qf[s], sacc, 0, 0, 0);
       float mx = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -191,14 +214,21 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
       ps += __shfl_xor(ps, 32, 64);
       l_run = l_run * alpha + ps;
       m_run = m_new;
+      if (kb > 0) {  // wave-uniform; O is still zero after the first key block
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float a = __shfl(alpha, acc_row(r, lh), 64);
-        o[0][r] *= a;
-        o[1][r] *= a;
+        for (int r = 0; r < 16; ++r) {
+          const float a = __shfl(alpha, acc_row(r, lh), 64);
+          o[0][r] *= a;
+          o[1][r] *= a;
+        }
       }
-      // A operand from the P accumulator (guide §3): k-step s (s = 0, 1) uses
-      // registers 8s..8s+7, element j <-> key 16s + 8(j>>2) + 4lh + (j&3).
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<uint4*>(lds + (8 * i + (lane >> 3)) * 192 + 16 * (lane & 7)) = vt[i];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's V tile is in LDS
+      // O += P V: A = P from the accumulator (k-step s: registers 8s..8s+7,
+      // element j <-> key 16s + 8(j>>2) + 4lh + (j&3)); B = V read transposed,
+      // two 4-key blocks per fragment (j = 0..3 and 4..7), lane column d = 32dt + li
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 pa;
@@ -206,16 +236,36 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
         for (int j = 0; j < 8; ++j) pa[j] = (__bf16)sacc[8 * s + j];
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
-          bf16x8 vb;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int kr = min(kb + 16 * s + 8 * (j >> 2) + 4 * lh + (j & 3), L - 1);
-            vb[j] = qkv[(s0 + kr) * LD + vcol + 32 * dt + li];
-          }
+          const unsigned char* b0 = lds + (16 * s + 4 * lh) * 192 + 64 * dt + tr_off;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(b0));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(b0 + 8 * 192));
+          // whole-vector bit cast (per-element bf16 inserts miscompile to a
+          // duplicated dword here: hipcc 7.2, seen in the ISA)
+          const bf16x8 vb = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
           o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, vb, o[dt], 0, 0, 0);
         }
       }
     }
+    // O tile -> LDS (rows q, 144-B pitch) -> 16-B row stores
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int q = acc_row(r, lh);
+      const float inv = 1.0f / __shfl(l_run, q, 64);
+      __bf16* orow = reinterpret_cast<__bf16*>(lds + q * 144);
+      orow[li] = (__bf16)(o[0][r] * inv);
+      orow[32 + li] = (__bf16)(o[1][r] * inv);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = 8 * i + (lane >> 3);
+      const uint4 v = *reinterpret_cast<const uint4*>(lds + q * 144 + 16 * (lane & 7));
+      if (q0 + q < L) *reinterpret_cast<uint4*>(ctx + (s0 + q0 + q) * D + h * HD + 8 * (lane & 7)) = v;
+    }
+    return;
   }
   // normalise by l[q] and store rows q0 + acc_row(r, lh), d = 32 dt + li
 #pragma unroll
