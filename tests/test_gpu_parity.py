@@ -88,6 +88,42 @@ def test_gemm_bf16(gpu_device, epi):
     np.testing.assert_allclose(out.cpu().double().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("epi", ["none", "relu", "exp", "gelu", "resadd", "geglu", "softmax64"])
+@pytest.mark.parametrize("out_dt", [torch.float32, torch.bfloat16])
+def test_gemm_bf16_256_epilogues(gpu_device, epi, out_dt):
+    """The 256x256 bf16 kernel's register epilogue (transposed accumulators) for
+    every epilogue and both output dtypes, ragged M, several N tiles, vs float64."""
+    g = torch.Generator().manual_seed(11)
+    M, N, K = 600, 512, 192
+    a = (torch.randn(M, K, generator=g) * 0.2).bfloat16()
+    w = (torch.randn(N, K, generator=g) * 0.1).bfloat16()
+    b = torch.randn(N, generator=g) * 0.1
+    ncols = N // 2 if epi == "geglu" else N
+    r = torch.randn(M, ncols, generator=g).to(out_dt)
+    acc = a.double() @ w.double().T + b.double()
+    wk, bk = w, b
+    if epi == "relu":
+        ref = acc.clamp_min(0)
+    elif epi == "exp":
+        ref = acc.exp()
+    elif epi == "gelu":
+        ref = torch.nn.functional.gelu(acc)
+    elif epi == "resadd":
+        ref = acc + r.double()
+    elif epi == "geglu":
+        ref = acc[:, :N // 2] * torch.nn.functional.gelu(acc[:, N // 2:])
+        wk, bk = interleave_geglu_rows(w), interleave_geglu_rows(b)
+    elif epi == "softmax64":
+        ref = torch.softmax(acc.reshape(M, N // 64, 64), -1).reshape(M, N)
+    else:
+        ref = acc
+    d = lambda t: t.contiguous().to(gpu_device)
+    out = ops.gemm(d(a), d(wk), d(bk), epilogue=epi, residual=d(r) if epi == "resadd" else None, out_dtype=out_dt)
+    torch.cuda.synchronize()
+    tol = 1e-4 if out_dt == torch.float32 else 1e-2
+    np.testing.assert_allclose(out.float().cpu().double().numpy(), ref.numpy(), rtol=tol, atol=tol)
+
+
 def test_gemm_identity_asymmetric(gpu_device):
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     for dt in (torch.float32, torch.bfloat16):
