@@ -22,6 +22,13 @@ import torch.distributed as dist
 from .engine import PoolScoreEngine
 
 
+def _host_staged(group=None) -> bool:
+    """True for gloo, which moves host buffers: device tensors are staged through
+    the host.  (RCCL needs one GPU per rank; the multi-rank GPU test runs gloo
+    ranks that share the box's one GPU.)"""
+    return dist.get_backend(group) == "gloo"
+
+
 def shard_rows(n: int, world: int) -> int:
     """Rows per rank for the news-table shard (ceil), so all shards are equal."""
     return (n + world - 1) // world
@@ -60,7 +67,14 @@ class ShardedTable:
         sl = slice(self.rank * self.rows, (self.rank + 1) * self.rows)
         self.eng.transform(rows=sl, out=self.local)
         if self.world > 1:
-            dist.all_gather_into_tensor(self.full, self.local, group=self.group)
+            if _host_staged(self.group) and self.local.is_cuda:
+                # gloo moves host memory: stage the slices through the host as raw bytes
+                host = torch.empty(self.full.shape, dtype=self.full.dtype)
+                dist.all_gather_into_tensor(host.view(torch.uint8), self.local.cpu().view(torch.uint8),
+                                            group=self.group)
+                self.full.copy_(host)
+            else:
+                dist.all_gather_into_tensor(self.full, self.local, group=self.group)
         self.eng.hist_table = self.full
         return self.full
 
@@ -76,6 +90,8 @@ def gather_scores(local_scores: torch.Tensor, world: int, group=None) -> Optiona
     """Concatenate per-rank score vectors (impression order) on every rank."""
     if world == 1:
         return local_scores
+    if _host_staged(group) and local_scores.is_cuda:
+        return gather_scores(local_scores.cpu(), world, group).to(local_scores.device)
     n = torch.tensor([local_scores.numel()], device=local_scores.device, dtype=torch.int64)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
@@ -85,3 +101,44 @@ def gather_scores(local_scores: torch.Tensor, world: int, group=None) -> Optiona
     outs = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(outs, buf, group=group)
     return torch.cat([o[:int(s)] for o, s in zip(outs, sizes)])
+
+
+def sharded_second_attention_score(history_rev_index, history_len_list, news_rev_index, impression_len_list,
+                                   news_embeddings: torch.Tensor, history_bool, attention_model: torch.nn.Module,
+                                   dtype: Optional[torch.dtype], rank: int, world: int, group=None) -> dict:
+    """``get_final_second_attention_score`` (data_model_helper.py:416-443) over
+    ``world`` ranks, one GPU each (BASELINE config 4): the impressions that have a
+    history are split into contiguous cost-balanced ranges (``partition_by_cost``),
+    every rank transforms 1/world of the news table and all-gathers it (RCCL),
+    pools + scores its own range, and the scores are gathered back in impression
+    order on every rank, where the dense ranks are taken exactly as on one GPU.
+    Same return value as the single-GPU function (bit-identical scores: every
+    row and impression is computed by the same kernels)."""
+    from . import ops
+    from .data_model_helper import COMPUTE_DTYPE
+    from .data_utils import group_items, lengths_to_offsets, rank_group_preds
+    dtype = dtype or COMPUTE_DTYPE
+    hb = np.asarray(history_bool, dtype=bool)
+    imp_len = np.asarray(impression_len_list)
+    sub_news = np.asarray(news_rev_index)[np.repeat(hb, imp_len)]
+    sub_len = imp_len[hb]
+    hist_idx = np.asarray(history_rev_index)
+    hist_len = np.asarray(history_len_list)
+    assert len(hist_len) == len(sub_len), "Number of rows should be consistent"
+    es = 2 if dtype == torch.bfloat16 else 4
+    k = 2 if attention_model.pooler_kind == "final" else 1
+    b = partition_by_cost(hist_len, sub_len, world, k * 1024 * es, 1024 * es)
+    a, e = int(b[rank]), int(b[rank + 1])
+    ho, co = lengths_to_offsets(hist_len), lengths_to_offsets(sub_len)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    eng = PoolScoreEngine(attention_model, dtype=dtype, device=dev).load_news(news_embeddings)
+    eng.load_impressions(hist_idx[ho[a]:ho[e]], hist_len[a:e], sub_news[co[a]:co[e]], sub_len[a:e])
+    local, _ = sharded_step(ShardedTable(eng, rank, world, group))
+    scores_d = gather_scores(local, world, group)
+    scores = scores_d.cpu().numpy()
+    if hb.all():
+        off = torch.as_tensor(lengths_to_offsets(imp_len)).to(dev)
+        grouped = group_items(ops.dense_rank(scores_d.contiguous(), off).cpu().numpy().astype(np.int64), imp_len)
+    else:  # reference quirk: grouping by the unfiltered lengths (see get_final_second_attention_score)
+        grouped = rank_group_preds(scores, imp_len)
+    return {"scores": scores, "grouped_scores": grouped}
