@@ -19,6 +19,10 @@
 
 #include <stdlib.h>
 
+#ifndef NR_GEMM_NT_STORE
+#define NR_GEMM_NT_STORE 0  // A/B build switch: non-temporal epilogue stores
+#endif
+
 namespace nr {
 
 constexpr int GBM = 128, GBN = 128;
@@ -52,6 +56,7 @@ struct EpiArgs {
   uint64_t seed;  // dropout stream
   uint32_t thr;   // drop iff drop_hash(seed, row * N + col) < thr  (thr = p * 2^32)
   float scale;    // 1 / (1 - p)
+  int group_m = 1;  // 256x256 tile order: >1 groups group_m M-tiles (see tile_of)
 };
 
 template <typename TO>
@@ -395,7 +400,11 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
         TO o[VEC];
 #pragma unroll
         for (int q = 0; q < VEC; ++q) o[q] = to_out<TO>(v[q]);
+#if NR_GEMM_NT_STORE
+        __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(o), reinterpret_cast<f32x4*>(C + row * ldc + ocol0 + cc));
+#else
         *reinterpret_cast<uint4*>(C + row * ldc + ocol0 + cc) = *reinterpret_cast<const uint4*>(o);
+#endif
       }
     }
     __syncthreads();
@@ -537,6 +546,25 @@ __global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, i
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
   return (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+}
+
+// Output tile of remapped id wg (an XCD runs a contiguous run of ids, ~32 at
+// a time).  gm = 1: row-major (the run shares one A panel and reads 32
+// different W panels, so at N = 8192 every W slice comes from beyond L2);
+// gm > 1: ids go column-major inside groups of gm M-tiles, so a run of 32
+// covers gm x 32/gm tiles and each A and W K-slice is fetched into the XCD's
+// L2 once for 32/gm resp. gm tiles (miss bytes per tile K-step
+// 32 KiB / (32/gm) + 32 KiB / gm instead of 32 KiB / 32 + 32 KiB).
+__device__ __forceinline__ void tile_of(int wg, int nx, int ny, int gm, int& mt, int& nt) {
+  if (gm <= 1) {
+    mt = wg / nx;
+    nt = wg % nx;
+    return;
+  }
+  const int per = gm * nx, g = wg / per, first = g * gm;
+  const int gsz = min(gm, ny - first), loc = wg - g * per;
+  mt = first + loc % gsz;
+  nt = loc / gsz;
 }
 
 template <typename TI, int EPI, typename TO, bool MF16>
@@ -734,7 +762,9 @@ __global__ __launch_bounds__(512, 2) void gemm256p_kernel(int64_t M, int64_t N, 
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE];
   const int nx = (int)gridDim.x;
   const int wg = xcd_remap((int)blockIdx.y * nx + (int)blockIdx.x, nx * (int)gridDim.y);
-  gemm256p_body<TI, EPI, TO, MF16>(smem, (int64_t)(wg / nx) * G2BM, (int64_t)(wg % nx) * G2BN, M, N, K, A, lda, W,
+  int mt, nt;
+  tile_of(wg, nx, (int)gridDim.y, ea.group_m, mt, nt);
+  gemm256p_body<TI, EPI, TO, MF16>(smem, (int64_t)mt * G2BM, (int64_t)nt * G2BN, M, N, K, A, lda, W,
                                    ldw, bias, R, ldr, C, ldc, ea);
 }
 
@@ -1194,11 +1224,15 @@ static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* 
   // persistent variant: opt-in (NR_GEMM_PERSIST=1) until its register pressure is fixed: its
   // spill reloads in the epilogue wait on the next tile's DMAs
   static const bool persist = getenv("NR_GEMM_PERSIST") != nullptr;
+  // tile order (tile_of): NR_GEMM_GROUP_M overrides the default M-tile group
+  static const int group_m = getenv("NR_GEMM_GROUP_M") ? atoi(getenv("NR_GEMM_GROUP_M")) : 4;
+  EpiArgs eg = ea;
+  eg.group_m = group_m;
   if constexpr (sizeof(TI) == 2) {
-    if (mf16 && persist) return launch_gemm256_pp<TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
-    if (mf16) return launch_gemm256_p16<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
+    if (mf16 && persist) return launch_gemm256_pp<TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
+    if (mf16) return launch_gemm256_p16<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
   }
-  return launch_gemm256_p<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
+  return launch_gemm256_p<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
 }
 
 template <typename TI, typename TO>
