@@ -19,6 +19,9 @@
 
 #include <stdlib.h>
 
+#ifndef NR_GEMM_EPI_BLOCK_SYNC
+#define NR_GEMM_EPI_BLOCK_SYNC 0  // A/B build switch: workgroup barriers between epilogue passes
+#endif
 #ifndef NR_GEMM_NT_STORE
 #define NR_GEMM_NT_STORE 0  // A/B build switch: non-temporal epilogue stores
 #endif
@@ -282,6 +285,16 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
   constexpr int RPI = 64 / LPR;                            // rows per wave instruction
   const int cl = lane & 31, rh = 4 * (lane >> 5);
   float* slab = reinterpret_cast<float*>(smem + wave * 16384);
+  // The slabs overlay the operand stages: one workgroup barrier so that no
+  // wave still reads operands; after it each wave only touches its own slab,
+  // so the passes order their LDS traffic wave-locally (no further workgroup
+  // barriers: waves drift apart and their store bursts spread out).
+#if NR_GEMM_EPI_BLOCK_SYNC
+#define NR_EPI_SYNC() __syncthreads()
+#else
+  __syncthreads();
+#define NR_EPI_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+#endif
   const int64_t wcol = n0 + wn * 64;
   const int64_t ocol0 = (EPI == NR_EPI_GEGLU) ? wcol / 2 : wcol;
   float ba = 0.f, bg = 0.f;
@@ -350,7 +363,7 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
         }
       }
     }
-    __syncthreads();
+    NR_EPI_SYNC();
     const int rr = lane / LPR, cc = (lane % LPR) * VEC;
 #pragma unroll
     for (int it = 0; it < 64 / RPI; ++it) {
@@ -407,8 +420,9 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
 #endif
       }
     }
-    __syncthreads();
+    NR_EPI_SYNC();
   }
+#undef NR_EPI_SYNC
 }
 
 template <typename TI, int EPI, typename TO>
