@@ -22,6 +22,9 @@
 #ifndef NR_GEMM_EPI_BLOCK_SYNC
 #define NR_GEMM_EPI_BLOCK_SYNC 0  // A/B build switch: workgroup barriers between epilogue passes
 #endif
+#ifndef NR_GEMM_STAMPS
+#define NR_GEMM_STAMPS 0  // diagnostic build switch: per-block phase stamps (tools/gemm_stamps.py)
+#endif
 #ifndef NR_GEMM_NT_STORE
 #define NR_GEMM_NT_STORE 0  // A/B build switch: non-temporal epilogue stores
 #endif
@@ -562,6 +565,13 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
 }
 
+#if NR_GEMM_STAMPS
+// Diagnostic build only (-DNR_GEMM_STAMPS=1, tools/gemm_stamps.py): per-block
+// s_memrealtime stamps of the 256x256 kernel's phases, written by lanes 0-7 of
+// wave 0 into a buffer nothing else reads.
+__device__ unsigned long long* g_gemm_stamps = nullptr;
+#endif
+
 // Output tile of remapped id wg (an XCD runs a contiguous run of ids, ~32 at
 // a time).  gm = 1: row-major (the run shares one A panel and reads 32
 // different W panels, so at N = 8192 every W slice comes from beyond L2);
@@ -723,6 +733,9 @@ __device__ __forceinline__ void gemm256p_body(unsigned char* smem, int64_t m0, i
   // DMAs landed too.
   const int wmu = __builtin_amdgcn_readfirstlane(wm);
   const int64_t nk = K / BK;
+#if NR_GEMM_STAMPS
+  const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
+#endif
   dmaB(0, 0, 0);
   dmaB(1, 0, 0);
   dmaA(0, 0, 0);
@@ -735,6 +748,9 @@ __device__ __forceinline__ void gemm256p_body(unsigned char* smem, int64_t m0, i
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
+#if NR_GEMM_STAMPS
+  const unsigned long long st1 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (wmu == 1) __builtin_amdgcn_s_barrier();  // stagger
   for (int64_t kt = 0; kt < nk; ++kt) {
     const int st = (int)(kt & 1), ns = st ^ 1;
@@ -764,7 +780,24 @@ __device__ __forceinline__ void gemm256p_body(unsigned char* smem, int64_t m0, i
   }
   if (wmu == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
 #undef NR_PHASE_SYNC_MMA
+#if NR_GEMM_STAMPS
+  const unsigned long long st2 = __builtin_amdgcn_s_memrealtime();
+#endif
   gemm256_store<EPI, TO, MF16>(acc, smem, wave, lane, wm, wn, m0, n0, M, N, bias, R, ldr, C, ldc, ea);
+#if NR_GEMM_STAMPS
+  const unsigned long long st3 = __builtin_amdgcn_s_memrealtime();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long st4 = __builtin_amdgcn_s_memrealtime();
+  if (wave == 0 && lane < 8 && g_gemm_stamps) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20); // XCC_ID
+    const unsigned long long v[8] = {st0, st1, st2, st3, st4, hw, xcc, (unsigned long long)(m0 << 20 | n0)};
+    unsigned long long x = v[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) x = lane == i ? v[i] : x;
+    g_gemm_stamps[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + lane] = x;
+  }
+#endif
 }
 
 template <typename TI, int EPI, typename TO, bool MF16 = false>
@@ -1403,3 +1436,9 @@ extern "C" int nr_gemm_grouped(int dtype_in, int dtype_out, int n, const int64_t
   NR_CHECK_LAUNCH("nr_gemm_grouped");
   return NR_OK;
 }
+
+#if NR_GEMM_STAMPS
+extern "C" int nr_debug_gemm_stamps(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(nr::g_gemm_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
+#endif
