@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+from itertools import islice
 from pathlib import Path
 from typing import Optional, Sequence
 
@@ -88,9 +89,8 @@ def split_behaviors(impressions: Sequence[str], history: Sequence[Optional[str]]
     raw = news_b.raw[:nbytes].decode("ascii")
     news_list = [raw[news_off[i]:news_off[i + 1]] for i in range(n_news)]
     if label_present:
-        ends = np.cumsum(imp_len)
-        lab = labels.astype(np.int64).tolist()
-        tuples = [tuple(lab[e - n:e]) for e, n in zip(ends.tolist(), imp_len.tolist())]
+        it = iter(labels.tolist())  # Python ints, like the reference's int(x[1])
+        tuples = [tuple(islice(it, n)) for n in imp_len.tolist()]
     else:
         tuples = []
     return {

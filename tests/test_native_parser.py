@@ -91,3 +91,30 @@ def test_native_parser_speed_and_equality_at_scale():
     _same(a, b)
     print(f"native {t_native:.3f}s vs python {t_py:.3f}s for {len(impr)} rows")
     assert t_native < t_py
+
+
+@pytest.mark.parametrize("threads", ["2", "5", "16"])
+def test_parallel_chunks_keep_first_appearance_order(monkeypatch, threads):
+    """Rows cut into many tiny chunks (NRH_CHUNK_BYTES=1): ids first seen in a
+    later chunk, ids shared by every chunk, falsy histories and unlabelled rows
+    all number exactly as the sequential reference loop does."""
+    monkeypatch.setenv("NRH_THREADS", threads)
+    monkeypatch.setenv("NRH_CHUNK_BYTES", "1")
+    rng = np.random.default_rng(int(threads))
+    ids = [f"N{i}" for i in rng.permutation(300)]
+    for labels in (True, False):
+        hist, imps = [], []
+        for r in range(97):
+            h = rng.choice(ids[: 20 + 3 * r], size=rng.integers(0, 6)).tolist()
+            hist.append(" ".join(h) if h else (None if r % 3 else ""))
+            c = rng.choice(ids[: 30 + 2 * r], size=rng.integers(1, 5)).tolist()
+            imps.append(" ".join(f"{x}-{int(rng.random() < 0.3)}" if labels else x for x in c))
+        _same(native.split_behaviors(imps, hist), data_ref.split_impressions_and_history(imps, hist))
+
+
+def test_parallel_chunks_report_the_first_failing_row(monkeypatch):
+    monkeypatch.setenv("NRH_THREADS", "4")
+    monkeypatch.setenv("NRH_CHUNK_BYTES", "1")
+    imps = ["N1-1 N2-0"] * 10 + ["N1-1 N2"] + ["N3-x"] * 5
+    assert native.split_behaviors(imps, [None] * len(imps)) is None
+    assert b"row 10:" in native.load().nrh_last_error()
