@@ -349,6 +349,18 @@ def main():
             del r, tb, im
             torch.cuda.empty_cache()
         extra["metrics_ms"] = round(metrics_ms(head), 3)
+        # PCIe-side costs (never part of `value`): the CSR index upload incl. its host-side
+        # offsets (load_impressions is idempotent) and the score download
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        head.eng.load_impressions(imps.hist_idx, imps.hist_len, imps.cand_idx, imps.cand_len)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        head.scores.cpu()
+        t2 = time.perf_counter()
+        extra["pcie_ms"] = {"h2d_index_arrays": round((t1 - t0) * 1e3, 3), "d2h_scores": round((t2 - t1) * 1e3, 3),
+                            "index_bytes": int(4 * (imps.n_hist + imps.n_cand) + 8 * 2 * (imps.n_imp + 1)),
+                            "score_bytes": int(4 * imps.n_cand)}
         extra["train_bf16_config5"] = train_step_ms(dev)
 
     cpu = None
