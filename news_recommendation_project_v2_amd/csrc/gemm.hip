@@ -25,6 +25,9 @@
 #ifndef NR_GEMM_STAMPS
 #define NR_GEMM_STAMPS 0  // diagnostic build switch: per-block phase stamps (tools/gemm_stamps.py)
 #endif
+#ifndef NR_GEMM_SLAB16
+#define NR_GEMM_SLAB16 0  // A/B build switch: bf16 epilogue slab for pointwise epilogues (measured slower)
+#endif
 #ifndef NR_GEMM_NT_STORE
 #define NR_GEMM_NT_STORE 0  // A/B build switch: non-temporal epilogue stores
 #endif
@@ -311,8 +314,78 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
     ba = bias[wcol + cl];
     bg = bias[wcol + 32 + cl];
   }
+  // bf16 output of a pointwise epilogue on 16x16 tiles: the slab holds the
+  // final bf16 values (half the LDS round trip).  A lane's 4 rows of one
+  // column are paired with the neighbour lane's column by one DPP swap so each
+  // LDS write is a 2-column bf16 dword; dwords XOR-swizzled by row pair so the
+  // 32 lanes of a write hit distinct banks (COLS 64; 2-way for GEGLU's 32).
+  constexpr bool SLAB16 = MF16 && NR_GEMM_SLAB16 && sizeof(TO) == 2 &&
+                          (EPI == NR_EPI_NONE || EPI == NR_EPI_RELU || EPI == NR_EPI_EXP || EPI == NR_EPI_GELU ||
+                           EPI == NR_EPI_GEGLU || EPI == NR_EPI_RELU_DROPOUT);
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
+    if constexpr (SLAB16) {
+      constexpr int DW = COLS / 2;  // dwords per slab row
+      uint32_t* s32 = reinterpret_cast<uint32_t*>(slab);
+      auto sidx = [](int row, int dw) {
+        const int x = DW == 32 ? ((row >> 1) & 3) << 3 : ((row >> 1) & 1) << 3;
+        return row * DW + (dw ^ x);
+      };
+      const int c16 = lane & 15, r16 = 4 * (lane >> 4);
+      const bool odd = lane & 1;
+      constexpr int NOUT = (EPI == NR_EPI_GEGLU) ? 2 : 4;  // 16-column output groups per wave
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int mi = 4 * pass + i;
+#pragma unroll
+        for (int ni = 0; ni < NOUT; ++ni) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if constexpr (EPI == NR_EPI_GEGLU) {
+              v[r] = (acc[mi][ni][r] + b16[ni]) * gelu_erf(acc[mi][ni + 2][r] + b16[ni + 2]);
+            } else {
+              float x = acc[mi][ni][r] + b16[ni];
+              if constexpr (EPI == NR_EPI_RELU) x = fmaxf(x, 0.f);
+              if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
+                const uint64_t gi = (uint64_t)((m0 + wm * 128 + pass * 64 + 16 * i + r16 + r) * N + wcol + 16 * ni + c16);
+                x = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(x, 0.f) * ea.scale;
+              }
+              if constexpr (EPI == NR_EPI_EXP) x = expf(x);
+              if constexpr (EPI == NR_EPI_GELU) x = gelu_erf(x);
+              v[r] = x;
+            }
+          }
+          // even lane keeps rows 0-1 and receives the odd neighbour's rows 0-1; odd keeps rows 2-3
+          const float x0 = odd ? v[0] : v[2], x1 = odd ? v[1] : v[3];
+          const float y0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x0), 0xB1, 0xF, 0xF, false));
+          const float y1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x1), 0xB1, 0xF, 0xF, false));
+          const float lo0 = odd ? y0 : v[0], hi0 = odd ? v[2] : y0;
+          const float lo1 = odd ? y1 : v[1], hi1 = odd ? v[3] : y1;
+          const int row0 = 16 * i + r16 + (odd ? 2 : 0);
+          const int dw = (16 * ni + (c16 & ~1)) >> 1;
+          const uint32_t p0 = (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)lo0) |
+                              ((uint32_t)__builtin_bit_cast(unsigned short, (__bf16)hi0) << 16);
+          const uint32_t p1 = (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)lo1) |
+                              ((uint32_t)__builtin_bit_cast(unsigned short, (__bf16)hi1) << 16);
+          s32[sidx(row0, dw)] = p0;
+          s32[sidx(row0 + 1, dw)] = p1;
+        }
+      }
+      NR_EPI_SYNC();
+      constexpr int LPR16 = DW / 4;     // lanes per row (16 B each)
+      constexpr int RPI16 = 64 / LPR16;  // rows per wave instruction
+      const int rr16 = lane / LPR16, cd = (lane % LPR16) * 4;
+#pragma unroll
+      for (int it = 0; it < 64 / RPI16; ++it) {
+        const int lr = it * RPI16 + rr16;
+        const int64_t row = m0 + wm * 128 + pass * 64 + lr;
+        const uint4 q = *reinterpret_cast<const uint4*>(s32 + sidx(lr, cd));
+        if (row < M) *reinterpret_cast<uint4*>(C + row * ldc + ocol0 + 2 * cd) = q;
+      }
+      NR_EPI_SYNC();
+      continue;
+    }
     if constexpr (MF16) {
       // 16x16 C/D map: col = lane & 15, row = 4 * (lane >> 4) + r
       const int c16 = lane & 15, r16 = 4 * (lane >> 4);
