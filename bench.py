@@ -1,28 +1,41 @@
 #!/usr/bin/env python3
 """Headline benchmark: scored candidates/sec on MIND-large-shaped impressions.
 
-    python bench.py [--gpus N --steps K --warmup W --pooler latent|final --dtype bf16|fp32]
+    python bench.py [--gpus N --steps K --warmup W --pooler latent|final --dtype bf16|fp32
+                     --scaling strong|weak --backend nccl|gloo]
 
-Workload (BASELINE.json configs[2], "MIND-large eval on 1xMI355X, bf16"):
-synthetic MIND-large-dev-shaped impressions (N = 72,023 news, I = 376,471
-impressions per GPU, h ~ geometric(1/33), c ~ geometric(1/37)), a seeded
-N(0,1) news table resident in HBM, deterministic random-init pooler weights
-(no checkpoint exists).  One step = the per-news pooler transform over all N
-news (MFMA GEMM chain) + candidate inverse norms + the fused pool+score kernel
-over every impression, i.e. everything `scripts/eval.py` computes between
-loading the table and ranking.  For N > 1 (one process per GPU under
-torch.distributed.run, RCCL) every rank owns its own MIND-large-dev-sized
-impression set (weak scaling); the news-table transform is sharded N ways and
-all-gathered once per step over xGMI.
+Workload (BASELINE.json configs[2] at N = 1, configs[3] at N > 1): synthetic
+MIND-large-dev-shaped impressions (N = 72,023 news, I = 376,471 impressions,
+h ~ geometric(1/33), c ~ geometric(1/37)), a seeded N(0,1) news table resident
+in HBM, deterministic random-init pooler weights (no checkpoint exists).  One
+step = the per-news pooler transform (MFMA GEMM chain) + candidate inverse
+norms + the fused pool+score kernel, i.e. everything `scripts/eval.py`
+computes between loading the table and ranking.
+
+Multi-GPU (one process per GPU, RCCL over xGMI).  ``--gpus N`` with no
+WORLD_SIZE in the environment re-launches this script under
+``torch.distributed.run`` with N ranks (as a child process, before any GPU
+call).  Default ``--scaling strong`` = configs[3]: ONE MIND-large-dev set;
+every rank transforms 1/N of the news table, one RCCL all-gather gives every
+GPU the whole table, impressions are split into N contiguous cost-balanced
+ranges (``partition_by_cost``) and each rank pools + scores its range.  The
+step is timed from a barrier to the last rank's completion (max over ranks)
+and ``value`` = the set's candidates / that time.  ``--scaling weak`` (and
+the ``weak_scaling`` extra at N > 1) gives every rank its own full set.
 
 Also reported in the same JSON line:
-  roofline      the pool+score kernel (dominant, HBM-bound): algorithmic bytes
-                per launch / its HIP-event-timed average duration vs 8 TB/s
-  cpu_baseline  the oracle (reference algorithm restated on PyTorch CPU:
+  roofline      the pool+score kernel (dominant; a random-row gather served by
+                HBM + Infinity Cache): algorithmic bytes per launch / its
+                HIP-event average duration, vs the 8 TB/s HBM spec and vs the
+                measured random-row gather ceiling of the microarch guide
+  cpu_baseline  the oracle (the reference algorithm restated on PyTorch CPU:
                 padded batches of 128, pooler per padded slot, per-impression
-                cosine loop) timed on this host on a bounded sample
-  extra         the FinalAttention pooler (the one scripts/eval.py runs), the
-                f32 numbers, per-stage times, and the bf16-vs-f32 AUC check
+                cosine loop) on all affinity cores of this host, on the first
+                1,000 impressions of a MIND-small-shaped set (configs[0]), for
+                both poolers; ``--cpu-10k`` adds 10,000
+  extra         the FinalAttention pooler, f32, per-stage times, AUC of the GPU
+                path vs the CPU reference on the config-1 sample, MIND-large
+                test shape, Zipf ids, device metrics, PCIe costs, config 5
 """
 from __future__ import annotations
 
@@ -30,6 +43,8 @@ import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -43,12 +58,12 @@ sys.path.insert(0, str(REPO))
 
 from news_recommendation_project_v2_amd import synthetic  # noqa: E402
 from news_recommendation_project_v2_amd import weights as W  # noqa: E402
-from news_recommendation_project_v2_amd.distributed import ShardedTable, sharded_step  # noqa: E402
-from news_recommendation_project_v2_amd.engine import PoolScoreEngine  # noqa: E402
-from news_recommendation_project_v2_amd.latent_attention import LatentAttentionModel  # noqa: E402
-from news_recommendation_project_v2_amd.modeling_utils import FinalAttention  # noqa: E402
+from news_recommendation_project_v2_amd.distributed import ShardedTable, partition_by_cost, sharded_step  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# measured random-row gather rate of a ~151 MB table, every CU gathering
+# (MI355X_MICROARCH.md "Indexed rows": 7.4-7.9 TB/s); the upper end is used
+GATHER_CEILING_GBS = 7900.0
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}
 DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32}
 
@@ -58,7 +73,28 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv: list) -> int:
+    """Run this script under torch.distributed.run with n ranks (child process;
+    nothing here has touched the GPU) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(Path(__file__).resolve()), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log("[bench] launching", " ".join(cmd))
+    return subprocess.call(cmd, env=env)
+
+
 def make_model(pooler: str, dev):
+    from news_recommendation_project_v2_amd.latent_attention import LatentAttentionModel
+    from news_recommendation_project_v2_amd.modeling_utils import FinalAttention
     if pooler == "final":
         m = FinalAttention(1024, 4096)
         m.load_state_dict(W.final_attention_state_dict(1234))
@@ -66,6 +102,10 @@ def make_model(pooler: str, dev):
         m = LatentAttentionModel()
         m.load_state_dict(W.latent_attention_state_dict(1234))
     return m.to(dev).eval()
+
+
+def state_dict(pooler: str) -> dict:
+    return W.final_attention_state_dict(1234) if pooler == "final" else W.latent_attention_state_dict(1234)
 
 
 def news_table(n: int, dev) -> torch.Tensor:
@@ -89,7 +129,10 @@ def tx_flops(n: int, pooler: str) -> float:
 
 
 class Run:
+    """One pooler/dtype on one rank: engine + its impression range + sharded table."""
+
     def __init__(self, pooler, dtype, imps, table, dev, rank, world):
+        from news_recommendation_project_v2_amd.engine import PoolScoreEngine
         self.pooler, self.dtype = pooler, dtype
         self.model = make_model(pooler, dev)
         self.eng = PoolScoreEngine(self.model, dtype=DTYPES[dtype], device=dev).load_news(table)
@@ -104,7 +147,7 @@ class Run:
     def stage_times(self, reps: int = 3):
         """HIP-event times (ms) of each stage, events on the launch stream."""
         s = torch.cuda.current_stream()
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         acc = np.zeros(3)
         for _ in range(reps):
             ev[0].record(s)
@@ -119,22 +162,23 @@ class Run:
         return acc / reps
 
 
-def timed(run: Run, steps: int, warmup: int, world: int, dev):
+def timed(step, steps: int, warmup: int, world: int, dev, host_reduce: bool):
+    """Warmup, then `steps` steps bracketed by barrier + device sync; max over ranks."""
     for _ in range(warmup):
-        run.step()
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        run.step()
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device="cpu" if host_reduce else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     return dt
@@ -169,7 +213,7 @@ def metrics_ms(run: Run, reps: int = 3) -> float:
 def train_step_ms(dev, batch_rows: int = 256, steps: int = 10) -> dict:
     """Config 5 (BASELINE configs[4]): one FinalAttentionTrainStep (fwd + bwd +
     clip + AdamW, bf16 MFMA) on a synthetic MIND-shaped batch."""
-    from news_recommendation_project_v2_amd.modeling_utils import get_token_attn_model
+    from news_recommendation_project_v2_amd.modeling_utils import FinalAttention, get_token_attn_model
     from news_recommendation_project_v2_amd.train_step import FinalAttentionTrainStep, TrainBatch
     rng = np.random.default_rng(1234)
     h = np.clip(rng.geometric(1 / 33.0, batch_rows), 1, 600)
@@ -201,58 +245,85 @@ def train_step_ms(dev, batch_rows: int = 256, steps: int = 10) -> dict:
             "gemm_tflops": round(eng.flops_per_step(Hs) / ms / 1e9, 1)}
 
 
-def cpu_baseline(pooler: str, imps, table_cpu: torch.Tensor, budget_s: float):
-    """Reference algorithm (oracle, PyTorch CPU f32) on the first impressions of
-    the same workload, batches of 128 until ~budget_s of CPU work."""
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_reference(pooler: str, imps, table_cpu: torch.Tensor, budget_s: float):
+    """The reference algorithm (oracle, PyTorch CPU f32: padded batches of 128,
+    pooler per padded slot, per-impression cosine) over the given impressions,
+    128 at a time, stopping early only if `budget_s` of CPU time is spent.
+    Returns (impressions done, candidates done, seconds, scores)."""
     from oracle import pool_ref
-    cores = min(16, len(os.sched_getaffinity(0)))
-    torch.set_num_threads(cores)
-    sd = W.final_attention_state_dict(1234) if pooler == "final" else W.latent_attention_state_dict(1234)
+    sd = state_dict(pooler)
     ho, co = imps.hist_off(), imps.cand_off()
-    done_imp, done_cand, t_used, parts = 0, 0, 0.0, []
-    while t_used < budget_s and done_imp < imps.n_imp:
+    done_imp, t_used, parts = 0, 0.0, []
+    while done_imp < imps.n_imp and t_used < budget_s:
         a, b = done_imp, min(done_imp + 128, imps.n_imp)
         t0 = time.perf_counter()
         parts.append(pool_ref.cos_sim_scores(pooler, sd, imps.hist_idx[ho[a]:ho[b]], imps.hist_len[a:b],
                                              imps.cand_idx[co[a]:co[b]], imps.cand_len[a:b], table_cpu))
         t_used += time.perf_counter() - t0
-        done_cand += int(co[b] - co[a])
         done_imp = b
-    cpu = platform.processor() or platform.machine()
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    res = {"value": done_cand / t_used, "unit": "scored candidates/s", "cores": cores, "kind": "port",
-           "sample": f"first {done_imp} impressions ({done_cand} candidates) of the same synthetic workload, "
-                     f"{pooler} pooler, f32, {t_used:.1f}s on {cores} threads of {cpu}"}
-    return res, done_imp, torch.cat(parts).numpy()
+    return done_imp, int(co[done_imp]), t_used, torch.cat(parts).numpy()
 
 
-def auc_vs_cpu(runs: dict, imps, n_imp: int, cpu_scores: np.ndarray) -> dict:
-    """BASELINE's parity half: mean AUC of the GPU path (device scores -> device
-    dense ranks -> device metrics) vs the CPU reference restatement (oracle f32
-    scores -> scipy rankdata -> sklearn roc_auc_score per impression), on the
-    impressions the CPU leg scored."""
+def cpu_leg(args, dev) -> tuple:
+    """the CPU reference restatement timed on this host's cores
+    (all of its affinity set) on the first 1,000 impressions of a MIND-small-
+    shaped set (configs[0]) for both poolers; the GPU path scores the same
+    impressions (f32 and bf16) for the AUC / score parity check."""
     from news_recommendation_project_v2_amd import evaluation
+    from news_recommendation_project_v2_amd.engine import PoolScoreEngine
     from oracle import data_ref, pool_ref
-    co = imps.cand_off()
-    nc = int(co[n_imp])
-    grouped_y = [imps.labels[co[i]:co[i + 1]] for i in range(n_imp)]
-    cpu = data_ref.score(pool_ref.dense_ranks(cpu_scores, imps.cand_len[:n_imp]), grouped_y)
-    out = {"impressions": n_imp, "candidates": nc, "cpu_ref": {k: cpu[k] for k in ("auc", "mrr", "ndcg5", "ndcg10")}}
-    for name, run in runs.items():
-        s, _ = run.step()
-        r = run.eng.rank(s)[:nc]
-        g = evaluation.score_device(r, imps.labels[:nc], co[:n_imp + 1])
-        out[name] = {k: g[k] for k in ("auc", "mrr", "ndcg5", "ndcg10")}
-        out[name]["max_abs_score_diff"] = float(np.abs(s[:nc].cpu().numpy() - cpu_scores).max())
-        out[name]["auc_abs_diff"] = abs(g["auc"] - cpu["auc"])
-        out[name]["auc_equal_4dp"] = round(g["auc"], 4) == round(cpu["auc"], 4)
-    return out
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
+    n_news, n_imp_full = synthetic.SHAPES[args.cpu_shape]
+    full = synthetic.mind_impressions(n_news, n_imp_full, seed=1234)
+    table_d = news_table(n_news, dev)
+    table_c = table_d.cpu()
+    samples = [args.cpu_impressions] + ([10_000] if args.cpu_10k else [])
+    out, parity = {}, {}
+    for pooler in ("latent", "final"):
+        for n_imp in samples:
+            imps = full.slice(0, n_imp)
+            done, ncand, secs, cpu_scores = cpu_reference(pooler, imps, table_c, args.cpu_seconds)
+            out.setdefault(pooler, {})[f"first_{n_imp}"] = {
+                "impressions": done, "candidates": ncand, "seconds": round(secs, 2),
+                "value": round(ncand / secs, 1)}
+            log(f"[bench] CPU reference {pooler} first {n_imp}: {done} imps {ncand} cands in {secs:.1f}s "
+                f"= {ncand / secs:.0f} cand/s on {cores} threads")
+            if n_imp != args.cpu_impressions:
+                continue
+            sub = imps.slice(0, done)
+            grouped_y = sub.grouped_labels()
+            cpu_m = data_ref.score(pool_ref.dense_ranks(cpu_scores, sub.cand_len), grouped_y)
+            parity[pooler] = {"impressions": done, "candidates": ncand,
+                              "cpu_ref": {k: cpu_m[k] for k in ("auc", "mrr", "ndcg5", "ndcg10")}}
+            for dt in ("fp32", "bf16"):
+                eng = PoolScoreEngine(make_model(pooler, dev), dtype=DTYPES[dt], device=dev).load_news(table_d)
+                eng.load_impressions(sub.hist_idx, sub.hist_len, sub.cand_idx, sub.cand_len)
+                s, _ = eng.step()
+                g = evaluation.score_device(eng.rank(s), sub.labels, sub.cand_off())
+                d = {k: g[k] for k in ("auc", "mrr", "ndcg5", "ndcg10")}
+                d["max_abs_score_diff"] = float(np.abs(s.cpu().numpy() - cpu_scores).max())
+                d["auc_abs_diff"] = abs(g["auc"] - cpu_m["auc"])
+                d["auc_equal_4dp"] = round(g["auc"], 4) == round(cpu_m["auc"], 4)
+                parity[pooler][f"gpu_{dt}"] = d
+                del eng
+    head = out[args.pooler][f"first_{args.cpu_impressions}"]
+    base = {"value": head["value"], "unit": "scored candidates/s", "cores": cores, "kind": "port",
+            "sample": f"first {head['impressions']} impressions ({head['candidates']} candidates) of the seeded "
+                      f"{args.cpu_shape}-shaped set (configs[0]), {args.pooler} pooler (headline), f32, "
+                      f"{head['seconds']}s on {cores} threads of {cpu_model()}; both poolers in by_pooler",
+            "by_pooler": out}
+    return base, parity
 
 
 def load_traffic(pooler: str, dtype: str):
@@ -263,6 +334,33 @@ def load_traffic(pooler: str, dtype: str):
     return None
 
 
+def dry_run(args, rank: int, world: int) -> None:
+    """--dry-run (CPU, gloo): the launch / partition / all-gather / max-over-ranks
+    plumbing without the GPU (what the CPU test suite can check)."""
+    n_news, n_imp = synthetic.SHAPES[args.shape]
+    n_imp = args.impressions or n_imp
+    full = synthetic.mind_impressions(n_news, n_imp, seed=1234)
+    b = partition_by_cost(full.hist_len, full.cand_len, world, 1024 * 2, 1024 * 2)
+    mine = full.slice(int(b[rank]), int(b[rank + 1]))
+    rows = (n_news + world - 1) // world
+    local = torch.full((rows, 4), float(rank))
+    table = torch.empty((rows * world, 4))
+    t0 = time.perf_counter()
+    dist.all_gather_into_tensor(table, local)
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    c = torch.tensor([mine.n_cand, mine.n_imp], dtype=torch.int64)
+    dist.all_reduce(c)
+    ok = bool(torch.equal(table[:, 0], torch.arange(world).repeat_interleave(rows).float()))
+    if rank == 0:
+        print(json.dumps({"metric": "scored candidates/sec on MIND-large impressions; AUC parity vs CPU ref",
+                          "dry_run": True, "value": None, "n_gpus": world, "scaling": args.scaling,
+                          "partition": [int(x) for x in b], "candidates_total": int(c[0]),
+                          "impressions_total": int(c[1]), "candidates_expected": full.n_cand,
+                          "allgather_ok": ok, "allgather_s": float(t.item())}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -271,62 +369,114 @@ def main():
     ap.add_argument("--pooler", choices=["latent", "final"], default="latent")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--shape", default="mind_large_dev", choices=list(synthetic.SHAPES))
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--impressions", type=int, default=0, help="override the shape's impression count")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong: one set partitioned over the ranks (configs[3]); weak: a full set per rank")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="gloo: test mode, ranks may share one GPU (tables staged through the host)")
+    ap.add_argument("--cpu-shape", default="mind_small_dev", choices=list(synthetic.SHAPES))
+    ap.add_argument("--cpu-impressions", type=int, default=1000)
+    ap.add_argument("--cpu-10k", action="store_true", help="also time the CPU reference on 10,000 impressions")
+    ap.add_argument("--cpu-seconds", type=float, default=60.0, help="CPU-time cap per pooler and sample")
     ap.add_argument("--no-extra", action="store_true", help="headline config only")
+    ap.add_argument("--dry-run", action="store_true", help="CPU-only check of the multi-rank plumbing")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        try:
+            dry_run(args, rank, world) if world > 1 else print(json.dumps({"dry_run": True, "n_gpus": 1}))
+        finally:
+            if world > 1:
+                dist.destroy_process_group()
+        return
+
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
+    host_reduce = args.backend == "gloo"
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     n_news, n_imp = synthetic.SHAPES[args.shape]
+    n_imp = args.impressions or n_imp
     t0 = time.time()
-    imps = synthetic.mind_impressions(n_news, n_imp, seed=1234 + rank)
+    es = 2 if args.dtype == "bf16" else 4
+    kw = 2 if args.pooler == "final" else 1
+    if args.scaling == "strong":
+        full = synthetic.mind_impressions(n_news, n_imp, seed=1234)
+        bounds = partition_by_cost(full.hist_len, full.cand_len, world, kw * 1024 * es, 1024 * es)
+        imps = full.slice(int(bounds[rank]), int(bounds[rank + 1]))
+        total_cand = full.n_cand
+    else:
+        full, bounds = None, None
+        imps = synthetic.mind_impressions(n_news, n_imp, seed=1234 + rank)
+        total_cand = None
     table = news_table(n_news, dev)
-    log(f"[bench] data ready in {time.time() - t0:.1f}s: N={n_news} I={imps.n_imp} C={imps.n_cand} H={imps.n_hist}")
+    log(f"[bench] data ready in {time.time() - t0:.1f}s: N={n_news} I={imps.n_imp} C={imps.n_cand} "
+        f"H={imps.n_hist} (rank 0 of {world}, {args.scaling} scaling)")
 
     head = Run(args.pooler, args.dtype, imps, table, dev, rank, world)
-    dt = timed(head, args.steps, args.warmup, world, dev)
+    dt = timed(head.step, args.steps, args.warmup, world, dev, host_reduce)
     ms = dt / args.steps * 1e3
-    total_cand = imps.n_cand * world  # every rank holds a same-sized set
-    if world > 1:
-        c = torch.tensor([imps.n_cand], dtype=torch.int64, device=dev)
-        dist.all_reduce(c)
+    if total_cand is None:  # weak: every rank's own set
+        c = torch.tensor([imps.n_cand], dtype=torch.int64, device="cpu" if host_reduce else dev)
+        if world > 1:
+            dist.all_reduce(c)
         total_cand = int(c.item())
     value = total_cand / (dt / args.steps)
     stages = head.stage_times()
-    es = 2 if args.dtype == "bf16" else 4
     bytes_ps = ps_bytes(imps, args.pooler, es)
     achieved = bytes_ps / (stages[2] * 1e-3) / 1e9
-    log(f"[bench] {args.pooler}/{args.dtype}: {ms:.2f} ms/step, {value:.3e} cand/s; stages ms "
-        f"transform+gather={stages[0]:.2f} invnorm={stages[1]:.3f} pool_score={stages[2]:.2f}")
+    log(f"[bench] {args.pooler}/{args.dtype} x{world}: {ms:.3f} ms/step, {value:.3e} cand/s; stages ms "
+        f"transform+gather={stages[0]:.3f} invnorm={stages[1]:.3f} pool_score={stages[2]:.3f}")
 
+    tx_rank = tx_flops(head.tab.rows, args.pooler)  # this rank's shard of the transform
     extra = {"stage_ms": {"transform_allgather": round(stages[0], 3), "inv_norm": round(stages[1], 4),
                           "pool_score": round(stages[2], 3)},
-             "transform_tflops": round(tx_flops(n_news, args.pooler) / world / (stages[0] * 1e-3) / 1e12, 1),
-             "transform_peak_frac": round(tx_flops(n_news, args.pooler) / world / (stages[0] * 1e-3) / 1e12
-                                          / MFMA_PEAK_TFLOPS[args.dtype], 3),
+             "transform_tflops": round(tx_rank / (stages[0] * 1e-3) / 1e12, 1),
+             "transform_peak_frac": round(tx_rank / (stages[0] * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS[args.dtype], 3),
              "step_roofline_frac": round((bytes_ps / (HBM_PEAK_GBS * 1e9)
-                                          + tx_flops(n_news, args.pooler) / world / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12))
-                                         / (ms * 1e-3), 4),
-             "n_news": n_news, "impressions_per_gpu": imps.n_imp, "candidates_per_gpu": imps.n_cand,
-             "history_slots_per_gpu": imps.n_hist}
-    if not args.no_extra:
+                                          + tx_rank / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)) / (ms * 1e-3), 4),
+             "n_news": n_news, "impressions_rank0": imps.n_imp, "candidates_rank0": imps.n_cand,
+             "history_slots_rank0": imps.n_hist, "candidates_total": total_cand}
+    if bounds is not None and world > 1:
+        extra["partition"] = [int(x) for x in bounds]
+
+    if world > 1 and not args.no_extra and args.scaling == "strong":
+        # weak scaling as an extra: every rank its own full MIND-large-dev-sized set
+        own = synthetic.mind_impressions(n_news, n_imp, seed=1234 + rank)
+        r = Run(args.pooler, args.dtype, own, table, dev, rank, world)
+        d = timed(r.step, max(3, args.steps // 2), 2, world, dev, host_reduce) / max(3, args.steps // 2)
+        c = torch.tensor([own.n_cand], dtype=torch.int64, device="cpu" if host_reduce else dev)
+        dist.all_reduce(c)
+        extra["weak_scaling"] = {"value": round(int(c.item()) / d, 1), "ms_per_step": round(d * 1e3, 3),
+                                 "impressions_per_gpu": own.n_imp}
+        del r, own
+        torch.cuda.empty_cache()
+
+    if world == 1 and not args.no_extra:
         for pooler, dtype in [(args.pooler, "fp32" if args.dtype == "bf16" else "bf16"),
                               ("final" if args.pooler == "latent" else "latent", args.dtype)]:
             r = Run(pooler, dtype, imps, table, dev, rank, world)
-            d = timed(r, max(3, args.steps // 2), 2, world, dev)
+            k = max(3, args.steps // 2)
+            d = timed(r.step, k, 2, world, dev, host_reduce) / k
             st = r.stage_times(2)
             e2 = 2 if dtype == "bf16" else 4
             extra[f"{pooler}_{dtype}"] = {
-                "value": round(total_cand / (d / max(3, args.steps // 2)), 1),
-                "ms_per_step": round(d / max(3, args.steps // 2) * 1e3, 3),
+                "value": round(total_cand / d, 1), "ms_per_step": round(d * 1e3, 3),
                 "pool_score_ms": round(st[2], 3), "transform_ms": round(st[0], 3),
                 "pool_score_GBs": round(ps_bytes(imps, pooler, e2) / (st[2] * 1e-3) / 1e9, 1)}
             if pooler == args.pooler:
@@ -337,13 +487,13 @@ def main():
         # throughput on the MIND-large *test* shape and cache sensitivity under Zipf(1.1) id popularity
         for tag, shape, zipf in [("mind_large_test", "mind_large_test", None), ("zipf1.1", args.shape, 1.1)]:
             nn_, ni_ = synthetic.SHAPES[shape]
-            im = synthetic.mind_impressions(nn_, ni_, seed=1234 + rank, zipf=zipf)
+            im = synthetic.mind_impressions(nn_, ni_, seed=1234, zipf=zipf)
             tb = table if nn_ == n_news else news_table(nn_, dev)
             r = Run(args.pooler, args.dtype, im, tb, dev, rank, world)
-            d = timed(r, 3, 1, world, dev) / 3
+            d = timed(r.step, 3, 1, world, dev, host_reduce) / 3
             st = r.stage_times(2)
-            extra[tag] = {"n_news": nn_, "impressions_per_gpu": im.n_imp, "candidates_per_gpu": im.n_cand,
-                          "value": round(im.n_cand * world / d, 1), "ms_per_step": round(d * 1e3, 3),
+            extra[tag] = {"n_news": nn_, "impressions": im.n_imp, "candidates": im.n_cand,
+                          "value": round(im.n_cand / d, 1), "ms_per_step": round(d * 1e3, 3),
                           "pool_score_ms": round(st[2], 3),
                           "pool_score_GBs": round(ps_bytes(im, args.pooler, es) / (st[2] * 1e-3) / 1e9, 1)}
             del r, tb, im
@@ -366,12 +516,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         log("[bench] timing the CPU reference restatement ...")
-        cpu, n_cpu, cpu_scores = cpu_baseline(args.pooler, imps, table.cpu(), args.cpu_seconds)
-        runs = {f"gpu_{args.dtype}": head}
-        if not args.no_extra:
-            runs[f"gpu_{'fp32' if args.dtype == 'bf16' else 'bf16'}"] = Run(
-                args.pooler, "fp32" if args.dtype == "bf16" else "bf16", imps, table, dev, rank, world)
-        extra["auc_vs_cpu_ref"] = auc_vs_cpu(runs, imps, n_cpu, cpu_scores)
+        cpu, extra["auc_vs_cpu_ref"] = cpu_leg(args, dev)
         log(f"[bench] AUC vs CPU reference: {json.dumps(extra['auc_vs_cpu_ref'])}")
 
     if rank == 0:
@@ -384,18 +529,25 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (seeded MIND-large-dev-shaped impressions, N(0,1) news table, deterministic "
                     "random-init pooler weights)",
             "config": {"workload": f"{args.shape} eval, {args.pooler} pooler: per-news transform + pool + "
                                    f"cosine score", "pooler": args.pooler, "n_news": n_news,
-                       "impressions_per_gpu": imps.n_imp, "parallelism": f"impressions x{world}, news-table "
-                                                                         f"transform sharded + all-gather"},
-            "roofline": {"bound": "hbm", "kernel": "pool_score_kernel", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic(args.pooler, args.dtype),
+                       "impressions": n_imp if args.scaling == "strong" else n_imp * world,
+                       "parallelism": f"impressions x{world} ({args.scaling}), news-table transform sharded + "
+                                      f"all-gather ({args.backend})"},
+            "roofline": {"bound": "hbm", "kernel": "pool_score_kernel",
+                         "bound_detail": "random-row gather of ~150-300 MB tables (L2 miss, served by HBM + "
+                                         "Infinity Cache); 8 TB/s is the HBM spec, the gather ceiling is the "
+                                         "guide's measured 7.4-7.9 TB/s",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "gather_ceiling": GATHER_CEILING_GBS,
+                         "frac_vs_gather_ceiling": round(achieved / GATHER_CEILING_GBS, 4),
+                         "traffic": load_traffic(args.pooler, args.dtype) if world == 1 else None,
                          "algorithmic_bytes_per_launch": bytes_ps, "avg_launch_ms": round(stages[2], 4)},
             "cpu_baseline": cpu,
             "extra": extra,

@@ -11,9 +11,7 @@ import ctypes
 import os
 from pathlib import Path
 
-# NR_HIP_LIB: another build of the same C-ABI (A/B timing of a kernel change on one box)
-LIB_PATH = (Path(os.environ["NR_HIP_LIB"]) if os.environ.get("NR_HIP_LIB")
-            else Path(__file__).resolve().with_name("libnewsrec_hip.so"))
+LIB_PATH = Path(__file__).resolve().with_name("libnewsrec_hip.so")
 
 NR_OK = 0
 NR_F32 = 0

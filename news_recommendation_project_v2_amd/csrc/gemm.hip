@@ -17,20 +17,6 @@
 // the MFMAs of tile k, one barrier per K tile.
 #include "nr_common.h"
 
-#include <stdlib.h>
-
-#ifndef NR_GEMM_EPI_BLOCK_SYNC
-#define NR_GEMM_EPI_BLOCK_SYNC 0  // A/B build switch: workgroup barriers between epilogue passes
-#endif
-#ifndef NR_GEMM_STAMPS
-#define NR_GEMM_STAMPS 0  // diagnostic build switch: per-block phase stamps (tools/gemm_stamps.py)
-#endif
-#ifndef NR_GEMM_SLAB16
-#define NR_GEMM_SLAB16 0  // A/B build switch: bf16 epilogue slab for pointwise epilogues (measured slower)
-#endif
-#ifndef NR_GEMM_NT_STORE
-#define NR_GEMM_NT_STORE 0  // A/B build switch: non-temporal epilogue stores
-#endif
 
 namespace nr {
 
@@ -295,12 +281,8 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
   // wave still reads operands; after it each wave only touches its own slab,
   // so the passes order their LDS traffic wave-locally (no further workgroup
   // barriers: waves drift apart and their store bursts spread out).
-#if NR_GEMM_EPI_BLOCK_SYNC
-#define NR_EPI_SYNC() __syncthreads()
-#else
   __syncthreads();
 #define NR_EPI_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
-#endif
   const int64_t wcol = n0 + wn * 64;
   const int64_t ocol0 = (EPI == NR_EPI_GEGLU) ? wcol / 2 : wcol;
   float ba = 0.f, bg = 0.f;
@@ -314,78 +296,8 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
     ba = bias[wcol + cl];
     bg = bias[wcol + 32 + cl];
   }
-  // bf16 output of a pointwise epilogue on 16x16 tiles: the slab holds the
-  // final bf16 values (half the LDS round trip).  A lane's 4 rows of one
-  // column are paired with the neighbour lane's column by one DPP swap so each
-  // LDS write is a 2-column bf16 dword; dwords XOR-swizzled by row pair so the
-  // 32 lanes of a write hit distinct banks (COLS 64; 2-way for GEGLU's 32).
-  constexpr bool SLAB16 = MF16 && NR_GEMM_SLAB16 && sizeof(TO) == 2 &&
-                          (EPI == NR_EPI_NONE || EPI == NR_EPI_RELU || EPI == NR_EPI_EXP || EPI == NR_EPI_GELU ||
-                           EPI == NR_EPI_GEGLU || EPI == NR_EPI_RELU_DROPOUT);
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
-    if constexpr (SLAB16) {
-      constexpr int DW = COLS / 2;  // dwords per slab row
-      uint32_t* s32 = reinterpret_cast<uint32_t*>(slab);
-      auto sidx = [](int row, int dw) {
-        const int x = DW == 32 ? ((row >> 1) & 3) << 3 : ((row >> 1) & 1) << 3;
-        return row * DW + (dw ^ x);
-      };
-      const int c16 = lane & 15, r16 = 4 * (lane >> 4);
-      const bool odd = lane & 1;
-      constexpr int NOUT = (EPI == NR_EPI_GEGLU) ? 2 : 4;  // 16-column output groups per wave
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int mi = 4 * pass + i;
-#pragma unroll
-        for (int ni = 0; ni < NOUT; ++ni) {
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            if constexpr (EPI == NR_EPI_GEGLU) {
-              v[r] = (acc[mi][ni][r] + b16[ni]) * gelu_erf(acc[mi][ni + 2][r] + b16[ni + 2]);
-            } else {
-              float x = acc[mi][ni][r] + b16[ni];
-              if constexpr (EPI == NR_EPI_RELU) x = fmaxf(x, 0.f);
-              if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
-                const uint64_t gi = (uint64_t)((m0 + wm * 128 + pass * 64 + 16 * i + r16 + r) * N + wcol + 16 * ni + c16);
-                x = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(x, 0.f) * ea.scale;
-              }
-              if constexpr (EPI == NR_EPI_EXP) x = expf(x);
-              if constexpr (EPI == NR_EPI_GELU) x = gelu_erf(x);
-              v[r] = x;
-            }
-          }
-          // even lane keeps rows 0-1 and receives the odd neighbour's rows 0-1; odd keeps rows 2-3
-          const float x0 = odd ? v[0] : v[2], x1 = odd ? v[1] : v[3];
-          const float y0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x0), 0xB1, 0xF, 0xF, false));
-          const float y1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x1), 0xB1, 0xF, 0xF, false));
-          const float lo0 = odd ? y0 : v[0], hi0 = odd ? v[2] : y0;
-          const float lo1 = odd ? y1 : v[1], hi1 = odd ? v[3] : y1;
-          const int row0 = 16 * i + r16 + (odd ? 2 : 0);
-          const int dw = (16 * ni + (c16 & ~1)) >> 1;
-          const uint32_t p0 = (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)lo0) |
-                              ((uint32_t)__builtin_bit_cast(unsigned short, (__bf16)hi0) << 16);
-          const uint32_t p1 = (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)lo1) |
-                              ((uint32_t)__builtin_bit_cast(unsigned short, (__bf16)hi1) << 16);
-          s32[sidx(row0, dw)] = p0;
-          s32[sidx(row0 + 1, dw)] = p1;
-        }
-      }
-      NR_EPI_SYNC();
-      constexpr int LPR16 = DW / 4;     // lanes per row (16 B each)
-      constexpr int RPI16 = 64 / LPR16;  // rows per wave instruction
-      const int rr16 = lane / LPR16, cd = (lane % LPR16) * 4;
-#pragma unroll
-      for (int it = 0; it < 64 / RPI16; ++it) {
-        const int lr = it * RPI16 + rr16;
-        const int64_t row = m0 + wm * 128 + pass * 64 + lr;
-        const uint4 q = *reinterpret_cast<const uint4*>(s32 + sidx(lr, cd));
-        if (row < M) *reinterpret_cast<uint4*>(C + row * ldc + ocol0 + 2 * cd) = q;
-      }
-      NR_EPI_SYNC();
-      continue;
-    }
     if constexpr (MF16) {
       // 16x16 C/D map: col = lane & 15, row = 4 * (lane >> 4) + r
       const int c16 = lane & 15, r16 = 4 * (lane >> 4);
@@ -489,130 +401,12 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
         TO o[VEC];
 #pragma unroll
         for (int q = 0; q < VEC; ++q) o[q] = to_out<TO>(v[q]);
-#if NR_GEMM_NT_STORE
-        __builtin_nontemporal_store(*reinterpret_cast<const f32x4*>(o), reinterpret_cast<f32x4*>(C + row * ldc + ocol0 + cc));
-#else
         *reinterpret_cast<uint4*>(C + row * ldc + ocol0 + cc) = *reinterpret_cast<const uint4*>(o);
-#endif
       }
     }
     NR_EPI_SYNC();
   }
 #undef NR_EPI_SYNC
-}
-
-template <typename TI, int EPI, typename TO>
-__global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, int64_t K,
-                                                             const TI* __restrict__ A, int64_t lda,
-                                                             const TI* __restrict__ W, int64_t ldw,
-                                                             const float* __restrict__ bias, const TO* R,
-                                                             int64_t ldr, TO* C, int64_t ldc, EpiArgs ea) {
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int64_t n0 = (int64_t)blockIdx.x * G2BN;
-  const int64_t m0 = (int64_t)blockIdx.y * G2BM;
-
-  // glds source pointers: wave issues 4 A + 4 B instructions per K tile, each
-  // filling 8 rows x 128 B; lane l fills (row R0 + l/8, LDS chunk l%8).
-  constexpr int BK = 128 / (int)sizeof(TI), CE = 16 / (int)sizeof(TI);
-  const TI* asrc[4];
-  const TI* bsrc[4];
-  int ldsoff[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int r0 = (wave * 4 + j) * 8;
-    const int row = r0 + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    const int64_t ar = min(m0 + row, M - 1);
-    asrc[j] = A + ar * lda + chunk * CE;
-    bsrc[j] = W + (n0 + row) * ldw + chunk * CE;
-    ldsoff[j] = r0 * 128;
-  }
-  auto issue = [&](int stage, int64_t kt) {
-    unsigned char* sa = smem + stage * G2_STAGE;
-    unsigned char* sb = sa + G2BM * 128;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      __builtin_amdgcn_global_load_lds((g_void*)(asrc[j] + kt * BK), (lds_void*)(sa + ldsoff[j]), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((g_void*)(bsrc[j] + kt * BK), (lds_void*)(sb + ldsoff[j]), 16, 0, 0);
-    }
-  };
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
-
-  const int fr = lane & 31, fh = lane >> 5;
-  int aoff[4], boff[2], asw[4], bsw[2];
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
-    const int row = wm * 128 + mi * 32 + fr;
-    aoff[mi] = row * 128;
-    asw[mi] = (row >> 1) & 7;
-  }
-#pragma unroll
-  for (int ni = 0; ni < 2; ++ni) {
-    const int row = wn * 64 + ni * 32 + fr;
-    boff[ni] = G2BM * 128 + row * 128;
-    bsw[ni] = (row >> 1) & 7;
-  }
-
-  auto compute = [&](int stage) {
-    const unsigned char* s = smem + stage * G2_STAGE;
-    if constexpr (sizeof(TI) == 2) {
-      // 32x32x16 bf16: lane (r, h) holds k = 16ks + 8h + j (chunk 2ks + h) of row r
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int c = 2 * ks + fh;
-        bf16x8 af[4], bfr[2];
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) af[mi] = *reinterpret_cast<const bf16x8*>(s + aoff[mi] + ((c ^ asw[mi]) << 4));
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) bfr[ni] = *reinterpret_cast<const bf16x8*>(s + boff[ni] + ((c ^ bsw[ni]) << 4));
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi], bfr[ni], acc[mi][ni], 0, 0, 0);
-      }
-    } else {
-      // 32x32x2 f32: lane half h covers k = 16h + 4q + t (chunk 4h + q), A and W alike
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c = 4 * fh + q;
-        f32x4 af[4], bfr[2];
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) af[mi] = *reinterpret_cast<const f32x4*>(s + aoff[mi] + ((c ^ asw[mi]) << 4));
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) bfr[ni] = *reinterpret_cast<const f32x4*>(s + boff[ni] + ((c ^ bsw[ni]) << 4));
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni)
-              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[mi][t], bfr[ni][t], acc[mi][ni], 0, 0, 0);
-      }
-    }
-  };
-
-  const int64_t nk = K / BK;
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int64_t kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) issue((int)((kt + 1) & 1), kt + 1);
-    compute((int)(kt & 1));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  gemm256_store<EPI, TO>(acc, smem, wave, lane, wm, wn, m0, n0, M, N, bias, R, ldr, C, ldc, ea);
 }
 
 // ---------------------------------------------------------------------------
@@ -629,7 +423,7 @@ __global__ __launch_bounds__(512, 2) void gemm256_kernel(int64_t M, int64_t N, i
 // prefetch into a stage never overwrites data a wave can still read (each
 // phase ends lgkmcnt(0) + barrier).  Block ids are remapped XCD-aware so the
 // N-tiles that share an A panel run on one XCD (its L2 holds the panel).
-// Same LDS images, swizzle and epilogue as gemm256_kernel.
+// LDS images: rows of 128 B, chunk c of row r at c ^ ((r >> 1) & 7) (T2 swizzle on the DMA source).
 // XCD-aware bijective remap of the launch order: dispatch slot `orig` runs on
 // XCD orig % 8; consecutive output tiles (the N tiles sharing an A panel) are
 // given to one XCD so its L2 holds the panel.
@@ -637,13 +431,6 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
   return (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
 }
-
-#if NR_GEMM_STAMPS
-// Diagnostic build only (-DNR_GEMM_STAMPS=1, tools/gemm_stamps.py): per-block
-// s_memrealtime stamps of the 256x256 kernel's phases, written by lanes 0-7 of
-// wave 0 into a buffer nothing else reads.
-__device__ unsigned long long* g_gemm_stamps = nullptr;
-#endif
 
 // Output tile of remapped id wg (an XCD runs a contiguous run of ids, ~32 at
 // a time).  gm = 1: row-major (the run shares one A panel and reads 32
@@ -806,9 +593,6 @@ __device__ __forceinline__ void gemm256p_body(unsigned char* smem, int64_t m0, i
   // DMAs landed too.
   const int wmu = __builtin_amdgcn_readfirstlane(wm);
   const int64_t nk = K / BK;
-#if NR_GEMM_STAMPS
-  const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
-#endif
   dmaB(0, 0, 0);
   dmaB(1, 0, 0);
   dmaA(0, 0, 0);
@@ -821,9 +605,6 @@ __device__ __forceinline__ void gemm256p_body(unsigned char* smem, int64_t m0, i
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
-#if NR_GEMM_STAMPS
-  const unsigned long long st1 = __builtin_amdgcn_s_memrealtime();
-#endif
   if (wmu == 1) __builtin_amdgcn_s_barrier();  // stagger
   for (int64_t kt = 0; kt < nk; ++kt) {
     const int st = (int)(kt & 1), ns = st ^ 1;
@@ -853,24 +634,7 @@ __device__ __forceinline__ void gemm256p_body(unsigned char* smem, int64_t m0, i
   }
   if (wmu == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
 #undef NR_PHASE_SYNC_MMA
-#if NR_GEMM_STAMPS
-  const unsigned long long st2 = __builtin_amdgcn_s_memrealtime();
-#endif
   gemm256_store<EPI, TO, MF16>(acc, smem, wave, lane, wm, wn, m0, n0, M, N, bias, R, ldr, C, ldc, ea);
-#if NR_GEMM_STAMPS
-  const unsigned long long st3 = __builtin_amdgcn_s_memrealtime();
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const unsigned long long st4 = __builtin_amdgcn_s_memrealtime();
-  if (wave == 0 && lane < 8 && g_gemm_stamps) {
-    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20); // XCC_ID
-    const unsigned long long v[8] = {st0, st1, st2, st3, st4, hw, xcc, (unsigned long long)(m0 << 20 | n0)};
-    unsigned long long x = v[0];
-#pragma unroll
-    for (int i = 1; i < 8; ++i) x = lane == i ? v[i] : x;
-    g_gemm_stamps[(blockIdx.y * gridDim.x + blockIdx.x) * 8 + lane] = x;
-  }
-#endif
 }
 
 template <typename TI, int EPI, typename TO, bool MF16 = false>
@@ -916,370 +680,6 @@ __global__ __launch_bounds__(512, 2) void gemm256p_group_kernel(GemmGroup g) {
   gemm256p_body<TI, NR_EPI_NONE, TO, MF16>(smem, (int64_t)(local / nx) * G2BM, (int64_t)(local % nx) * G2BN, g.M[p],
                                            g.N[p], g.K[p], (const TI*)g.A[p], g.lda[p], (const TI*)g.W[p], g.ldw[p],
                                            nullptr, nullptr, 0, (TO*)g.C[p], g.ldc[p], EpiArgs{0, 0, 1.f});
-}
-
-// ---------------------------------------------------------------------------
-// Persistent bf16 variant (16x16x32 MFMA tiles): one 512-thread workgroup per
-// CU walks its share of the 256x256 output tiles.  The main loop is
-// gemm256p_kernel's; what changes is the tile boundary: as soon as a tile's K
-// loop ends, the NEXT tile's prologue DMAs (K tile 0, and K tile 1's B halves)
-// are issued into the two operand stages, and the finished tile's epilogue
-// runs from a separate 32 KiB LDS region (a 4 KiB, 16-row slab per wave) while
-// they fly.  With one workgroup per CU (234 VGPRs, 160 KiB LDS) the prologue
-// latency and the epilogue (GEGLU's erf, stores) would otherwise be exposed
-// once per tile: at K = 512-1024 that is 10-20 % of a tile.  Tiles are split
-// into 8 contiguous ranges, one per XCD (workgroups b = x mod 8), so the tiles
-// an XCD runs concurrently share A panels in its L2.
-template <int EPI, typename TO>
-__device__ __forceinline__ void epi16_store(const f32x4 (&acc)[8][4], float* slab, int lane, int wm, int wn,
-                                            int64_t m0, int64_t n0, int64_t M, int64_t N,
-                                            const float (&b16)[4], const TO* R, int64_t ldr, TO* C,
-                                            int64_t ldc, const EpiArgs& ea) {
-  constexpr int COLS = (EPI == NR_EPI_GEGLU) ? 32 : 64;
-  constexpr int VEC = 16 / (int)sizeof(TO);
-  constexpr int LPR = COLS / VEC;
-  constexpr int RPI = 64 / LPR;
-  constexpr int ITS = 16 / RPI;
-  const int64_t wcol = n0 + wn * 64;
-  const int64_t ocol0 = (EPI == NR_EPI_GEGLU) ? wcol / 2 : wcol;
-  const int c16 = lane & 15, r16 = 4 * (lane >> 4);
-  // slab [16][COLS] f32; column bit 4 flipped on rows 4-7 / 12-15 so the two
-  // 16-lane halves of a 32-lane store group hit different banks
-  auto sidx = [](int row, int col) { return row * COLS + (col ^ ((row & 4) << 2)); };
-  const int rr = lane / LPR, cc = (lane % LPR) * VEC;
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = r16 + r;
-      if constexpr (EPI == NR_EPI_GEGLU) {
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-          slab[sidx(row, 16 * ni + c16)] = (acc[mi][ni][r] + b16[ni]) * gelu_erf(acc[mi][ni + 2][r] + b16[ni + 2]);
-      } else {
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          float v = acc[mi][ni][r] + b16[ni];
-          if constexpr (EPI == NR_EPI_RELU) v = fmaxf(v, 0.f);
-          if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
-            const uint64_t gi = (uint64_t)((m0 + wm * 128 + mi * 16 + row) * N + wcol + 16 * ni + c16);
-            v = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(v, 0.f) * ea.scale;
-          }
-          if constexpr (EPI == NR_EPI_EXP) v = expf(v);
-          if constexpr (EPI == NR_EPI_GELU) v = gelu_erf(v);
-          slab[sidx(row, 16 * ni + c16)] = v;
-        }
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < ITS; ++it) {
-      const int lr = it * RPI + rr;
-      const int64_t row = m0 + wm * 128 + mi * 16 + lr;
-      float v[VEC];
-#pragma unroll
-      for (int q = 0; q < VEC; q += 4) {
-        const float4 f = *reinterpret_cast<const float4*>(slab + sidx(lr, cc + q));
-        v[q] = f.x; v[q + 1] = f.y; v[q + 2] = f.z; v[q + 3] = f.w;
-      }
-      if constexpr (EPI == NR_EPI_SOFTMAX64) {
-        float m = v[0];
-#pragma unroll
-        for (int q = 1; q < VEC; ++q) m = fmaxf(m, v[q]);
-#pragma unroll
-        for (int o = 1; o < LPR; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-        float sum = 0.f;
-#pragma unroll
-        for (int q = 0; q < VEC; ++q) { v[q] = expf(v[q] - m); sum += v[q]; }
-#pragma unroll
-        for (int o = 1; o < LPR; o <<= 1) sum += __shfl_xor(sum, o, 64);
-        const float inv = 1.0f / sum;
-#pragma unroll
-        for (int q = 0; q < VEC; ++q) v[q] *= inv;
-      }
-      if (row < M) {
-        if constexpr (EPI == NR_EPI_RESADD || EPI == NR_EPI_DRELU) {
-          const uint4 rv = *reinterpret_cast<const uint4*>(R + row * ldr + ocol0 + cc);
-          float rf[VEC];
-          if constexpr (sizeof(TO) == 4) {
-            rf[0] = __uint_as_float(rv.x); rf[1] = __uint_as_float(rv.y);
-            rf[2] = __uint_as_float(rv.z); rf[3] = __uint_as_float(rv.w);
-          } else {
-            const uint32_t w4[4] = {rv.x, rv.y, rv.z, rv.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) { rf[2 * q] = bf16_lo(w4[q]); rf[2 * q + 1] = bf16_hi(w4[q]); }
-          }
-#pragma unroll
-          for (int q = 0; q < VEC; ++q) {
-            if constexpr (EPI == NR_EPI_RESADD) v[q] += rf[q];
-            else v[q] = rf[q] > 0.f ? v[q] * ea.scale : 0.f;
-          }
-        }
-        TO o[VEC];
-#pragma unroll
-        for (int q = 0; q < VEC; ++q) o[q] = to_out<TO>(v[q]);
-        *reinterpret_cast<uint4*>(C + row * ldc + ocol0 + cc) = *reinterpret_cast<const uint4*>(o);
-      }
-    }
-  }
-}
-
-constexpr int G2_EPI_SLAB = 16 * 64 * 4;  // bytes per wave
-
-template <int EPI, typename TO>
-__global__ __launch_bounds__(512, 2) void gemm256pp_kernel(int64_t M, int64_t N, int64_t K,
-                                                           const __bf16* __restrict__ A, int64_t lda,
-                                                           const __bf16* __restrict__ W, int64_t ldw,
-                                                           const float* __restrict__ bias, const TO* R,
-                                                           int64_t ldr, TO* C, int64_t ldc, EpiArgs ea,
-                                                           int tiles_n, int n_tiles) {
-  typedef __bf16 TI;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE + 8 * G2_EPI_SLAB];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int wmu = __builtin_amdgcn_readfirstlane(wm);
-  float* slab = reinterpret_cast<float*>(smem + 2 * G2_STAGE + wave * G2_EPI_SLAB);
-
-  // tile schedule: XCD group x = blockIdx % 8 owns a contiguous range of tiles
-  const int G = (int)gridDim.x;
-  int t, t_end, t_step;
-  if (G % 8 == 0 && G >= 8) {
-    const int x = (int)blockIdx.x & 7, li = (int)blockIdx.x >> 3;
-    const int q = n_tiles >> 3, r = n_tiles & 7;
-    const int lo = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-    t = lo + li;
-    t_end = lo + q + (x < r ? 1 : 0);
-    t_step = G >> 3;
-  } else {
-    t = (int)blockIdx.x;
-    t_end = n_tiles;
-    t_step = G;
-  }
-  if (t >= t_end) return;  // workgroup-uniform
-
-  constexpr int BK = 64, CE = 8;
-  // DMA addressing recomputed per issue from tile-uniform m0/n0 and a few
-  // lane constants (keeps ~16 VGPRs of 64-bit pointers out of the persistent
-  // loop).  Lane l of wave w fills row 128h + 16w + 8j + l/8, 16-B chunk
-  // (l & 7) ^ ((4j + l/16) & 7) of the swizzled image (= chunk ^ (row>>1 & 7)).
-  int64_t tm0 = 0, tn0 = 0;
-  const int rl = 16 * wave + (lane >> 3);
-  auto cj = [&](int j) { return (lane & 7) ^ ((4 * j + (lane >> 4)) & 7); };
-  auto dmaA = [&](int h, int stage, int64_t kt) {
-    unsigned char* sa = smem + stage * G2_STAGE;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t row = min(tm0 + 128 * h + 8 * j + rl, M - 1);
-      const TI* src = A + row * lda + cj(j) * CE + kt * BK;
-      __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(sa + (128 * h + 16 * wave + 8 * j) * 128), 16, 0, 0);
-    }
-  };
-  auto dmaB = [&](int h, int stage, int64_t kt) {
-    unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const TI* src = W + (tn0 + 128 * h + 8 * j + rl) * ldw + cj(j) * CE + kt * BK;
-      __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(sb + (128 * h + 16 * wave + 8 * j) * 128), 16, 0, 0);
-    }
-  };
-  auto setup = [&](int tile) {
-    tn0 = (int64_t)(tile % tiles_n) * G2BN;
-    tm0 = (int64_t)(tile / tiles_n) * G2BM;
-  };
-  const int64_t nk = K / BK;
-  auto prologue = [&]() {
-    dmaB(0, 0, 0);
-    dmaB(1, 0, 0);
-    dmaA(0, 0, 0);
-    dmaA(1, 0, 0);
-    if (nk > 1) {
-      dmaB(0, 1, 1);
-      dmaB(1, 1, 1);
-    }
-  };
-
-  // fragment addresses: 16x16x32 tiles; the swizzle term (row >> 1) & 7 is
-  // the same for every tile of a lane (tiles are 16 rows apart)
-  const int c16 = lane & 15;
-  const int sw = (c16 >> 1) & 7;
-  const int abase = (wm * 128 + c16) * 128;
-  const int bbase = G2BM * 128 + (wn * 64 + c16) * 128;
-  const int cf0 = ((0 + (lane >> 4)) ^ sw) << 4, cf1 = ((4 + (lane >> 4)) ^ sw) << 4;
-  typedef f32x4 frag_t;
-  frag_t fa[4][2], fb0[2][2], fb1[2][2];
-  f32x4 acc[8][4];
-  auto readA = [&](int stage, int qm) {
-    const unsigned char* sp = smem + stage * G2_STAGE + abase + qm * 4 * 2048;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      fa[i][0] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf0);
-      fa[i][1] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf1);
-    }
-  };
-  auto readB = [&](int stage, int qn, frag_t (&fb)[2][2]) {
-    const unsigned char* sp = smem + stage * G2_STAGE + bbase + qn * 2 * 2048;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      fb[j][0] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf0);
-      fb[j][1] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf1);
-    }
-  };
-  auto mma = [&](int qm, int qn, const frag_t (&fb)[2][2]) {
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 * qm + i][2 * qn + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8, fa[i][f]), __builtin_bit_cast(bf16x8, fb[j][f]), acc[4 * qm + i][2 * qn + j],
-              0, 0, 0);
-  };
-#define NR_PHASE_SYNC_MMA(QM, NI, FB)                   \
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
-  __builtin_amdgcn_sched_barrier(0);                   \
-  __builtin_amdgcn_s_barrier();                        \
-  __builtin_amdgcn_s_setprio(1);                       \
-  mma(QM, NI, FB);                                     \
-  __builtin_amdgcn_s_setprio(0);                       \
-  __builtin_amdgcn_s_barrier();
-
-  // The epilogue of a full tile issues exactly EPI_STORES 16-byte stores per
-  // wave AFTER the next tile's prologue DMAs; vmcnt retires loads, stores and
-  // LDS-DMA in issue order (MI355X_MICROARCH: one counter, issue order), so
-  // vmcnt(EPI_STORES) means "the prologue has landed" while the previous
-  // tile's stores drain under this tile's MFMAs.  After a ragged (M-tail)
-  // tile fewer stores were issued: drain everything.
-  constexpr int EPI_COLS = (EPI == NR_EPI_GEGLU) ? 32 : 64;
-  constexpr int EPI_STORES = 8 * (16 / (64 / (EPI_COLS / (16 / (int)sizeof(TO)))));
-  static_assert(EPI_STORES == 8 || EPI_STORES == 16 || EPI_STORES == 32, "epilogue store count");
-  setup(t);
-  prologue();
-  bool drain_all = true;
-  while (true) {
-    if (drain_all) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (EPI_STORES == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if constexpr (EPI_STORES == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (wmu == 1) __builtin_amdgcn_s_barrier();  // stagger the wave groups
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[mi][ni][r] = 0.f;
-    for (int64_t kt = 0; kt < nk; ++kt) {
-      const int st = (int)(kt & 1), ns = st ^ 1;
-      const bool pre1 = kt + 1 < nk, pre2 = kt + 2 < nk;
-      readA(st, 0);
-      readB(st, 0, fb0);
-      if (pre1) dmaA(0, ns, kt + 1);
-      NR_PHASE_SYNC_MMA(0, 0, fb0)
-      readB(st, 1, fb1);
-      if (pre1) dmaA(1, ns, kt + 1);
-      NR_PHASE_SYNC_MMA(0, 1, fb1)
-      readA(st, 1);
-      if (pre2) dmaB(0, st, kt + 2);
-      NR_PHASE_SYNC_MMA(1, 1, fb1)
-      if (pre2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (pre2) dmaB(1, st, kt + 2);
-      __builtin_amdgcn_s_setprio(1);
-      mma(1, 0, fb0);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_s_barrier();
-    }
-    if (wmu == 0) __builtin_amdgcn_s_barrier();  // re-align the groups: every stage read is retired
-    const int64_t n0 = tn0, m0 = tm0;
-    const int tn = t + t_step;
-    const bool more = tn < t_end;
-    // everything the epilogue reads from memory is loaded BEFORE the next
-    // tile's DMAs: a later load's wait would also wait for the (older) DMAs
-    float b16[4] = {0.f, 0.f, 0.f, 0.f};
-    if (bias) {
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) b16[ni] = bias[n0 + wn * 64 + 16 * ni + (lane & 15)];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (more) {  // next tile's operands fly while this tile's epilogue runs
-      setup(tn);
-      prologue();
-    }
-    epi16_store<EPI, TO>(acc, slab, lane, wm, wn, m0, n0, M, N, b16, R, ldr, C, ldc, ea);
-    if (!more) break;
-    drain_all = m0 + G2BM > M;  // ragged tile: some stores were skipped
-    t = tn;
-  }
-#undef NR_PHASE_SYNC_MMA
-}
-
-template <typename TO>
-static int launch_gemm256_pp(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
-                             const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
-                             void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
-  const int tiles_n = (int)(N / G2BN);
-  const int64_t tiles = (int64_t)tiles_n * ((M + G2BM - 1) / G2BM);
-  if (tiles > (1ll << 30)) {
-    set_error("nr_gemm: too many tiles");
-    return NR_ERR_UNSUPPORTED;
-  }
-  const int nt = (int)tiles;
-  static int n_cu = 0;
-  if (!n_cu) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    n_cu = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-               ? prop.multiProcessorCount : 256;
-    n_cu = n_cu / 8 * 8;
-    if (n_cu < 8) n_cu = 8;
-  }
-  const dim3 grid((unsigned)(nt < n_cu ? nt : n_cu));
-  const __bf16* a = (const __bf16*)A;
-  const __bf16* w = (const __bf16*)W;
-  const TO* r = (const TO*)R;
-  TO* c = (TO*)C;
-#define NR_PP(E) hipLaunchKernelGGL((gemm256pp_kernel<E, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea, tiles_n, nt)
-  switch (epi) {
-    case NR_EPI_NONE: NR_PP(NR_EPI_NONE); break;
-    case NR_EPI_RELU: NR_PP(NR_EPI_RELU); break;
-    case NR_EPI_EXP: NR_PP(NR_EPI_EXP); break;
-    case NR_EPI_GEGLU: NR_PP(NR_EPI_GEGLU); break;
-    case NR_EPI_RESADD: NR_PP(NR_EPI_RESADD); break;
-    case NR_EPI_GELU: NR_PP(NR_EPI_GELU); break;
-    case NR_EPI_RELU_DROPOUT: NR_PP(NR_EPI_RELU_DROPOUT); break;
-    case NR_EPI_DRELU: NR_PP(NR_EPI_DRELU); break;
-    case NR_EPI_SOFTMAX64: NR_PP(NR_EPI_SOFTMAX64); break;
-    default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
-  }
-#undef NR_PP
-  NR_CHECK_LAUNCH("nr_gemm");
-  return NR_OK;
-}
-
-template <typename TI, typename TO>
-static int launch_gemm256_v1(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
-                          const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
-                          void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
-  dim3 grid((unsigned)(N / G2BN), (unsigned)((M + G2BM - 1) / G2BM));
-  const TI* a = (const TI*)A;
-  const TI* w = (const TI*)W;
-  const TO* r = (const TO*)R;
-  TO* c = (TO*)C;
-  switch (epi) {
-    case NR_EPI_NONE: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_NONE, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
-    case NR_EPI_RELU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_RELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
-    case NR_EPI_EXP: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_EXP, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
-    case NR_EPI_GEGLU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_GEGLU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
-    case NR_EPI_RESADD: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_RESADD, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
-    case NR_EPI_GELU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_GELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
-    case NR_EPI_RELU_DROPOUT: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_RELU_DROPOUT, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
-    case NR_EPI_DRELU: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_DRELU, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
-    case NR_EPI_SOFTMAX64: hipLaunchKernelGGL((gemm256_kernel<TI, NR_EPI_SOFTMAX64, TO>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea); break;
-    default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
-  }
-  NR_CHECK_LAUNCH("nr_gemm");
-  return NR_OK;
 }
 
 template <typename TI, typename TO>
@@ -1332,26 +732,18 @@ static int launch_gemm256_p16(int epi, int64_t M, int64_t N, int64_t K, const vo
   return NR_OK;
 }
 
+// bf16: 16x16x32 MFMA tiles (5-8 % faster than 32x32x16 on the pooler shapes,
+// profiles/round1/s2/gemm_mf16_vs_mf32.txt); f32: the exact-f32 32x32x2 tiles.
+// Tile order: groups of 4 M-tiles (tile_of; profiles/round1/s5/gemm_group).
+constexpr int kGemmGroupM = 4;
+
 template <typename TI, typename TO>
 static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                           const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
                           void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
-  static const bool v1 = getenv("NR_GEMM_V1") != nullptr;  // A/B switch: the 2-stage glds kernel
-  // bf16 default: 16x16x32 MFMA tiles (5-8 % faster than 32x32x16 on the pooler shapes,
-  // profiles/round1/s2/gemm_mf16_vs_mf32.txt); NR_GEMM_MF32=1 selects the 32x32x16 tiles
-  static const bool mf16 = getenv("NR_GEMM_MF32") == nullptr;
-  if (v1) return launch_gemm256_v1<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
-  // persistent variant: opt-in (NR_GEMM_PERSIST=1) until its register pressure is fixed: its
-  // spill reloads in the epilogue wait on the next tile's DMAs
-  static const bool persist = getenv("NR_GEMM_PERSIST") != nullptr;
-  // tile order (tile_of): NR_GEMM_GROUP_M overrides the default M-tile group
-  static const int group_m = getenv("NR_GEMM_GROUP_M") ? atoi(getenv("NR_GEMM_GROUP_M")) : 4;
   EpiArgs eg = ea;
-  eg.group_m = group_m;
-  if constexpr (sizeof(TI) == 2) {
-    if (mf16 && persist) return launch_gemm256_pp<TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
-    if (mf16) return launch_gemm256_p16<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
-  }
+  eg.group_m = kGemmGroupM;
+  if constexpr (sizeof(TI) == 2) return launch_gemm256_p16<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
   return launch_gemm256_p<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
 }
 
@@ -1410,11 +802,10 @@ int gemm_dispatch_ex(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N,
   NR_CHECK_ARG((M + GBM - 1) / GBM <= 65535, "nr_gemm: M too large (> 8.3M rows)");
   // 256x256 glds kernel when the shape allows (every pooler GEMM); the
   // 128x128 register-staged kernel covers N % 256 != 0 and unaligned outputs.
-  static const bool force_small = getenv("NR_GEMM_SMALL_TILE") != nullptr;  // A/B switch for profiling
   const int64_t vo = dtype_out == NR_F32 ? 4 : 8;  // the LDS-staged epilogue stores 16 B per lane
   const bool aligned_out = ((uintptr_t)C & 15) == 0 && ldc % vo == 0 &&
                            ((epi != NR_EPI_RESADD && epi != NR_EPI_DRELU) || (((uintptr_t)R & 15) == 0 && ldr % vo == 0));
-  const bool big = (N % G2BN == 0) && aligned_out && !force_small;
+  const bool big = (N % G2BN == 0) && aligned_out;
   if (epi == NR_EPI_SOFTMAX64 && !big) {
     set_error("nr_gemm: SOFTMAX64 needs N %% 256 == 0 and 16-byte aligned output rows");
     return NR_ERR_UNSUPPORTED;
@@ -1510,8 +901,3 @@ extern "C" int nr_gemm_grouped(int dtype_in, int dtype_out, int n, const int64_t
   return NR_OK;
 }
 
-#if NR_GEMM_STAMPS
-extern "C" int nr_debug_gemm_stamps(void* buf) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(nr::g_gemm_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
-}
-#endif

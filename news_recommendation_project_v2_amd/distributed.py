@@ -55,17 +55,27 @@ class ShardedTable:
         n = engine.hist_src.shape[0]
         self.rows = shard_rows(n, world)
         width = 2048 if engine.pooler == "final" else 1024
-        if self.rows * world != n:  # pad the source so every rank transforms `rows` rows
-            pad = torch.zeros((self.rows * world - n, engine.hist_src.shape[1]), dtype=engine.hist_src.dtype,
-                              device=engine.device)
-            engine.hist_src = torch.cat([engine.hist_src, pad]).contiguous()
+        # the engine's source table is left as it is; when N is not a multiple of
+        # world the LAST rank's slice is short and it transforms a zero-padded copy
+        # of just that slice (every rank contributes `rows` rows to the gather)
+        self.src = engine.hist_src
+        lo, hi = rank * self.rows, min((rank + 1) * self.rows, n)
+        self.lo = lo
+        if hi - lo != self.rows:
+            part = torch.zeros((self.rows, engine.hist_src.shape[1]), dtype=engine.hist_src.dtype,
+                               device=engine.device)
+            if hi > lo:
+                part[:hi - lo] = engine.hist_src[lo:hi]
+            self.src, self.lo = part.contiguous(), 0
         self.full = torch.empty((self.rows * world, width), dtype=engine.dtype, device=engine.device)
-        self.local = self.full[rank * self.rows:(rank + 1) * self.rows] if world == 1 else \
+        # RCCL all-gathers in place (the rank's input is its own slice of the output);
+        # gloo needs a separate host-staged input
+        in_place = world == 1 or not _host_staged(group)
+        self.local = self.full[rank * self.rows:(rank + 1) * self.rows] if in_place else \
             torch.empty((self.rows, width), dtype=engine.dtype, device=engine.device)
 
     def build(self) -> torch.Tensor:
-        sl = slice(self.rank * self.rows, (self.rank + 1) * self.rows)
-        self.eng.transform(rows=sl, out=self.local)
+        self.eng.transform(rows=slice(self.lo, self.lo + self.rows), out=self.local, src=self.src)
         if self.world > 1:
             if _host_staged(self.group) and self.local.is_cuda:
                 # gloo moves host memory: stage the slices through the host as raw bytes

@@ -70,9 +70,11 @@ class PoolScoreEngine:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self._ws
 
-    def transform(self, rows: Optional[slice] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Per-news pooler table for hist_src[rows] (default: all rows)."""
-        src = self.hist_src if rows is None else self.hist_src[rows]
+    def transform(self, rows: Optional[slice] = None, out: Optional[torch.Tensor] = None,
+                  src: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Per-news pooler table for src[rows] (default: all rows of hist_src)."""
+        src = self.hist_src if src is None else src
+        src = src if rows is None else src[rows]
         ws = self._workspace(src.shape[0])
         if self.pooler == "final":
             return ops.final_attn_transform(src, self.weights, out=out, workspace=ws)

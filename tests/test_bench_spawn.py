@@ -1,0 +1,28 @@
+"""bench.py --gpus N without a torch.distributed launcher must start N ranks
+itself (before any GPU call) and report n_gpus = N.  The --dry-run mode runs
+that launch, the strong-scaling partition, the table all-gather and the
+max-over-ranks reduction over gloo on the CPU."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_spawns_ranks(world):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", str(world), "--dry-run", "--impressions", "1500"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == world and res["scaling"] == "strong"
+    assert res["partition"][0] == 0 and res["partition"][-1] == 1500 and len(res["partition"]) == world + 1
+    assert res["impressions_total"] == 1500
+    assert res["candidates_total"] == res["candidates_expected"]
+    assert res["allgather_ok"]

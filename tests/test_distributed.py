@@ -26,8 +26,9 @@ class StubEngine:
         self.device = table.device
         self.hist_table = None
 
-    def transform(self, rows=None, out=None):
-        src = self.hist_src if rows is None else self.hist_src[rows]
+    def transform(self, rows=None, out=None, src=None):
+        src = self.hist_src if src is None else src
+        src = src if rows is None else src[rows]
         res = src * 2 + 1
         if out is not None:
             out.copy_(res)
@@ -52,7 +53,8 @@ def _worker(rank, world, port, n_news, q):
         eng = StubEngine(table.clone())
         st = ShardedTable(eng, rank, world)
         full = st.build()
-        ok_table = torch.equal(full[:n_news], table * 2 + 1) and eng.hist_table is full
+        ok_table = (torch.equal(full[:n_news], table * 2 + 1) and eng.hist_table is full
+                    and torch.equal(eng.hist_src, table))  # the engine's source table is not modified
         local = torch.arange(rank * 10, rank * 10 + 3 + rank, dtype=torch.float32)
         allsc = gather_scores(local, world)
         want = torch.cat([torch.arange(r * 10, r * 10 + 3 + r, dtype=torch.float32) for r in range(world)])
