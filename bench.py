@@ -30,9 +30,10 @@ Also reported in the same JSON line:
                 measured random-row gather ceiling of the microarch guide
   cpu_baseline  the oracle (the reference algorithm restated on PyTorch CPU:
                 padded batches of 128, pooler per padded slot, per-impression
-                cosine loop) on all affinity cores of this host, on the first
-                1,000 impressions of a MIND-small-shaped set (configs[0]), for
-                both poolers; ``--cpu-10k`` adds 10,000
+                cosine loop) on this host's CPU share (all affinity cores, or
+                OMP_NUM_THREADS where the pool declares a per-GPU share), on the
+                first 1,000 impressions of a MIND-small-shaped set (configs[0]),
+                for both poolers; ``--cpu-10k`` adds 10,000
   extra         the FinalAttention pooler, f32, per-stage times, AUC of the GPU
                 path vs the CPU reference on the config-1 sample, MIND-large
                 test shape, Zipf ids, device metrics, PCIe costs, config 5
@@ -282,7 +283,12 @@ def cpu_leg(args, dev) -> tuple:
     from news_recommendation_project_v2_amd import evaluation
     from news_recommendation_project_v2_amd.engine import PoolScoreEngine
     from oracle import data_ref, pool_ref
-    cores = len(os.sched_getaffinity(0))
+    # The GPU pool gives each GPU a CPU share and says so in OMP_NUM_THREADS (16 per GPU)
+    # while the affinity mask lists every CPU of the host (256): at 256 threads on that
+    # share the restatement ran 74 cand/s against ~3k at 16 (profiles/round2/cpu_threads.txt).
+    # Use the share when the pool declares one, else the whole affinity set.
+    affinity = len(os.sched_getaffinity(0))
+    cores = min(affinity, int(os.environ.get("OMP_NUM_THREADS") or affinity))
     torch.set_num_threads(cores)
     n_news, n_imp_full = synthetic.SHAPES[args.cpu_shape]
     full = synthetic.mind_impressions(n_news, n_imp_full, seed=1234)
@@ -322,7 +328,7 @@ def cpu_leg(args, dev) -> tuple:
             "sample": f"first {head['impressions']} impressions ({head['candidates']} candidates) of the seeded "
                       f"{args.cpu_shape}-shaped set (configs[0]), {args.pooler} pooler (headline), f32, "
                       f"{head['seconds']}s on {cores} threads of {cpu_model()}; both poolers in by_pooler",
-            "by_pooler": out}
+            "by_pooler": out, "affinity_cpus": affinity}
     return base, parity
 
 

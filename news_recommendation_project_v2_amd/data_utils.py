@@ -29,9 +29,14 @@ def load_dataset(data_dir: Path, news_dataset: NewsDataset, num_samples: Optiona
     """Read ``{data_dir}/processed/{split}/behaviors.parquet`` and ``news_text.parquet``
     (layout written by the reference's ``store_processed_data``, data_utils.py:442-455).
 
-    Returns ``(behaviors, feature_dict)`` like data_utils.py:114-122.  Entity
+    Returns ``(behaviors, feature_dict)`` like data_utils.py:114-122, including
+    the per-news mean entity embeddings of ``entity_embeds.pkl`` (:40-42,
+    :56-99; a news with no known entity gets the 100-d zero vector).  Entity
     embeddings and category maps are optional here (they are not read by the
-    embed -> pool -> score path); missing files give empty dicts.
+    embed -> pool -> score path); missing files leave those keys out.  The
+    WITH_HISTORY / WITHOUT_HISTORY filter and the ``behaviors.sample`` draw
+    are the reference's (:100-107), so the same ``random_state`` generator
+    picks the same impressions (tests/test_dataset_golden.py).
     """
     import pandas as pd
 
@@ -46,6 +51,19 @@ def load_dataset(data_dir: Path, news_dataset: NewsDataset, num_samples: Optiona
     sub_cat_dict = _json(Path(data_dir) / "sub_categories.json")
 
     feats: dict[str, Any] = {"news_text_dict": news_text["news_text"].to_dict()}
+    ent_path = base / "entity_embeds.pkl"
+    if ent_path.is_file():
+        import joblib  # the reference's own format for this file (data_utils.py:40-42)
+        entity_embeds = joblib.load(ent_path)
+
+        def mean_entity(x) -> np.ndarray:
+            embeds = [] if pd.isnull(x) else [entity_embeds[e["WikidataId"]] for e in json.loads(x)
+                                              if e["WikidataId"] in entity_embeds]
+            return np.mean(embeds if embeds else [[0] * 100], axis=0)
+
+        for col, key in (("Title Entities", "news_title_entity"), ("Abstract Entities", "news_abstract_entity")):
+            if col in news_text:
+                feats[key] = {k: mean_entity(v) for k, v in news_text[col].to_dict().items()}
     if "Title" in news_text:
         feats["news_title_dict"] = {k: "News Title: " + v for k, v in news_text["Title"].to_dict().items()}
     if "Abstract" in news_text:
@@ -77,9 +95,13 @@ def split_impressions_and_history(impressions: Sequence[str], history: Sequence[
     assert len(impressions) > 0, "No Impressions given"
     from .native import split_behaviors
     res = split_behaviors(impressions, history)  # C++ parser (libnewsrec_host.so)
-    if res is not None:
-        return res
-    return split_impressions_and_history_py(impressions, history)
+    if res is None:
+        res = split_impressions_and_history_py(impressions, history)
+    if len(res["history_len_list"]) == 0:
+        # the reference builds row 1 of history_rev_ind_array with np.concatenate over the
+        # history rows (data_utils.py:225-227), which raises when no row has a history
+        raise ValueError("need at least one array to concatenate")
+    return res
 
 
 def split_impressions_and_history_py(impressions: Sequence[str], history: Sequence[Optional[str]]) -> dict[str, Any]:
@@ -403,6 +425,10 @@ def train_batch_csr(conn, rows, maxlen: Optional[int] = None):
     uniq, rev = np.unique(allidx, return_inverse=True)
     ids = ",".join(str(int(i) + 1) for i in uniq)
     res = conn.execute(f"SELECT data FROM tensors WHERE id IN ({ids}) ORDER BY id;").fetchall()
+    if len(res) != len(uniq):
+        # the reference fails on first_res[...] with an IndexError here; every index
+        # below addresses rows of `last`, and the device gathers do not bound-check
+        raise IndexError(f"token DB returned {len(res)} rows for {len(uniq)} requested news ids")
     last = torch.stack([t[min(len(t), maxlen) - 1] for t in (read_token_blob(r[0]) for r in res)])
     Hs = int(lens.sum())
     B = len(pos)

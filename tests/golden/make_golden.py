@@ -361,7 +361,117 @@ def gen_train(dmh, du, mu):
     np.savez_compressed(HERE / "train_step.npz", weight_seed=1234, **out)
 
 
-GENERATORS = ("split", "rank", "final", "latent", "encoder", "token_attn", "train")
+def dataset_inputs(seed: int = 31, n_news: int = 60, n_rows: int = 240):
+    """A tiny processed MIND split in the reference's on-disk layout
+    (store_processed_data, data_utils.py:442-455): behaviours rows (some with
+    no history), news text / title / abstract (some missing) / category /
+    subcategory / entity JSON columns, the WikidataId -> 100-d entity table
+    (some ids unknown), and the category maps."""
+    rng = np.random.default_rng(seed)
+    news = [f"N{i}" for i in range(1, n_news + 1)]
+    cats, subs = ["news", "sports", "finance", "travel", "video"], [f"sub{i}" for i in range(7)]
+    qids = [f"Q{i}" for i in range(40)]
+    known = qids[:30]
+
+    def ents():
+        if rng.random() < 0.25:
+            return None
+        return "[" + ", ".join('{"Label": "x", "WikidataId": "%s"}' % q for q in rng.choice(qids, int(rng.integers(1, 4)))) + "]"
+
+    news_cols = {
+        "NewsID": news,
+        "Category": [cats[int(i)] for i in rng.integers(0, len(cats), n_news)],
+        "SubCategory": [subs[int(i)] for i in rng.integers(0, len(subs), n_news)],
+        "Title": [f"title {i} " + "w" * int(rng.integers(1, 9)) for i in range(n_news)],
+        "Abstract": [None if rng.random() < 0.2 else f"abstract {i}" for i in range(n_news)],
+        "Title Entities": [ents() for _ in range(n_news)],
+        "Abstract Entities": [ents() for _ in range(n_news)],
+    }
+    news_cols["news_text"] = [f"Title: {t}" for t in news_cols["Title"]]
+    hist, imps = [], []
+    for i in range(n_rows):
+        h = rng.choice(news, int(rng.integers(1, 9)))
+        hist.append(None if rng.random() < 0.3 else " ".join(h))
+        c = rng.choice(news, int(rng.integers(2, 9)))
+        lab = (rng.random(len(c)) < 0.3).astype(int)
+        imps.append(" ".join(f"{n}-{int(y)}" for n, y in zip(c, lab)))
+    entity = {q: rng.standard_normal(100).tolist() for q in known}
+    return news_cols, {"ImpressionID": np.arange(1, n_rows + 1), "History": hist, "Impressions": imps}, entity, \
+        {c: i for i, c in enumerate(cats)}, {s: i for i, s in enumerate(subs)}
+
+
+def write_dataset(root: Path, split: str, news_cols, beh_cols, entity, cat_map, sub_map) -> None:
+    import joblib
+    import pandas as pd
+    d = root / "processed" / split
+    d.mkdir(parents=True, exist_ok=True)
+    pd.DataFrame(news_cols).to_parquet(d / "news_text.parquet")
+    pd.DataFrame(beh_cols).to_parquet(d / "behaviors.parquet")
+    joblib.dump(entity, d / "entity_embeds.pkl")
+    (root / "categories.json").write_text(__import__("json").dumps(cat_map))
+    (root / "sub_categories.json").write_text(__import__("json").dumps(sub_map))
+
+
+DATASET_CASES = [  # (split, num_samples, subset) run in this order on ONE rng, as scripts/eval.py:38-52 does
+    ("MINDsmall_train", 50, "WITH_HISTORY"),
+    ("MINDsmall_dev", 40, "WITH_HISTORY"),
+    ("MINDsmall_dev", None, "ALL"),
+    ("MINDsmall_dev", 30, "WITHOUT_HISTORY"),
+]
+
+
+def gen_dataset(du):
+    """Config 1 (scripts/eval.py:38-52): the reference's load_dataset on a tiny
+    processed split (WITH_HISTORY / ALL / WITHOUT_HISTORY, behaviors.sample
+    with a shared np.random.Generator) followed by its TransformData
+    (components.py:45-114); inputs and every output array are stored."""
+    import tempfile
+    import news_rec_utils.components as comp
+    import news_rec_utils.config as rc
+    news_cols, beh_cols, entity, cat_map, sub_map = dataset_inputs()
+    root = Path(tempfile.mkdtemp())
+    for split in {c[0] for c in DATASET_CASES}:
+        write_dataset(root, split, news_cols, beh_cols, entity, cat_map, sub_map)
+    rng = np.random.default_rng(1234)
+    out = {}
+    for k, (split, n, subset) in enumerate(DATASET_CASES):
+        beh, feats = du.load_dataset(root, rc.NewsDataset[split], num_samples=n, data_subset=rc.DataSubset[subset],
+                                     random_state=rng)
+        out[f"c{k}_ImpressionID"] = beh["ImpressionID"].to_numpy()
+        try:
+            ctx = comp.TransformData().transform({"behaviors": beh, **feats})
+        except ValueError as e:  # no history row at all: the reference's np.concatenate([]) raises
+            out[f"c{k}_error"] = np.array(f"ValueError: {e}")
+            continue
+        lab_flat, lab_len = flat(ctx["labels"])
+        out.update({f"c{k}_news_list": np.asarray(ctx["news_list"]),
+                    f"c{k}_impression_rev_ind_array": ctx["impression_rev_ind_array"],
+                    f"c{k}_impression_len_list": ctx["impression_len_list"],
+                    f"c{k}_history_rev_ind_array": ctx["history_rev_ind_array"],
+                    f"c{k}_history_len_list": ctx["history_len_list"],
+                    f"c{k}_labels_flat": lab_flat.astype(np.int64), f"c{k}_labels_len": lab_len,
+                    f"c{k}_history_bool": ctx["history_bool"].to_numpy(),
+                    f"c{k}_title_entity_embed": ctx["title_entity_embed"].numpy(),
+                    f"c{k}_abstract_entity_embed": ctx["abstract_entity_embed"].numpy(),
+                    f"c{k}_cat_indices": ctx["cat_indices"].numpy(), f"c{k}_subcat_indices": ctx["subcat_indices"].numpy()})
+        keys = sorted(feats["news_title_dict"])[:5]
+        out[f"c{k}_title_keys"] = np.array(keys)
+        out[f"c{k}_title_vals"] = np.array([feats["news_title_dict"][x] for x in keys])
+        akeys = sorted(feats["news_abstract_dict"])
+        out[f"c{k}_abstract_keys"] = np.array(akeys)
+    ent_ids = sorted(entity)
+    np.savez_compressed(
+        HERE / "dataset.npz", cases=np.array([f"{s}|{n}|{b}" for s, n, b in DATASET_CASES]),
+        news_cols=np.array(list(news_cols)),
+        **{f"news_{c}": np.array(["<NONE>" if v is None else v for v in news_cols[c]]) for c in news_cols},
+        beh_ImpressionID=beh_cols["ImpressionID"],
+        beh_History=np.array(["<NONE>" if v is None else v for v in beh_cols["History"]]),
+        beh_Impressions=np.array(beh_cols["Impressions"]),
+        entity_ids=np.array(ent_ids), entity_vecs=np.array([entity[q] for q in ent_ids]),
+        cat_keys=np.array(list(cat_map)), sub_keys=np.array(list(sub_map)), **out)
+
+
+GENERATORS = ("split", "rank", "final", "latent", "encoder", "token_attn", "train", "dataset")
 
 
 def main():
@@ -392,6 +502,8 @@ def main():
         gen_token_attn(dmh, du, mu)
     if "train" in which:
         gen_train(dmh, du, mu)
+    if "dataset" in which:
+        gen_dataset(du)
     for p in sorted(HERE.glob("*.npz")):
         print(p.name, p.stat().st_size)
 
