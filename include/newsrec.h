@@ -43,6 +43,8 @@ extern "C" {
 /* history poolers */
 #define NR_POOL_FINAL 0  /* FinalAttention additive per-dim softmax pooler */
 #define NR_POOL_LATENT 1 /* LatentAttentionModel masked mean + L2 normalize */
+#define NR_POOL_MEAN 2   /* masked mean only (average_pool, modeling_utils.py:55-59) */
+#define NR_POOL_NONE -1  /* nr_encoder_forward: no pooling (per-token hidden states only) */
 
 /* GEMM epilogues (applied to acc = A·Wᵀ) */
 #define NR_EPI_NONE 0   /* C = acc + bias                                   */
@@ -175,15 +177,20 @@ int nr_row_inv_norm(int dtype, int64_t rows, int64_t dim, const void* x, int64_t
  *
  * hist_table  per-news pooler table in `dtype`, row stride hist_ld:
  *             NR_POOL_FINAL : row = [x(dim) | exp(w)(dim)]
- *             NR_POOL_LATENT: row = h(dim)
+ *             NR_POOL_LATENT: row = h(dim)   (u = normalize(mean))
+ *             NR_POOL_MEAN  : row = h(dim)   (u = mean)
  * cand_table  raw news embeddings [*, dim] in `dtype` (row stride cand_ld)
  * cand_inv_norm  f32 1/max(||cand_table row||, 1e-8)
  * hist_idx/hist_off, cand_idx/cand_off   CSR (int32 rows, int64 offsets,
- *             n_imp + 1 entries each)
+ *             n_imp + 1 entries each).  hist_idx NULL: impression i pools the
+ *             consecutive table rows hist_off[i] .. hist_off[i+1]-1.
+ *             cand_off NULL: pooling only (no candidate is read; users required).
  * scores      f32 [cand_off[n_imp]] in impression order
  * users       nullable f32 [n_imp][dim]: the pooled user vectors
- *             (FinalAttention output / normalized latent mean)
- * Supported dim: 1024.
+ *             (FinalAttention output / normalized latent mean / mean)
+ * Supported dim: 1024 (NR_ERR_UNSUPPORTED otherwise; the reference's
+ * EMBEDDING_DIM == 4096 latent branch, latent_attention.py:89-97, has no kernel).
+ * Row indices are not bounds-checked: they must address rows of the tables.
  */
 int nr_pool_score(int pooler, int dtype, int64_t dim, const void* hist_table, int64_t hist_ld,
                   const void* cand_table, int64_t cand_ld, const float* cand_inv_norm,
@@ -196,8 +203,9 @@ int nr_pool_score(int pooler, int dtype, int64_t dim, const void* hist_table, in
  * scores of the same impression that are strictly greater.  Bit-exact
  * restatement of scipy.stats.rankdata(-x, method="dense") used by
  * rank_group_preds (data_utils.py:414-415).  Impressions must have at most
- * 2048 candidates (NR_ERR_UNSUPPORTED otherwise, checked on the device and
- * reported through `status`, a caller-zeroed int32 on the device).
+ * 2048 candidates (MIND has <= 300): a larger one is not ranked and sets
+ * *status = NR_ERR_UNSUPPORTED (`status`: a caller-zeroed int32 on the device,
+ * checked by the Python wrapper, which raises).
  */
 int nr_dense_rank(const float* scores, const int64_t* cand_off, int64_t n_imp, int32_t* ranks,
                   int32_t* status, void* stream);
@@ -255,9 +263,9 @@ int nr_latent_transform(int dtype, int64_t n, const void* emb, int64_t emb_ld,
  * softmax(q kᵀ / sqrt(64)) v with the key-padding mask, as run by
  * get_text_embed_eval (modeling_utils.py:282-300).  The layer GEMMs use
  * nr_gemm (NR_EPI_RESADD / NR_EPI_GELU), the post-LNs nr_layernorm, and the
- * masked mean + F.normalize (average_pool, modeling_utils.py:55-59,
- * data_model_helper.py:65-78) is nr_pool_score with NR_POOL_LATENT over
- * consecutive token rows.
+ * masked mean (+ F.normalize) (average_pool, modeling_utils.py:55-59,
+ * data_model_helper.py:65-78) is nr_pool_score with NR_POOL_MEAN (NR_POOL_LATENT)
+ * over consecutive token rows; nr_encoder_forward (below) chains all of it.
  *
  * nr_embed_ln: out[t] = LN(word[ids[t]] + type[0] + pos_emb[pos[t]]), dim 1024.
  * nr_attention_varlen: qkv [T][3072] (q | k | v, 16 heads x 64 per part),
@@ -334,6 +342,48 @@ int nr_sumsq(int64_t n, const float* x, float* out, void* stream);
 int nr_adamw(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf16, int64_t step, float lr,
              float beta1, float beta2, float eps, float weight_decay, float max_norm, const float* sumsq,
              void* stream);
+
+/*
+ * ---- Whole title-encoder forward (get_embeddings, data_model_helper.py:45-84:
+ * get_embed_from_model -> get_text_embed_eval modeling_utils.py:282-323 ->
+ * XLMRobertaModel -> average_pool (+ F.normalize for e5-instruct)) ----------
+ * Packed varlen tokens, no padding: sequence i is ids[cu_i .. cu_i + seq_lens[i]),
+ * cu = prefix sum of seq_lens (computed on the device).  Positions follow
+ * transformers' create_position_ids_from_input_ids (pad id 1: pad + cumsum(id
+ * != pad) * (id != pad)).  Per layer (post-LN BERT, eps `eps`):
+ *   x = LN1(Attn(x Wqkvᵀ + bqkv) Woᵀ + bo + x);  x = LN2(gelu(x W1ᵀ + b1) W2ᵀ + b2 + x)
+ * `layers` is a HOST array of n_layers descriptors of device weights (torch
+ * nn.Linear layout, `dtype`; biases and LN parameters f32).  Output:
+ *   pool NR_POOL_MEAN   pooled [n_seq][1024] f32 = average_pool(last_hidden_state)
+ *   pool NR_POOL_LATENT pooled = F.normalize(average_pool(...), p=2, eps=1e-12)
+ *   pool NR_POOL_NONE   no pooled output
+ * hidden (nullable, [n_tokens][1024] `dtype`): the packed last_hidden_state.
+ * ids and seq_lens are device int32 arrays (seq_lens[i] >= 1); n_tokens = their
+ * sum.  status (nullable, caller-zeroed device int32): |1 a position id
+ * reached n_positions (clamped), |2 a token id outside [0, vocab) (clamped).
+ * ws: nr_encoder_workspace_bytes(dtype, n_tokens, n_seq) bytes.
+ */
+typedef struct nr_encoder_layer {
+  const void* wqkv;    /* [3072][1024]: self.query | self.key | self.value weights */
+  const float* bqkv;   /* [3072] */
+  const void* wo;      /* attention.output.dense [1024][1024] */
+  const float* bo;
+  const float* ln1_g;  /* attention.output.LayerNorm */
+  const float* ln1_b;
+  const void* w1;      /* intermediate.dense [4096][1024] */
+  const float* b1;
+  const void* w2;      /* output.dense [1024][4096] */
+  const float* b2;
+  const float* ln2_g;  /* output.LayerNorm */
+  const float* ln2_b;
+} nr_encoder_layer;
+
+int64_t nr_encoder_workspace_bytes(int dtype, int64_t n_tokens, int64_t n_seq);
+int nr_encoder_forward(int dtype, int n_layers, const nr_encoder_layer* layers, const void* word_emb,
+                       int64_t vocab, const void* pos_emb, int64_t n_positions, const void* type_emb,
+                       const float* emb_ln_g, const float* emb_ln_b, float eps, int64_t n_seq,
+                       int64_t n_tokens, const int32_t* seq_lens, const int32_t* ids, int pool, float* pooled,
+                       void* hidden, int32_t* status, void* ws, int64_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

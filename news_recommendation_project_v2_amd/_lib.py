@@ -19,6 +19,8 @@ NR_BF16 = 1
 NR_F16 = 2
 NR_POOL_FINAL = 0
 NR_POOL_LATENT = 1
+NR_POOL_MEAN = 2
+NR_POOL_NONE = -1
 NR_EPI_NONE = 0
 NR_EPI_RELU = 1
 NR_EPI_EXP = 2
@@ -66,7 +68,16 @@ SIGNATURES = {
     "nr_ln_param_grad": (_i, [_i, _l, _l, _p, _l, _p, _f, _p, _l, _p, _p, _p]),
     "nr_sumsq": (_i, [_l, _p, _p, _p]),
     "nr_adamw": (_i, [_l, _p, _p, _p, _p, _p, _l, _f, _f, _f, _f, _f, _f, _p, _p]),
+    "nr_encoder_workspace_bytes": (_l, [_i, _l, _l]),
+    "nr_encoder_forward": (_i, [_i, _i, _p, _p, _l, _p, _l, _p, _p, _p, _f, _l, _l, _p, _p, _i, _p, _p, _p, _p, _l,
+                                _p]),
 }
+
+
+class EncoderLayer(ctypes.Structure):
+    """struct nr_encoder_layer (include/newsrec.h): device pointers of one layer."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("wqkv", "bqkv", "wo", "bo", "ln1_g", "ln1_b", "w1", "b1", "w2", "b2",
+                                             "ln2_g", "ln2_b")]
 
 
 class NewsRecHIPError(RuntimeError):

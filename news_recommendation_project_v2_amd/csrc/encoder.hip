@@ -80,6 +80,9 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = blockIdx.y * 4 + wave;     // head
   const int qb_global = blockIdx.x;        // global query-block index
+  // nr_encoder_forward launches an upper bound of query blocks (the exact count
+  // lives on the device): blocks past the last one exit (block-uniform)
+  if (qb_global >= qoff[n_seq]) return;
   // 64-ary search for the sequence owning this query block (qoff: prefix of
   // ceil(L/32), qoff[n_seq] = total): each step probes 64 boundaries with one
   // wave load + ballot, so 20k sequences take 3 dependent loads, not 15.
@@ -280,7 +283,201 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
   }
 }
 
+// ------------------------------------------------------------ whole forward
+constexpr int kPadId = 1;  // XLM-R <pad>; positions start at kPadId + 1
+
+// cu32/cu64 = prefix sums of seq_lens, qoff = prefix sum of ceil(len / 32):
+// one 1024-thread workgroup walks the sequences 1024 at a time (wave scans +
+// one LDS pass), carrying the running totals.
+__global__ __launch_bounds__(1024) void encoder_offsets_kernel(int64_t n_seq, const int32_t* __restrict__ lens,
+                                                               int32_t* __restrict__ cu32, int64_t* __restrict__ cu64,
+                                                               int32_t* __restrict__ qoff) {
+  __shared__ int64_t wtok[16];
+  __shared__ int32_t wqb[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int64_t carry_t = 0;
+  int32_t carry_q = 0;
+  if (tid == 0) {
+    cu32[0] = 0;
+    cu64[0] = 0;
+    qoff[0] = 0;
+  }
+  for (int64_t base = 0; base < n_seq; base += 1024) {
+    const int64_t i = base + tid;
+    const int32_t L = i < n_seq ? lens[i] : 0;
+    int64_t t = L;
+    int32_t q = (L + 31) / 32;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {  // inclusive wave scans
+      const int64_t tt = __shfl_up(t, o, 64);
+      const int32_t qq = __shfl_up(q, o, 64);
+      if (lane >= o) {
+        t += tt;
+        q += qq;
+      }
+    }
+    if (lane == 63) {
+      wtok[wave] = t;
+      wqb[wave] = q;
+    }
+    __syncthreads();
+    int64_t pt = carry_t;
+    int32_t pq = carry_q;
+    for (int w = 0; w < wave; ++w) {
+      pt += wtok[w];
+      pq += wqb[w];
+    }
+    if (i < n_seq) {
+      cu64[i + 1] = pt + t;
+      cu32[i + 1] = (int32_t)(pt + t);
+      qoff[i + 1] = pq + q;
+    }
+    for (int w = 0; w < 16; ++w) {
+      carry_t += wtok[w];
+      carry_q += wqb[w];
+    }
+    __syncthreads();
+  }
+}
+
+// transformers create_position_ids_from_input_ids per packed sequence:
+// pos = pad + cumsum(id != pad) * (id != pad).  One wave per sequence.  Out-of-
+// range ids / positions are clamped (so no row outside the tables is read) and
+// flagged in *status.
+__global__ __launch_bounds__(256) void encoder_positions_kernel(int64_t n_seq, const int32_t* __restrict__ cu,
+                                                                int32_t* __restrict__ ids, int32_t* __restrict__ pos,
+                                                                int64_t vocab, int64_t n_positions,
+                                                                int32_t* __restrict__ status) {
+  const int lane = threadIdx.x & 63;
+  const int64_t seq = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (seq >= n_seq) return;
+  const int64_t s0 = cu[seq];
+  const int L = cu[seq + 1] - cu[seq];
+  int carry = 0, flag = 0;
+  for (int b = 0; b < L; b += 64) {
+    const int t = b + lane;
+    int id = kPadId;
+    if (t < L) {
+      id = ids[s0 + t];
+      if (id < 0 || id >= vocab) {
+        flag |= 2;
+        id = id < 0 ? 0 : (int)(vocab - 1);
+        ids[s0 + t] = id;
+      }
+    }
+    const bool m = t < L && id != kPadId;
+    const unsigned long long bal = __ballot(m);
+    const int incl = __popcll(bal & ((2ull << lane) - 1));
+    int p = m ? kPadId + carry + incl : kPadId;
+    if (p >= n_positions) {
+      flag |= 1;
+      p = (int)(n_positions - 1);
+    }
+    if (t < L) pos[s0 + t] = p;
+    carry += __popcll(bal);
+  }
+  if (flag && status) atomicOr(status, flag);
+}
+
+static int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+struct EncWs {  // workspace carve-up of nr_encoder_forward
+  int64_t x, big, ctx, tmp, pos, cu32, qoff, cu64, total;
+};
+static EncWs enc_ws(int dtype, int64_t T, int64_t n, bool own_x) {
+  const int64_t es = dtype == NR_F32 ? 4 : 2;
+  EncWs w{};
+  int64_t o = 0;
+  w.x = o;   o += own_x ? align256(T * 1024 * es) : 0;
+  w.big = o; o += align256(T * 4096 * es);  // qkv [T][3072], later the FFN hidden [T][4096]
+  w.ctx = o; o += align256(T * 1024 * es);
+  w.tmp = o; o += align256(T * 1024 * es);
+  w.pos = o; o += align256(T * 4);
+  w.cu32 = o; o += align256((n + 1) * 4);
+  w.qoff = o; o += align256((n + 1) * 4);
+  w.cu64 = o; o += align256((n + 1) * 8);
+  w.total = o;
+  return w;
+}
+
 }  // namespace nr
+
+extern "C" int64_t nr_encoder_workspace_bytes(int dtype, int64_t n_tokens, int64_t n_seq) {
+  // sized for hidden == NULL (the library keeps x); a caller-provided hidden needs less
+  return nr::enc_ws(dtype, n_tokens, n_seq, true).total;
+}
+
+extern "C" int nr_encoder_forward(int dtype, int n_layers, const nr_encoder_layer* layers, const void* word_emb,
+                                  int64_t vocab, const void* pos_emb, int64_t n_positions, const void* type_emb,
+                                  const float* emb_ln_g, const float* emb_ln_b, float eps, int64_t n_seq,
+                                  int64_t n_tokens, const int32_t* seq_lens, const int32_t* ids, int pool,
+                                  float* pooled, void* hidden, int32_t* status, void* ws, int64_t ws_bytes,
+                                  void* stream) {
+  nr::clear_error();
+  NR_CHECK_ARG(dtype == NR_F32 || dtype == NR_BF16, "nr_encoder_forward: bad dtype %d", dtype);
+  NR_CHECK_ARG(n_layers >= 0 && (n_layers == 0 || layers), "nr_encoder_forward: bad layers");
+  NR_CHECK_ARG(pool == NR_POOL_MEAN || pool == NR_POOL_LATENT || pool == NR_POOL_NONE,
+               "nr_encoder_forward: bad pool %d", pool);
+  NR_CHECK_ARG(n_seq >= 0 && n_tokens >= 0, "nr_encoder_forward: negative sizes");
+  if (n_seq == 0) return NR_OK;
+  NR_CHECK_ARG(n_tokens <= 0x7fffffff && n_seq <= 0x7fffffff, "nr_encoder_forward: too many tokens / sequences");
+  NR_CHECK_ARG(word_emb && pos_emb && type_emb && emb_ln_g && emb_ln_b && seq_lens && ids && ws,
+               "nr_encoder_forward: null pointer");
+  NR_CHECK_ARG(vocab > 0 && n_positions > nr::kPadId + 1, "nr_encoder_forward: bad vocab / n_positions");
+  NR_CHECK_ARG(pool == NR_POOL_NONE || pooled, "nr_encoder_forward: pooled is NULL");
+  NR_CHECK_ARG(pool != NR_POOL_NONE || hidden, "nr_encoder_forward: nothing to output");
+  for (int l = 0; l < n_layers; ++l) {
+    const nr_encoder_layer& L = layers[l];
+    NR_CHECK_ARG(L.wqkv && L.bqkv && L.wo && L.bo && L.ln1_g && L.ln1_b && L.w1 && L.b1 && L.w2 && L.b2 &&
+                     L.ln2_g && L.ln2_b, "nr_encoder_forward: layer %d has a null pointer", l);
+  }
+  const nr::EncWs w = nr::enc_ws(dtype, n_tokens, n_seq, hidden == nullptr);
+  NR_CHECK_ARG(ws_bytes >= w.total, "nr_encoder_forward: workspace too small (%lld < %lld)", (long long)ws_bytes,
+               (long long)w.total);
+  NR_CHECK_ARG(((uintptr_t)ws & 255) == 0 && (!hidden || ((uintptr_t)hidden & 15) == 0),
+               "nr_encoder_forward: ws must be 256-byte aligned, hidden 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  char* b = (char*)ws;
+  void* x = hidden ? hidden : (void*)(b + w.x);
+  void* big = b + w.big;
+  void* ctx = b + w.ctx;
+  void* tmp = b + w.tmp;
+  int32_t* pos = (int32_t*)(b + w.pos);
+  int32_t* cu32 = (int32_t*)(b + w.cu32);
+  int32_t* qoff = (int32_t*)(b + w.qoff);
+  int64_t* cu64 = (int64_t*)(b + w.cu64);
+  const int64_t T = n_tokens, D = 1024, F = 4096;
+  // the ids are clamped in place when out of range: work on a copy in the workspace
+  int32_t* ids_ws = (int32_t*)tmp;  // tmp is first written by layer 0's O-projection
+  if (hipMemcpyAsync(ids_ws, ids, T * 4, hipMemcpyDeviceToDevice, s) != hipSuccess) {
+    nr::set_error("nr_encoder_forward: copy of ids failed");
+    return NR_ERR_HIP;
+  }
+  hipLaunchKernelGGL(nr::encoder_offsets_kernel, dim3(1), dim3(1024), 0, s, n_seq, seq_lens, cu32, cu64, qoff);
+  NR_CHECK_LAUNCH("nr_encoder_forward(offsets)");
+  hipLaunchKernelGGL(nr::encoder_positions_kernel, dim3((unsigned)((n_seq + 3) / 4)), dim3(256), 0, s, n_seq, cu32,
+                     ids_ws, pos, vocab, n_positions, status);
+  NR_CHECK_LAUNCH("nr_encoder_forward(positions)");
+  int rc;
+  if ((rc = nr_embed_ln(dtype, T, ids_ws, pos, word_emb, pos_emb, type_emb, emb_ln_g, emb_ln_b, eps, x, stream)))
+    return rc;
+  // upper bound of the query-block count (exact count sits in qoff[n_seq] on the device)
+  const int64_t qb_bound = (T + 31) / 32 + n_seq;
+  for (int l = 0; l < n_layers; ++l) {
+    const nr_encoder_layer& L = layers[l];
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_NONE, T, 3 * D, D, x, D, L.wqkv, D, L.bqkv, nullptr, 0, big, 3 * D, s)))
+      return rc;
+    if ((rc = nr_attention_varlen(dtype, (int32_t)n_seq, qb_bound, big, cu32, qoff, ctx, stream))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RESADD, T, D, D, ctx, D, L.wo, D, L.bo, x, D, tmp, D, s))) return rc;
+    if ((rc = nr::layernorm_dispatch(dtype, dtype, T, D, tmp, D, L.ln1_g, L.ln1_b, eps, x, D, s))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_GELU, T, F, D, x, D, L.w1, D, L.b1, nullptr, 0, big, F, s))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RESADD, T, D, F, big, F, L.w2, F, L.b2, x, D, tmp, D, s))) return rc;
+    if ((rc = nr::layernorm_dispatch(dtype, dtype, T, D, tmp, D, L.ln2_g, L.ln2_b, eps, x, D, s))) return rc;
+  }
+  if (pool != NR_POOL_NONE)
+    if ((rc = nr::pool_rows_dispatch(pool, dtype, x, D, cu64, n_seq, pooled, s))) return rc;
+  return NR_OK;
+}
 
 extern "C" int nr_embed_ln(int dtype, int64_t n_tokens, const int32_t* ids, const int32_t* pos,
                            const void* word, const void* pos_emb, const void* type_emb, const float* gamma,

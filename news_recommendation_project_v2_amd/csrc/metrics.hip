@@ -17,6 +17,9 @@
 namespace nr {
 
 constexpr int kMaxCand = 2048;
+// the rank-bin rewrite below packs (run << 12) | k with run, k <= kMaxCand in
+// 12-bit fields: raising kMaxCand past 4095 needs a wider packing
+static_assert(kMaxCand < 4096, "metrics_kernel packs counts in 12 bits");
 
 __global__ __launch_bounds__(256) void metrics_kernel(const int32_t* __restrict__ ranks, const float* __restrict__ labels,
                                                       const int64_t* __restrict__ off, int64_t n_imp,
@@ -58,7 +61,8 @@ __global__ __launch_bounds__(256) void metrics_kernel(const int32_t* __restrict_
     return;
   }
   // h[v] <- number of candidates with dense rank > v (lower score): suffix sum
-  // over 1..c, 32 bins per lane, then a wave scan of the lane totals.
+  // over 1..c, ceil(c / 64) consecutive bins per lane, then a wave scan of the
+  // lane totals.
   const int per = (c + 63) / 64;
   const int lo = 1 + lane * per, hi = min(c, lo + per - 1);
   int tot = 0;
@@ -69,10 +73,11 @@ __global__ __launch_bounds__(256) void metrics_kernel(const int32_t* __restrict_
     if (lane + m < 64) suf += t;
   }
   int run = suf - tot;  // candidates in bins above this lane's range
-  // rewrite bins high -> low: keep the count in the upper 16 bits
+  // rewrite bins high -> low: bits 12+ = candidates ranked strictly below the
+  // bin (run), bits 0-11 = the bin's own count (k)
   for (int v = hi; v >= lo; --v) {
     const int k = h[v];
-    h[v] = (run << 12) | k;  // run <= 2048 (12 bits), k <= 2048 needs 12 bits
+    h[v] = (run << 12) | k;  // run, k <= kMaxCand < 4096
     run += k;
   }
   __builtin_amdgcn_wave_barrier();

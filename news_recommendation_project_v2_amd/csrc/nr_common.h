@@ -31,6 +31,8 @@ int layernorm_dispatch(int dti, int dto, int64_t rows, int64_t dim, const void* 
                        hipStream_t s);
 int softmax64_dispatch(int64_t rows, int64_t groups, const float* x, int64_t ldx, int dto, void* y,
                        int64_t ldy, hipStream_t s);
+int pool_rows_dispatch(int pooler, int dtype, const void* table, int64_t ld, const int64_t* off, int64_t n_seg,
+                       float* users, hipStream_t s);
 int inv_norm_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps,
                       float* out, hipStream_t s);
 

@@ -10,6 +10,7 @@
 // chain (gemm.hip); this kernel only gathers table rows:
 //   FINAL : u = sum_j x_j*p_j / (sum_j p_j + 1e-10)     (p = exp(w), per dim)
 //   LATENT: u = normalize(sum_j h_j / h_i, eps 1e-12)
+//   MEAN  : u = sum_j h_j / h_i            (average_pool, modeling_utils.py:55-59)
 //   score_c = (u . e_c) / max(|u|, 1e-8) / max(|e_c|, 1e-8)
 //
 // Work decomposition: one wave (64 lanes) per impression, 4 impressions per
@@ -81,6 +82,8 @@ template <> struct PoolCfg<float, NR_POOL_FINAL> { static constexpr int R = 2; }
 template <> struct PoolCfg<float, NR_POOL_LATENT> { static constexpr int R = 4; };
 template <> struct PoolCfg<__bf16, NR_POOL_FINAL> { static constexpr int R = 4; };
 template <> struct PoolCfg<__bf16, NR_POOL_LATENT> { static constexpr int R = 8; };
+template <> struct PoolCfg<float, NR_POOL_MEAN> { static constexpr int R = 4; };
+template <> struct PoolCfg<__bf16, NR_POOL_MEAN> { static constexpr int R = 8; };
 
 // transpose-reduce of 4 per-lane partial dots; returns the total of dot q in
 // lane 16*q (and its 15 neighbours).
@@ -124,7 +127,8 @@ __global__ __launch_bounds__(256) void pool_score_kernel(
   const int64_t h0 = hoff[imp], h1 = hoff[imp + 1];
   for (int64_t base = h0; base < h1; base += 64) {
     const int cnt = (int)min((int64_t)64, h1 - base);
-    const int myidx = lane < cnt ? hidx[base + lane] : 0;
+    // hidx == nullptr: the segment's rows are consecutive table rows (token pooling)
+    const int myidx = lane < cnt ? (hidx ? hidx[base + lane] : (int)(base + lane)) : 0;
     int r = 0;
     for (; r + R <= cnt; r += R) {
       uint4 bx[R][NL];
@@ -178,6 +182,10 @@ __global__ __launch_bounds__(256) void pool_score_kernel(
     // modeling_utils.py:224-228: w = exp(w)*m; w /= (sum w + 1e-10); sum x*w
 #pragma unroll
     for (int i = 0; i < EPL; ++i) u[i] = acc[i] / (den[i] + 1e-10f);
+  } else if constexpr (POOL == NR_POOL_MEAN) {
+    const float d = (float)(h1 - h0);
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) u[i] = acc[i] / d;
   } else {
     // latent_attention.py:166-170: s / d, then F.normalize(p=2, eps=1e-12)
     const float d = (float)(h1 - h0);
@@ -201,6 +209,7 @@ __global__ __launch_bounds__(256) void pool_score_kernel(
   }
 
   // ---------------- candidate scoring ----------------
+  if (coff == nullptr) return;  // pooling only
   const int64_t c0 = coff[imp], c1 = coff[imp + 1];
   for (int64_t base = c0; base < c1; base += 64) {
     const int cnt = (int)min((int64_t)64, c1 - base);
@@ -249,6 +258,21 @@ static int launch_pool_score(const void* ht, int64_t hld, const void* ct, int64_
   return NR_OK;
 }
 
+// Pooling only (no candidates) of consecutive rows: segment i = table rows
+// off[i] .. off[i+1]-1, u written to users [n_seg][1024] f32.
+int pool_rows_dispatch(int pooler, int dtype, const void* table, int64_t ld, const int64_t* off, int64_t n_seg,
+                       float* users, hipStream_t s) {
+  if (n_seg == 0) return NR_OK;
+  if (dtype == NR_F32) {
+    if (pooler == NR_POOL_MEAN)
+      return launch_pool_score<float, NR_POOL_MEAN>(table, ld, table, ld, nullptr, nullptr, off, nullptr, nullptr, n_seg, nullptr, users, s);
+    return launch_pool_score<float, NR_POOL_LATENT>(table, ld, table, ld, nullptr, nullptr, off, nullptr, nullptr, n_seg, nullptr, users, s);
+  }
+  if (pooler == NR_POOL_MEAN)
+    return launch_pool_score<__bf16, NR_POOL_MEAN>(table, ld, table, ld, nullptr, nullptr, off, nullptr, nullptr, n_seg, nullptr, users, s);
+  return launch_pool_score<__bf16, NR_POOL_LATENT>(table, ld, table, ld, nullptr, nullptr, off, nullptr, nullptr, n_seg, nullptr, users, s);
+}
+
 }  // namespace nr
 
 extern "C" int nr_pool_score(int pooler, int dtype, int64_t dim, const void* hist_table,
@@ -262,13 +286,18 @@ extern "C" int nr_pool_score(int pooler, int dtype, int64_t dim, const void* his
     nr::set_error("nr_pool_score: dim %lld unsupported (1024 only)", (long long)dim);
     return NR_ERR_UNSUPPORTED;
   }
-  NR_CHECK_ARG(pooler == NR_POOL_FINAL || pooler == NR_POOL_LATENT, "nr_pool_score: bad pooler %d", pooler);
+  NR_CHECK_ARG(pooler == NR_POOL_FINAL || pooler == NR_POOL_LATENT || pooler == NR_POOL_MEAN,
+               "nr_pool_score: bad pooler %d", pooler);
   NR_CHECK_ARG(dtype == NR_F32 || dtype == NR_BF16, "nr_pool_score: bad dtype %d", dtype);
   NR_CHECK_ARG(n_imp >= 0, "nr_pool_score: n_imp < 0");
   if (n_imp == 0) return NR_OK;
-  NR_CHECK_ARG(hist_table && cand_table && cand_inv_norm && hist_idx && hist_off && cand_idx &&
-                   cand_off && scores,
-               "nr_pool_score: null pointer");
+  const bool score = cand_off != nullptr;
+  NR_CHECK_ARG(hist_table && hist_off && (score || users), "nr_pool_score: null pointer");
+  NR_CHECK_ARG(!score || (cand_table && cand_inv_norm && cand_idx && scores), "nr_pool_score: null candidate pointer");
+  if (!score) {
+    cand_table = hist_table;
+    cand_ld = hist_ld;
+  }
   const int64_t min_hld = pooler == NR_POOL_FINAL ? 2 * dim : dim;
   NR_CHECK_ARG(hist_ld >= min_hld && cand_ld >= dim, "nr_pool_score: leading dimension too small");
   const int64_t align = dtype == NR_F32 ? 4 : 8;
@@ -276,6 +305,11 @@ extern "C" int nr_pool_score(int pooler, int dtype, int64_t dim, const void* his
                    ((uintptr_t)hist_table & 15) == 0 && ((uintptr_t)cand_table & 15) == 0,
                "nr_pool_score: tables must be 16-byte aligned with 16-byte row strides");
   hipStream_t s = (hipStream_t)stream;
+  if (pooler == NR_POOL_MEAN) {
+    if (dtype == NR_F32)
+      return nr::launch_pool_score<float, NR_POOL_MEAN>(hist_table, hist_ld, cand_table, cand_ld, cand_inv_norm, hist_idx, hist_off, cand_idx, cand_off, n_imp, scores, users, s);
+    return nr::launch_pool_score<__bf16, NR_POOL_MEAN>(hist_table, hist_ld, cand_table, cand_ld, cand_inv_norm, hist_idx, hist_off, cand_idx, cand_off, n_imp, scores, users, s);
+  }
   if (dtype == NR_F32) {
     if (pooler == NR_POOL_FINAL)
       return nr::launch_pool_score<float, NR_POOL_FINAL>(hist_table, hist_ld, cand_table, cand_ld, cand_inv_norm, hist_idx, hist_off, cand_idx, cand_off, n_imp, scores, users, s);

@@ -6,11 +6,12 @@ Replaces, for the e5-large-instruct / XLM-R-large encoder that
   * padded batches of tokenised titles, the full HF forward, the D2H copy of
     every [B, L, 1024] hidden state and ``average_pool`` + ``F.normalize`` on
     the host,
-with packed varlen token rows on the device (no padding), one embedding+LN
-kernel, per layer a fused QKV GEMM, the MFMA varlen attention kernel, GEMMs
-with residual / GELU epilogues, post-LayerNorms, and the masked mean +
-L2-normalise done by the segmented pool kernel (latent pooler over
-consecutive token rows).  Only the [B, 1024] embeddings leave the device.
+with packed varlen token rows on the device (no padding) and ONE C-ABI call
+per chunk, ``nr_encoder_forward``: embedding + LN, per layer a fused QKV GEMM,
+the MFMA varlen attention kernel, GEMMs with residual / GELU epilogues,
+post-LayerNorms, and the masked mean (average_pool; + F.normalize only for
+the e5-instruct branch of get_embeddings) by the segmented pool kernel over
+consecutive token rows.  Only the [B, 1024] embeddings leave the device.
 
 Weights use the transformers ``XLMRobertaModel`` state-dict keys
 (``embeddings.*``, ``encoder.layer.{i}.*``; a ``roberta.``/``model.`` prefix is
@@ -25,7 +26,8 @@ from typing import Iterable, Optional, Sequence
 import numpy as np
 import torch
 
-from . import ops
+from . import _lib, ops
+from .config import NEWS_TEXT_MAXLEN
 
 PAD_ID = 1          # XLM-R <pad>; positions start at PAD_ID + 1
 LN_EPS = 1e-5       # XLM-R layer_norm_eps (NOT XLMRobertaConfig's 1e-12 default)
@@ -88,6 +90,15 @@ class XLMREncoder:
                 "ln2": (f(p + "output.LayerNorm.weight"), f(p + "output.LayerNorm.bias")),
             })
 
+        self._emb = {"word": self.word, "pos": self.pos, "type": self.type0, "ln_g": self.eln[0], "ln_b": self.eln[1]}
+        self._layers = (_lib.EncoderLayer * n)()
+        for i, L in enumerate(self.layers):
+            ptrs = [L["wqkv"], L["bqkv"], L["wo"], L["bo"], L["ln1"][0], L["ln1"][1], L["w1"], L["b1"], L["w2"],
+                    L["b2"], L["ln2"][0], L["ln2"][1]]
+            for (name, _), t in zip(_lib.EncoderLayer._fields_, ptrs):
+                setattr(self._layers[i], name, t.data_ptr())
+        self._ws = None
+
     @classmethod
     def from_pretrained_dir(cls, path, **kw) -> "XLMREncoder":
         """Local HF directory (model.safetensors or pytorch_model.bin); no network."""
@@ -101,36 +112,27 @@ class XLMREncoder:
         return cls(sd, **kw)
 
     # ------------------------------------------------------------------ forward
-    def _chunk_forward(self, ids: np.ndarray, lens: np.ndarray) -> torch.Tensor:
-        x, cu = self._chunk_hidden(ids, lens)
-        # average_pool + F.normalize == latent pooling over each sequence's rows
-        from .modeling_utils import pool_rows
-        return pool_rows("latent", x, torch.as_tensor(cu).to(self.device))
+    def _forward(self, ids: np.ndarray, lens: np.ndarray, pool: Optional[str], want_hidden: bool,
+                 status: torch.Tensor):
+        """One nr_encoder_forward call over a chunk of packed sequences."""
+        dev = self.device
+        ids_d = torch.as_tensor(np.ascontiguousarray(ids, dtype=np.int32)).to(dev)
+        lens_d = torch.as_tensor(np.ascontiguousarray(lens, dtype=np.int32)).to(dev)
+        T = int(np.asarray(lens, dtype=np.int64).sum())
+        need = _lib.load().nr_encoder_workspace_bytes(_lib.NR_F32 if self.dtype == torch.float32 else _lib.NR_BF16,
+                                                      T, len(lens))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        return ops.encoder_forward(self._layers, self._emb, ids_d, lens_d, T, pool=pool, want_hidden=want_hidden,
+                                   eps=LN_EPS, workspace=self._ws, status=status)
 
-    def _chunk_hidden(self, ids: np.ndarray, lens: np.ndarray):
-        """last_hidden_state of the valid tokens, packed [T, 1024] (+ host offsets)."""
-        dev, dt = self.device, self.dtype
-        T = int(lens.sum())
-        ids_d = torch.as_tensor(ids.astype(np.int32)).to(dev)
-        pos_d = torch.as_tensor(positions_for(ids, lens)).to(dev)
-        cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
-        qb = np.concatenate([[0], np.cumsum((lens + 31) // 32)]).astype(np.int64)
-        cu_i32 = torch.as_tensor(cu.astype(np.int32)).to(dev)
-        qb_i32 = torch.as_tensor(qb.astype(np.int32)).to(dev)
-        x = ops.embed_ln(ids_d, pos_d, self.word, self.pos, self.type0, self.eln[0], self.eln[1], LN_EPS)
-        qkv = torch.empty((T, 3 * HIDDEN), dtype=dt, device=dev)
-        ctx = torch.empty((T, HIDDEN), dtype=dt, device=dev)
-        tmp = torch.empty((T, HIDDEN), dtype=dt, device=dev)
-        ffn = torch.empty((T, FFN), dtype=dt, device=dev)
-        for L in self.layers:
-            ops.gemm(x, L["wqkv"], L["bqkv"], out=qkv)
-            ops.attention_varlen(qkv, cu_i32, qb_i32, int(qb[-1]), out=ctx)
-            ops.gemm(ctx, L["wo"], L["bo"], epilogue="resadd", residual=x, out=tmp)
-            ops.layernorm(tmp, L["ln1"][0], L["ln1"][1], LN_EPS, out=x)
-            ops.gemm(x, L["w1"], L["b1"], epilogue="gelu", out=ffn)
-            ops.gemm(ffn, L["w2"], L["b2"], epilogue="resadd", residual=x, out=tmp)
-            ops.layernorm(tmp, L["ln2"][0], L["ln2"][1], LN_EPS, out=x)
-        return x, cu
+    @staticmethod
+    def _check_status(status: torch.Tensor) -> None:
+        st = int(status.item())
+        if st & 2:  # the reference's nn.Embedding lookup raises IndexError here
+            raise IndexError("token id outside the encoder vocabulary")
+        if st & 1:
+            raise IndexError(f"sequence longer than the position table ({NEWS_TEXT_MAXLEN} tokens after truncation)")
 
     def _chunks(self, lens: np.ndarray):
         """Consecutive sequence ranges [s, e) of at most max_tokens tokens."""
@@ -143,14 +145,20 @@ class XLMREncoder:
             yield s, e, off
             s = e
 
-    def encode_packed(self, ids: np.ndarray, lens: np.ndarray) -> torch.Tensor:
+    def encode_packed(self, ids: np.ndarray, lens: np.ndarray, normalize: bool = False) -> torch.Tensor:
         """ids: flat int tokens of all sequences; lens: tokens per sequence.
-        Returns L2-normalised mean-pooled embeddings [B, 1024] f32 on device."""
+        Returns average_pool(last_hidden_state) [B, 1024] f32 on the device
+        (get_text_embed_eval, modeling_utils.py:282-300), L2-normalised when
+        ``normalize`` (the e5-instruct branch of get_embeddings,
+        data_model_helper.py:65-78)."""
         ids = np.asarray(ids)
         lens = np.asarray(lens, dtype=np.int64)
         if np.any(lens <= 0):
             raise ValueError("every sequence needs at least one token")
-        out = [self._chunk_forward(ids[off[s]:off[e]], lens[s:e]) for s, e, off in self._chunks(lens)]
+        status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        pool = "normalize" if normalize else "mean"
+        out = [self._forward(ids[off[s]:off[e]], lens[s:e], pool, False, status)[0] for s, e, off in self._chunks(lens)]
+        self._check_status(status)
         return torch.cat(out) if out else torch.zeros((0, HIDDEN), device=self.device)
 
     def hidden_states_packed(self, ids: np.ndarray, lens: np.ndarray):
@@ -161,8 +169,10 @@ class XLMREncoder:
         lens = np.asarray(lens, dtype=np.int64)
         if np.any(lens <= 0):
             raise ValueError("every sequence needs at least one token")
+        status = torch.zeros(1, dtype=torch.int32, device=self.device)
         for s, e, off in self._chunks(lens):
-            x, _ = self._chunk_hidden(ids[off[s]:off[e]], lens[s:e])
+            _, x = self._forward(ids[off[s]:off[e]], lens[s:e], None, True, status)
+            self._check_status(status)
             yield s, x, lens[s:e]
 
     def encode_padded(self, input_ids: torch.Tensor, attention_mask: torch.Tensor) -> torch.Tensor:
@@ -216,8 +226,11 @@ def get_embeddings(model_path: str, news_list: Iterable[str], news_text_dict: di
     enc = XLMREncoder.from_pretrained_dir(model_path, dtype=dtype)
     news = list(news_list)
     passages = [news_text_dict[n] for n in news]
-    p = enc.encode_packed(*tokenize(tok, passages, NEWS_TEXT_MAXLEN)).cpu()
     if "e5" in str(model_path) and "instruct" in str(model_path):
-        q = enc.encode_packed(*tokenize(tok, [QUERY_INSTRUCTION + t for t in passages], NEWS_TEXT_MAXLEN)).cpu()
+        # data_model_helper.py:59-80: query + passage passes, each F.normalize'd
+        q = enc.encode_packed(*tokenize(tok, [QUERY_INSTRUCTION + t for t in passages], NEWS_TEXT_MAXLEN),
+                              normalize=True).cpu()
+        p = enc.encode_packed(*tokenize(tok, passages, NEWS_TEXT_MAXLEN), normalize=True).cpu()
         return q, p
-    return p
+    # data_model_helper.py:81-84: any other model returns the raw average_pool
+    return enc.encode_packed(*tokenize(tok, passages, NEWS_TEXT_MAXLEN)).cpu()

@@ -71,17 +71,7 @@ def flatten_valid(embeddings: torch.Tensor, attention_mask: torch.Tensor):
 
 def pool_rows(pooler: str, table: torch.Tensor, hist_off: torch.Tensor) -> torch.Tensor:
     """Pool consecutive table rows per segment with the HIP kernel (no candidates)."""
-    n = table.shape[0]
-    dev = table.device
-    hist_idx = torch.arange(n, dtype=torch.int32, device=dev)
-    n_seg = hist_off.numel() - 1
-    cand_off = torch.zeros(n_seg + 1, dtype=torch.int64, device=dev)
-    cand_tab = torch.zeros((1, 1024), dtype=table.dtype, device=dev)
-    cand_inv = torch.zeros(1, dtype=torch.float32, device=dev)
-    empty = torch.zeros(1, dtype=torch.int32, device=dev)
-    _, users = ops.pool_score(pooler, table, cand_tab, cand_inv, hist_idx, hist_off, empty, cand_off, 0,
-                              want_users=True)
-    return users
+    return ops.pool_rows(pooler, table, hist_off)
 
 
 class FinalAttention(torch.nn.Module):

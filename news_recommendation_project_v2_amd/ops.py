@@ -23,7 +23,7 @@ _EPI = {
     "gelu": _lib.NR_EPI_GELU,
     "softmax64": _lib.NR_EPI_SOFTMAX64,
 }
-POOLERS = {"final": _lib.NR_POOL_FINAL, "latent": _lib.NR_POOL_LATENT}
+POOLERS = {"final": _lib.NR_POOL_FINAL, "latent": _lib.NR_POOL_LATENT, "mean": _lib.NR_POOL_MEAN}
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -318,6 +318,51 @@ def attention_varlen(qkv: torch.Tensor, cu_seqlens: torch.Tensor, qblock_off: to
     _lib.call("nr_attention_varlen", _dtype(qkv, "qkv"), cu_seqlens.numel() - 1, n_qblocks, _ptr(qkv),
               _ptr(cu_seqlens), _ptr(qblock_off), _ptr(out), _stream(dev))
     return out
+
+
+def pool_rows(pooler: str, table: torch.Tensor, off: torch.Tensor) -> torch.Tensor:
+    """Pool consecutive rows per segment (segment i = rows off[i]..off[i+1]-1):
+    users [n_seg, 1024] f32 ("mean" = average_pool, "latent" = + F.normalize,
+    "final" = FinalAttention pooling of [x | exp(w)] rows)."""
+    dev = _dev(table, off)
+    if off.dtype != torch.int64 or not off.is_contiguous():
+        raise _lib.NewsRecHIPError("pool_rows: off must be contiguous int64")
+    n_seg = off.numel() - 1
+    users = torch.empty((n_seg, 1024), dtype=torch.float32, device=dev)
+    if n_seg == 0:
+        return users
+    _lib.call("nr_pool_score", POOLERS[pooler], _dtype(table, "table"), 1024, _ptr(table), _rowmajor(table, "table"),
+              None, 0, None, None, _ptr(off), None, None, n_seg, None, _ptr(users), _stream(dev))
+    return users
+
+
+_ENC_POOL = {"mean": _lib.NR_POOL_MEAN, "normalize": _lib.NR_POOL_LATENT, None: _lib.NR_POOL_NONE}
+
+
+def encoder_forward(layers, emb: dict, ids: torch.Tensor, seq_lens: torch.Tensor, n_tokens: int,
+                    pool: Optional[str] = "mean", want_hidden: bool = False, eps: float = 1e-5,
+                    workspace: Optional[torch.Tensor] = None, status: Optional[torch.Tensor] = None):
+    """Whole XLM-R forward through ``nr_encoder_forward`` (one C-ABI call).
+
+    layers: a ctypes array of ``_lib.EncoderLayer``; emb: word / pos / type
+    embedding tensors (dtype of the weights) and LN gamma / beta (f32); ids
+    int32 [n_tokens] and seq_lens int32 [n_seq] on the device.  Returns
+    (pooled [n_seq, 1024] f32 or None, hidden [n_tokens, 1024] or None)."""
+    dev = _dev(ids, seq_lens, emb["word"], workspace, status)
+    if ids.dtype != torch.int32 or seq_lens.dtype != torch.int32 or not ids.is_contiguous():
+        raise _lib.NewsRecHIPError("encoder_forward: ids / seq_lens must be contiguous int32")
+    dt = _dtype(emb["word"], "word")
+    n_seq = seq_lens.numel()
+    pooled = torch.empty((n_seq, 1024), dtype=torch.float32, device=dev) if pool else None
+    hidden = torch.empty((n_tokens, 1024), dtype=emb["word"].dtype, device=dev) if want_hidden else None
+    need = _lib.load().nr_encoder_workspace_bytes(dt, n_tokens, n_seq)
+    if workspace is None or workspace.numel() * workspace.element_size() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=dev)
+    _lib.call("nr_encoder_forward", dt, len(layers), ctypes.cast(layers, ctypes.c_void_p) if len(layers) else None,
+              _ptr(emb["word"]), emb["word"].shape[0], _ptr(emb["pos"]), emb["pos"].shape[0], _ptr(emb["type"]),
+              _ptr(emb["ln_g"]), _ptr(emb["ln_b"]), ctypes.c_float(eps), n_seq, n_tokens, _ptr(seq_lens), _ptr(ids),
+              _ENC_POOL[pool], _ptr(pooled), _ptr(hidden), _ptr(status), _ptr(workspace), need, _stream(dev))
+    return pooled, hidden
 
 
 # ------------------------------------------------------------------ training step (config 5)

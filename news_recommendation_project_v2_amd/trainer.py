@@ -69,21 +69,43 @@ class AttentionAttentionTrainer:
                           hist_off=torch.as_tensor(hoff).to(d), pos=torch.as_tensor(pos).to(d),
                           neg=torch.as_tensor(neg).to(d))
 
+    NAN_CHECK_EVERY = 64  # batches between host checks of the device-side losses
+
     def train_one_epoch(self) -> float:
+        """trainer.py:1030-1117.  The reference syncs on every loss and stops the
+        epoch after the first NaN batch (whose optimizer step it has already
+        applied, :1069-1072).  Here losses stay on the device and are checked
+        every NAN_CHECK_EVERY batches, so up to that many further steps may run
+        after a NaN.  The results are the same: a NaN loss means NaN gradients,
+        the clipped AdamW step of that batch already makes every parameter NaN in
+        both implementations, and the epoch loss sums exactly the batches before
+        the first NaN, like the reference's running_loss."""
         self.token_attention_model.train()
         self.final_attention_model.train()
         running_loss, running_count = 0.0, 0
-        losses = []
+        pending: list = []
+        stop = False
+
+        def drain() -> bool:
+            nonlocal running_loss, running_count
+            for loss, n in pending:
+                v = float(loss.item()) if not isinstance(loss, float) else loss
+                if math.isnan(v):
+                    print("Nan loss found. Please check")
+                    return True
+                running_loss += v * n
+                running_count += n
+            pending.clear()
+            return False
+
         for lo, hi in self.train_dataset.batches():
             batch = self.device_batch(lo, hi)
-            losses.append((self.engine.step(batch), hi - lo))
-        for loss, n in losses:  # one sync at the end of the epoch
-            v = float(loss.item()) if not isinstance(loss, float) else loss
-            if math.isnan(v):
-                print("Nan loss found. Please check")
+            pending.append((self.engine.step(batch), hi - lo))
+            if len(pending) >= self.NAN_CHECK_EVERY and drain():
+                stop = True
                 break
-            running_loss += v * n
-            running_count += n
+        if not stop:
+            drain()
         self._invalidate_eval_cache()
         return running_loss / max(running_count, 1)
 

@@ -98,14 +98,68 @@ def pooled_history(pooler: str, sd: dict, hist_idx: np.ndarray, hist_len: np.nda
 
 
 def cos_sim_scores(pooler: str, sd: dict, hist_idx, hist_len, cand_idx, cand_len, table: torch.Tensor,
-                   batch_size: int = 128, return_users: bool = False):
-    """get_cos_sim_scores: pooled users, then per-impression cosine."""
-    users = pooled_history(pooler, sd, hist_idx, hist_len, table, batch_size)
+                   batch_size: int = 128, return_users: bool = False, query_table=None):
+    """get_cos_sim_scores: pooled users (from query_table when given,
+    data_model_helper.py:189-196), then per-impression cosine against `table`."""
+    users = pooled_history(pooler, sd, hist_idx, hist_len, table if query_table is None else query_table,
+                           batch_size)
     res = []
     with torch.no_grad():
         for i, sub in enumerate(group(np.asarray(cand_idx), np.asarray(cand_len))):
             res.append(F.cosine_similarity(users[i], table[torch.as_tensor(sub, dtype=torch.long)]))
     scores = torch.cat(res) if res else torch.zeros(0)
+    return (scores, users) if return_users else scores
+
+
+def per_news_tables(pooler: str, sd: dict, table: torch.Tensor, chunk: int = 2048):
+    """The pooler's per-item math once per news row (the reference
+    runs it per padded history slot; every valid slot of news j computes the
+    same row): FinalAttention -> (x, exp(w)) rows of modeling_utils.py:218-224;
+    Latent -> the hiddens of latent_attention.py:157-163."""
+    outs = []
+    with torch.no_grad():
+        for s in range(0, table.shape[0], chunk):
+            e = table[s:s + chunk].unsqueeze(1)  # [n, 1, D]: one slot per row
+            if pooler == "final":
+                x = F.linear(F.relu(F.linear(F.relu(F.linear(e, sd["linear1.weight"], sd["linear1.bias"])),
+                                             sd["linear2.weight"], sd["linear2.bias"])),
+                             sd["linear3.weight"], sd["linear3.bias"])
+                w = F.linear(F.relu(F.linear(x, sd["linear4.weight"], sd["linear4.bias"])), sd["linear5.weight"])
+                outs.append(torch.cat([x, torch.exp(w)], dim=-1)[:, 0])
+            else:
+                outs.append(latent_hiddens(sd, e)[:, 0])
+    return torch.cat(outs)
+
+
+def cos_sim_scores_per_news(pooler: str, sd: dict, hist_idx, hist_len, cand_idx, cand_len, table: torch.Tensor,
+                            query_table=None, return_users: bool = False):
+    """get_cos_sim_scores restated per unique news (fast oracle for large
+    checks): per-news tables, then the masked reductions of the poolers
+    (FinalAttention: sum x p / (sum p + 1e-10), modeling_utils.py:224-228;
+    Latent: normalize(mean), latent_attention.py:165-170) and F.cosine_similarity
+    (data_model_helper.py:223-227).  Equal to cos_sim_scores up to f32
+    summation order (pinned against the reference golden in
+    tests/test_oracle_golden.py)."""
+    src = table if query_table is None else query_table
+    hist_idx = torch.as_tensor(np.asarray(hist_idx, dtype=np.int64))
+    hl = torch.as_tensor(np.asarray(hist_len, dtype=np.int64))
+    seg = torch.repeat_interleave(torch.arange(len(hl)), hl)
+    n = len(hl)
+    with torch.no_grad():
+        uniq, inv = torch.unique(hist_idx, return_inverse=True)
+        tab = per_news_tables(pooler, sd, src[uniq])
+        rows = tab[inv]
+        if pooler == "final":
+            x, p = rows[:, :1024], rows[:, 1024:]
+            num = torch.zeros(n, 1024).index_add_(0, seg, x * p)
+            den = torch.zeros(n, 1024).index_add_(0, seg, p)
+            users = num / (den + 1e-10)
+        else:
+            s = torch.zeros(n, 1024).index_add_(0, seg, rows)
+            users = F.normalize(s / hl.unsqueeze(1).float(), p=2, dim=-1)
+        ci = torch.as_tensor(np.asarray(cand_idx, dtype=np.int64))
+        cseg = torch.repeat_interleave(torch.arange(n), torch.as_tensor(np.asarray(cand_len, dtype=np.int64)))
+        scores = F.cosine_similarity(users[cseg], table[ci], dim=-1)
     return (scores, users) if return_users else scores
 
 

@@ -67,7 +67,9 @@ class SyntheticEmbeddings:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--data-dir", type=Path, default=Path("data"))
-    ap.add_argument("--emb-dir", type=Path, default=Path("new_embeddings"))
+    ap.add_argument("--emb-dir", type=Path, default=None,
+                    help="tables {split}.pt (default new_embeddings/; with --synthetic: random tables unless given, "
+                         "e.g. the save_emb.py --synthetic output)")
     ap.add_argument("--ckpt", type=Path, default=None, help="pooler state_dict (default: models/final_attn/Epoch_5.pt)")
     ap.add_argument("--pooler", choices=["final", "latent"], default="final")
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
@@ -108,13 +110,14 @@ def main():
         split = NewsDataset[name]
         if args.synthetic:
             ctx = synthetic_context(split, args.num_impressions or 2000, seed=1234 + i)
-            loader = SyntheticEmbeddings(1234 + i)
+            # the save_emb.py --synthetic tables of the same split / impressions when given (config 2)
+            loader = LoadEmbeddingComponent(args.emb_dir) if args.emb_dir else SyntheticEmbeddings(1234 + i)
         else:
             from news_recommendation_project_v2_amd.data_utils import load_dataset
             beh, feats = load_dataset(args.data_dir, split, num_samples=args.num_impressions,
                                       data_subset=DataSubset.WITH_HISTORY, random_state=rng)
             ctx = {"news_dataset": split, "behaviors": beh, **feats}
-            loader = LoadEmbeddingComponent(args.emb_dir)
+            loader = LoadEmbeddingComponent(args.emb_dir or Path("new_embeddings"))
         steps = [("init_transform", TransformData()), ("load_embedding", loader)]
         if world == 1:
             steps.append(("final_attn_comp", comp))

@@ -61,8 +61,9 @@ class SyntheticEmbeddingsComponent(PipelineComponent):
         p_ids, p_lens = synthetic_titles(n, self.seed, self.vocab, 20)
         q_ids, q_lens = synthetic_titles(n, self.seed, self.vocab, 20, prefix_len=26)
         new = ctx.copy()
-        new["news_embeddings"] = self.encoder.encode_packed(p_ids, p_lens).cpu()
-        new["query_news_embeddings"] = self.encoder.encode_packed(q_ids, q_lens).cpu()
+        # e5-instruct branch of get_embeddings (data_model_helper.py:59-80): both passes normalised
+        new["news_embeddings"] = self.encoder.encode_packed(p_ids, p_lens, normalize=True).cpu()
+        new["query_news_embeddings"] = self.encoder.encode_packed(q_ids, q_lens, normalize=True).cpu()
         dt = time.time() - t0
         tok = int(p_lens.sum() + q_lens.sum())
         print(f"[save_emb] {ctx['news_dataset'].value}: {n} news, {tok} tokens in {dt:.2f}s "

@@ -41,3 +41,20 @@ def test_library_exports_every_header_symbol():
     assert rc == -1 and b"dtype" in loaded.nr_last_error()
     rc = loaded.nr_pool_score(0, 0, 512, None, 0, None, 0, None, None, None, None, None, 1, None, None, None)
     assert rc == -3 and b"dim" in loaded.nr_last_error()
+
+
+def test_encoder_forward_validates_on_the_host():
+    if not _lib.LIB_PATH.is_file():
+        pytest.skip("libnewsrec_hip.so not built (run __graft_entry__.build())")
+    lib = _lib.load()
+    assert ctypes.sizeof(_lib.EncoderLayer) == 12 * ctypes.sizeof(ctypes.c_void_p)
+    rc = lib.nr_encoder_forward(9, 0, None, None, 1, None, 514, None, None, None, 1e-5, 1, 4, None, None,
+                                _lib.NR_POOL_MEAN, None, None, None, None, 0, None)
+    assert rc == -1 and b"dtype" in lib.nr_last_error()
+    rc = lib.nr_encoder_forward(_lib.NR_F32, 0, None, None, 1, None, 514, None, None, None, 1e-5, 1, 4, None, None,
+                                7, None, None, None, None, 0, None)
+    assert rc == -1 and b"pool" in lib.nr_last_error()
+    assert lib.nr_encoder_workspace_bytes(_lib.NR_BF16, 1000, 10) > 1000 * 1024 * 2 * 7
+    rc = lib.nr_pool_score(_lib.NR_POOL_MEAN, 0, 1024, None, 1024, None, 0, None, None, None, None, None, 1, None, None,
+                           None)
+    assert rc == -1 and b"null" in lib.nr_last_error()

@@ -53,6 +53,10 @@ def test_pool_oracle_matches_reference(pooler):
                                             table, return_users=True)
     np.testing.assert_allclose(scores.numpy(), g["scores"], rtol=0, atol=1e-6)
     np.testing.assert_allclose(users.numpy(), g["users"], rtol=0, atol=1e-5)
+    qtable = W.news_table(int(g["query_table_seed"]), int(g["n_news"]), 1024, name=str(g["query_table_name"]))
+    s2 = pool_ref.cos_sim_scores(pooler, sd, g["hist_idx"], g["hist_len"], g["cand_idx"], g["cand_len"], table,
+                                 query_table=qtable)
+    np.testing.assert_allclose(s2.numpy(), g["scores_2tab"], rtol=0, atol=1e-6)
     ranks = pool_ref.dense_ranks(scores.numpy(), g["cand_len"])
     for a, b in zip(ranks, unflat(g["fs_ranks_flat"], g["fs_ranks_len"])):
         np.testing.assert_array_equal(a, b)
@@ -61,6 +65,25 @@ def test_pool_oracle_matches_reference(pooler):
         with torch.no_grad():
             out = pool_ref.latent_hiddens(sd, table[rows])
         np.testing.assert_allclose(out.numpy(), g["unpooled_out"], rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("pooler", ["final", "latent"])
+def test_per_news_oracle_matches_reference(pooler):
+    """The fast per-unique-news oracle (used for the large GPU parity checks)
+    against the reference's padded-batch outputs, one table and two tables."""
+    g = golden(f"pool_{pooler}")
+    sd = (W.final_attention_state_dict(int(g["weight_seed"])) if pooler == "final"
+          else W.latent_attention_state_dict(int(g["weight_seed"]), ln_random=True))
+    table = W.news_table(1234, int(g["n_news"]), 1024, name=str(g["table_name"]))
+    scores, users = pool_ref.cos_sim_scores_per_news(pooler, sd, g["hist_idx"], g["hist_len"], g["cand_idx"],
+                                                     g["cand_len"], table, return_users=True)
+    np.testing.assert_allclose(scores.numpy(), g["scores"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(users.numpy(), g["users"], rtol=0, atol=1e-5)
+    qtable = W.news_table(int(g["query_table_seed"]), int(g["n_news"]), 1024, name=str(g["query_table_name"]))
+    s2 = pool_ref.cos_sim_scores_per_news(pooler, sd, g["hist_idx"], g["hist_len"], g["cand_idx"], g["cand_len"],
+                                          table, query_table=qtable)
+    np.testing.assert_allclose(s2.numpy(), g["scores_2tab"], rtol=0, atol=1e-6)
+    assert np.abs(g["scores_2tab"] - g["scores"]).max() > 1e-2  # the query table matters
 
 
 def test_token_attn_oracle_matches_reference():
