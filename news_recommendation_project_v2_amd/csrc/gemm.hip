@@ -682,6 +682,409 @@ __global__ __launch_bounds__(512, 2) void gemm256p_group_kernel(GemmGroup g) {
                                            nullptr, nullptr, 0, (TO*)g.C[p], g.ldc[p], EpiArgs{0, 0, 1.f});
 }
 
+// ---------------------------------------------------------------------------
+// Persistent bf16 -> bf16 GEMM with a register-direct epilogue (the default
+// for bf16 operands and bf16 output: every per-news transform GEMM and the
+// bf16 encoder).  One 512-thread workgroup per CU walks its share of the
+// 256x256 output tiles (8 XCD-contiguous ranges, the grouped tile order of
+// tile_of), so a CU never idles between tiles waiting for a new workgroup.
+// The main loop is gemm256p_body's 4-phase pipeline with the MFMA operands
+// swapped (acc = W fragment x A fragment): the 16x16 accumulator of lane l
+// then holds C[row l & 15][cols 4 (l >> 4) .. +3], four consecutive columns of
+// one row, which leave as ONE 8-byte store straight from registers (no LDS
+// slab, no workgroup barrier in the epilogue).  Tile boundary: the epilogue's
+// bias / residual loads are issued, then the next tile's prologue DMAs, then
+// the epilogue computes and stores while those DMAs land; the next tile waits
+// vmcnt(stores [+ its 4 stage-1 DMAs]) — one counter retires in issue order —
+// so the stores drain under the next tile's first MFMA phases.
+template <int EPI>
+struct PersistCfg {
+  static constexpr int kStores = EPI == NR_EPI_GEGLU ? 16 : 32;  // 8-B stores per lane per tile
+  static constexpr bool kR = EPI == NR_EPI_RESADD || EPI == NR_EPI_DRELU;
+};
+
+// Epilogue loads hidden from hipcc's vmcnt bookkeeping (see gemm256t_kernel),
+// and the matching hand-counted wait, which names the loaded registers as
+// read-write operands so no consumer is scheduled above it (guide §5.7 (ii)).
+__device__ __forceinline__ float asm_load_f32(const float* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ uint2 asm_load_b64(const void* p) {
+  uint2 v;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+template <int N, bool HR>
+__device__ __forceinline__ void wait_vm(f32x4 (&bv)[4], uint2 (&rv)[2][4]) {
+  if constexpr (HR)
+    asm volatile("s_waitcnt vmcnt(%c[n])"
+                 : "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]), "+v"(rv[0][0]), "+v"(rv[0][1]),
+                   "+v"(rv[0][2]), "+v"(rv[0][3]), "+v"(rv[1][0]), "+v"(rv[1][1]), "+v"(rv[1][2]), "+v"(rv[1][3])
+                 : [n] "i"(N)
+                 : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%c[n])" : "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]) : [n] "i"(N) : "memory");
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)a) |
+         ((uint32_t)__builtin_bit_cast(unsigned short, (__bf16)b) << 16);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, int64_t K,
+                                                          const __bf16* __restrict__ A, int64_t lda,
+                                                          const __bf16* __restrict__ W, int64_t ldw,
+                                                          const float* __restrict__ bias, const __bf16* R,
+                                                          int64_t ldr, __bf16* C, int64_t ldc, EpiArgs ea,
+                                                          int ntn, int ntm, int n_tiles) {
+  typedef __bf16 TI;
+  constexpr int BK = 64, CE = 8;
+  constexpr int NST = PersistCfg<EPI>::kStores;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int wmu = __builtin_amdgcn_readfirstlane(wm);
+  const int64_t nk = K / BK;
+
+  // tile schedule: XCD group x = blockIdx % 8 owns a contiguous range of tile
+  // ids; its ~32 workgroups run consecutive ids, which tile_of groups into
+  // 4 M-tiles x 8 N-tiles sharing A and W panels in that XCD's L2
+  const int G = (int)gridDim.x;
+  int t, t_end, t_step;
+  if (G % 8 == 0) {
+    const int x = (int)blockIdx.x & 7, li = (int)blockIdx.x >> 3;
+    const int qq = n_tiles >> 3, rr = n_tiles & 7;
+    const int lo = x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq;
+    t = lo + li;
+    t_end = lo + qq + (x < rr ? 1 : 0);
+    t_step = G >> 3;
+  } else {
+    t = (int)blockIdx.x;
+    t_end = n_tiles;
+    t_step = G;
+  }
+  if (t >= t_end) return;  // workgroup-uniform
+
+  int64_t m0 = 0, n0 = 0;
+  auto setup = [&](int tile) {
+    int mt, nt;
+    tile_of(tile, ntn, ntm, ea.group_m, mt, nt);
+    m0 = (int64_t)mt * G2BM;
+    n0 = (int64_t)nt * G2BN;
+  };
+  // DMA sources recomputed per issue from (m0, n0): lane l of wave w fills row
+  // 128h + 16w + 8j + l/8, 16-B chunk (l & 7) ^ ((row >> 1) & 7) of the image
+  const int rl = 16 * wave + (lane >> 3);
+  auto cj = [&](int j) { return (lane & 7) ^ ((4 * j + (lane >> 4)) & 7); };
+  auto dmaA = [&](int h, int stage, int64_t kt) {
+    unsigned char* sa = smem + stage * G2_STAGE;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t row = min(m0 + 128 * h + 8 * j + rl, M - 1);
+      const TI* src = A + row * lda + cj(j) * CE + kt * BK;
+      __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(sa + (128 * h + 16 * wave + 8 * j) * 128), 16, 0, 0);
+    }
+  };
+  auto dmaB = [&](int h, int stage, int64_t kt) {
+    unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const TI* src = W + (n0 + 128 * h + 8 * j + rl) * ldw + cj(j) * CE + kt * BK;
+      __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(sb + (128 * h + 16 * wave + 8 * j) * 128), 16, 0, 0);
+    }
+  };
+  auto prologue = [&]() {  // 8 DMAs (stage 0) + 4 (stage 1's B halves) per wave
+    dmaB(0, 0, 0);
+    dmaB(1, 0, 0);
+    dmaA(0, 0, 0);
+    dmaA(1, 0, 0);
+    if (nk > 1) {
+      dmaB(0, 1, 1);
+      dmaB(1, 1, 1);
+    }
+  };
+
+  // fragment reads (16x16x32 operand map: row lane & 15, k chunk 4 f + lane / 16)
+  const int c16 = lane & 15, q4 = lane >> 4;
+  const int sw = (c16 >> 1) & 7;
+  const int abase = (wm * 128 + c16) * 128;
+  const int bbase = G2BM * 128 + (wn * 64 + c16) * 128;
+  const int cf0 = ((0 + q4) ^ sw) << 4, cf1 = ((4 + q4) ^ sw) << 4;
+  typedef f32x4 frag_t;
+  frag_t fa[4][2], fb0[2][2], fb1[2][2];
+  f32x4 acc[8][4];
+  auto readA = [&](int stage, int qm) {
+    const unsigned char* sp = smem + stage * G2_STAGE + abase + qm * 4 * 2048;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa[i][0] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf0);
+      fa[i][1] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf1);
+    }
+  };
+  auto readB = [&](int stage, int qn, frag_t (&fb)[2][2]) {
+    const unsigned char* sp = smem + stage * G2_STAGE + bbase + qn * 2 * 2048;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      fb[j][0] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf0);
+      fb[j][1] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf1);
+    }
+  };
+  // swapped operands: D[n][m] = sum_k W[n][k] A[m][k] = C[m][n]
+  auto mma = [&](int qm, int qn, const frag_t (&fb)[2][2]) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * qm + i][2 * qn + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, fb[j][f]), __builtin_bit_cast(bf16x8, fa[i][f]), acc[4 * qm + i][2 * qn + j],
+              0, 0, 0);
+  };
+#define NR_PHASE_SYNC_MMA(QM, NI, FB)                   \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
+  __builtin_amdgcn_sched_barrier(0);                   \
+  __builtin_amdgcn_s_barrier();                        \
+  __builtin_amdgcn_s_setprio(1);                       \
+  mma(QM, NI, FB);                                     \
+  __builtin_amdgcn_s_setprio(0);                       \
+  __builtin_amdgcn_s_barrier();
+
+  setup(t);
+  prologue();
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bool first = true, drain_all = false;
+  while (true) {
+    if (!first) {
+      // the previous tile's NST stores were issued after this tile's prologue
+      // DMAs: waiting for all but the youngest NST (+ 4 stage-1 DMAs) lands stage 0
+      if (drain_all) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (nk > 1) {
+        if constexpr (NST == 32) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      } else {
+        if constexpr (NST == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      }
+    }
+    first = false;
+    __builtin_amdgcn_s_barrier();
+    if (wmu == 1) __builtin_amdgcn_s_barrier();  // stagger the wave groups
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[mi][ni][r] = 0.f;
+    for (int64_t kt = 0; kt < nk; ++kt) {
+      const int st = (int)(kt & 1), ns = st ^ 1;
+      const bool pre1 = kt + 1 < nk, pre2 = kt + 2 < nk;
+      readA(st, 0);
+      readB(st, 0, fb0);
+      if (pre1) dmaA(0, ns, kt + 1);
+      NR_PHASE_SYNC_MMA(0, 0, fb0)
+      readB(st, 1, fb1);
+      if (pre1) dmaA(1, ns, kt + 1);
+      NR_PHASE_SYNC_MMA(0, 1, fb1)
+      readA(st, 1);
+      if (pre2) dmaB(0, st, kt + 2);
+      NR_PHASE_SYNC_MMA(1, 1, fb1)
+      if (pre2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (pre2) dmaB(1, st, kt + 2);
+      __builtin_amdgcn_s_setprio(1);
+      mma(1, 0, fb0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+    }
+    if (wmu == 0) __builtin_amdgcn_s_barrier();  // re-align the groups: every stage read is retired
+
+    // ---------------- epilogue of tile (m0, n0) ----------------
+    // Loads are inline asm (hipcc would otherwise wait vmcnt(0) before their
+    // first use while LDS-DMAs fly, draining the next tile's prologue); their
+    // completion is counted here by hand, in issue order:
+    //   bias (16), R rows mi 0-1 (8), prologue DMAs (NP), then per mi: wait,
+    //   compute, stores S_mi, R rows mi + 2 (R epilogues only)
+    const int64_t em0 = m0, en0 = n0;
+    const int64_t row0 = em0 + wm * 128 + c16;      // + 16 mi
+    const int64_t col0 = en0 + wn * 64 + 4 * q4;    // + 16 ni
+    constexpr bool HR = PersistCfg<EPI>::kR;
+    f32x4 bv[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      if (bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bv[ni][r] = asm_load_f32(bias + col0 + 16 * ni + r);
+      } else {
+        bv[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    uint2 rv[2][4];  // R rows of mi (ring of 2), R epilogues only
+    auto loadR = [&](int mi) {
+      const int64_t row = min(row0 + 16 * mi, M - 1);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) rv[mi & 1][ni] = asm_load_b64(R + row * ldr + col0 + 16 * ni);
+    };
+    if constexpr (HR) {
+      loadR(0);
+      loadR(1);
+    }
+    const int tn = t + t_step;
+    const bool more = tn < t_end;
+    const int np = more ? (nk > 1 ? 12 : 8) : 0;  // prologue DMAs issued below
+    if (more) {  // the next tile's operands fly while this tile's epilogue runs
+      setup(tn);
+      prologue();
+    }
+    const bool ragged = em0 + G2BM > M;  // some stores are skipped: exact counts do not hold
+    // bias (and R rows 0) landed: everything but the NP DMAs (+ R rows 1) done
+    if (ragged) wait_vm<0, HR>(bv, rv);
+    else if constexpr (HR) {
+      if (np == 12) wait_vm<16, HR>(bv, rv); else if (np == 8) wait_vm<12, HR>(bv, rv); else wait_vm<4, HR>(bv, rv);
+    } else {
+      if (np == 12) wait_vm<12, HR>(bv, rv); else if (np == 8) wait_vm<8, HR>(bv, rv); else wait_vm<0, HR>(bv, rv);
+    }
+    drain_all = ragged;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int64_t row = row0 + 16 * mi;
+      if constexpr (HR) {
+        if (mi >= 1) {  // R rows mi landed; younger: stores of mi-1 (4), R rows mi+1 (4, mi <= 6) [+ NP at mi 1]
+          if (ragged) wait_vm<0, HR>(bv, rv);
+          else if (mi == 1) {
+            if (np == 12) wait_vm<20, HR>(bv, rv); else if (np == 8) wait_vm<16, HR>(bv, rv); else wait_vm<8, HR>(bv, rv);
+          } else if (mi <= 6) wait_vm<8, HR>(bv, rv);
+          else wait_vm<4, HR>(bv, rv);
+        }
+      }
+      if constexpr (EPI == NR_EPI_GEGLU) {
+        // W rows interleaved in 32-row (a, g) blocks: ni 0, 1 = a, ni 2, 3 = g
+        const int64_t ocol = (en0 + wn * 64) / 2 + 4 * q4;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (acc[mi][ni][r] + bv[ni][r]) * gelu_erf(acc[mi][ni + 2][r] + bv[ni + 2][r]);
+          if (row < M)
+            *reinterpret_cast<uint2*>(C + row * ldc + ocol + 16 * ni) = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one row group at a time: bounds the erf temporaries' live ranges
+      } else {
+        float v[4][4];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = acc[mi][ni][r] + bv[ni][r];
+            if constexpr (EPI == NR_EPI_RELU) x = fmaxf(x, 0.f);
+            if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
+              const uint64_t gi = (uint64_t)(row * N + col0 + 16 * ni + r);
+              x = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(x, 0.f) * ea.scale;
+            }
+            if constexpr (EPI == NR_EPI_EXP) x = expf(x);
+            if constexpr (EPI == NR_EPI_GELU) x = gelu_erf(x);
+            if constexpr (HR) {
+              const uint32_t w2 = r < 2 ? rv[mi & 1][ni].x : rv[mi & 1][ni].y;
+              const float rr = (r & 1) ? bf16_hi(w2) : bf16_lo(w2);
+              if constexpr (EPI == NR_EPI_RESADD) x += rr;
+              else x = rr > 0.f ? acc[mi][ni][r] * ea.scale : 0.f;  // DRELU: no bias
+            }
+            v[ni][r] = x;
+          }
+        if constexpr (EPI == NR_EPI_SOFTMAX64) {
+          // the wave's 64 columns are one softmax group; row (l & 15)'s values
+          // sit in lanes l, l ^ 16, l ^ 32, l ^ 48 (4 x 4 each)
+          float mx = v[0][0];
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mx = fmaxf(mx, v[ni][r]);
+          mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+          mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+          float sum = 0.f;
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[ni][r] = expf(v[ni][r] - mx);
+              sum += v[ni][r];
+            }
+          sum += __shfl_xor(sum, 16, 64);
+          sum += __shfl_xor(sum, 32, 64);
+          const float inv = 1.0f / sum;
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[ni][r] *= inv;
+        }
+        if (row < M) {
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            *reinterpret_cast<uint2*>(C + row * ldc + col0 + 16 * ni) =
+                uint2{pack_bf16x2(v[ni][0], v[ni][1]), pack_bf16x2(v[ni][2], v[ni][3])};
+        }
+        if constexpr (HR) {
+          if (mi + 2 < 8) loadR(mi + 2);
+        }
+      }
+    }
+    if (!more) break;
+    t = tn;
+  }
+#undef NR_PHASE_SYNC_MMA
+}
+
+static int num_cus() {
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    const int n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                      ? prop.multiProcessorCount : 256;
+    n_cu = n >= 8 ? n / 8 * 8 : 8;
+  }
+  return n_cu;
+}
+
+static int launch_gemm256_t(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W,
+                            int64_t ldw, const float* bias, const void* R, int64_t ldr, void* C, int64_t ldc,
+                            const EpiArgs& ea, hipStream_t s) {
+  const int ntn = (int)(N / G2BN);
+  const int64_t ntm = (M + G2BM - 1) / G2BM;
+  const int64_t tiles = ntm * ntn;
+  if (tiles > (1ll << 30)) {
+    set_error("nr_gemm: too many tiles");
+    return NR_ERR_UNSUPPORTED;
+  }
+  const int nt = (int)tiles, ncu = num_cus();
+  const dim3 grid((unsigned)(nt < ncu ? nt : ncu));
+  const __bf16* a = (const __bf16*)A;
+  const __bf16* w = (const __bf16*)W;
+  const __bf16* r = (const __bf16*)R;
+  __bf16* c = (__bf16*)C;
+#define NR_T(E) hipLaunchKernelGGL((gemm256t_kernel<E>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea, ntn, (int)ntm, nt)
+  switch (epi) {
+    case NR_EPI_NONE: NR_T(NR_EPI_NONE); break;
+    case NR_EPI_RELU: NR_T(NR_EPI_RELU); break;
+    case NR_EPI_EXP: NR_T(NR_EPI_EXP); break;
+    case NR_EPI_GEGLU: NR_T(NR_EPI_GEGLU); break;
+    case NR_EPI_RESADD: NR_T(NR_EPI_RESADD); break;
+    case NR_EPI_GELU: NR_T(NR_EPI_GELU); break;
+    case NR_EPI_RELU_DROPOUT: NR_T(NR_EPI_RELU_DROPOUT); break;
+    case NR_EPI_DRELU: NR_T(NR_EPI_DRELU); break;
+    case NR_EPI_SOFTMAX64: NR_T(NR_EPI_SOFTMAX64); break;
+    default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
+  }
+#undef NR_T
+  NR_CHECK_LAUNCH("nr_gemm");
+  return NR_OK;
+}
+
 template <typename TI, typename TO>
 static int launch_gemm256_p(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                           const void* W, int64_t ldw, const float* bias, const void* R, int64_t ldr,
@@ -743,6 +1146,7 @@ static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* 
                           void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
   EpiArgs eg = ea;
   eg.group_m = kGemmGroupM;
+  if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) return launch_gemm256_t(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
   if constexpr (sizeof(TI) == 2) return launch_gemm256_p16<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
   return launch_gemm256_p<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
 }
