@@ -716,16 +716,41 @@ __device__ __forceinline__ uint2 asm_load_b64(const void* p) {
   asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
   return v;
 }
-template <int N, bool HR>
-__device__ __forceinline__ void wait_vm(f32x4 (&bv)[4], uint2 (&rv)[2][4]) {
+// s_waitcnt vmcnt(C[sel]) for a wave-uniform sel in {0, 1, 2}, as ONE asm
+// statement (a compiler-level branch between waits would make the register
+// allocator copy the loaded registers at the merge, reading them before the
+// data lands).  It names every register the epilogue's asm loads write, each
+// as the very variable the load returned, so no consumer is scheduled above it.
+#define NR_WAIT_SEL_ASM                                                                  \
+  "s_cmp_eq_u32 %[sel], 0\n\ts_cbranch_scc1 .Lnrw0_%=\n\ts_cmp_eq_u32 %[sel], 1\n\t"  \
+  "s_cbranch_scc1 .Lnrw1_%=\n\ts_waitcnt vmcnt(%c[c2])\n\ts_branch .Lnrwe_%=\n"        \
+  ".Lnrw0_%=:\n\ts_waitcnt vmcnt(%c[c0])\n\ts_branch .Lnrwe_%=\n"                     \
+  ".Lnrw1_%=:\n\ts_waitcnt vmcnt(%c[c1])\n.Lnrwe_%=:"
+template <int C0, int C1, int C2, bool HR>
+__device__ __forceinline__ void wait_sel(int sel, float (&bs)[16], uint2 (&rv)[2][4]) {
   if constexpr (HR)
-    asm volatile("s_waitcnt vmcnt(%c[n])"
-                 : "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]), "+v"(rv[0][0]), "+v"(rv[0][1]),
-                   "+v"(rv[0][2]), "+v"(rv[0][3]), "+v"(rv[1][0]), "+v"(rv[1][1]), "+v"(rv[1][2]), "+v"(rv[1][3])
-                 : [n] "i"(N)
-                 : "memory");
+    asm volatile(NR_WAIT_SEL_ASM
+                 : "+v"(bs[0]), "+v"(bs[1]), "+v"(bs[2]), "+v"(bs[3]), "+v"(bs[4]), "+v"(bs[5]), "+v"(bs[6]),
+                   "+v"(bs[7]), "+v"(bs[8]), "+v"(bs[9]), "+v"(bs[10]), "+v"(bs[11]), "+v"(bs[12]), "+v"(bs[13]),
+                   "+v"(bs[14]), "+v"(bs[15]), "+v"(rv[0][0]), "+v"(rv[0][1]), "+v"(rv[0][2]), "+v"(rv[0][3]),
+                   "+v"(rv[1][0]), "+v"(rv[1][1]), "+v"(rv[1][2]), "+v"(rv[1][3])
+                 : [sel] "s"(sel), [c0] "i"(C0), [c1] "i"(C1), [c2] "i"(C2)
+                 : "memory", "scc");
   else
-    asm volatile("s_waitcnt vmcnt(%c[n])" : "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]) : [n] "i"(N) : "memory");
+    asm volatile(NR_WAIT_SEL_ASM
+                 : "+v"(bs[0]), "+v"(bs[1]), "+v"(bs[2]), "+v"(bs[3]), "+v"(bs[4]), "+v"(bs[5]), "+v"(bs[6]),
+                   "+v"(bs[7]), "+v"(bs[8]), "+v"(bs[9]), "+v"(bs[10]), "+v"(bs[11]), "+v"(bs[12]), "+v"(bs[13]),
+                   "+v"(bs[14]), "+v"(bs[15])
+                 : [sel] "s"(sel), [c0] "i"(C0), [c1] "i"(C1), [c2] "i"(C2)
+                 : "memory", "scc");
+}
+template <int C0, int C1, int C2>
+__device__ __forceinline__ void wait_sel_r(int sel, uint2 (&rv)[2][4]) {
+  asm volatile(NR_WAIT_SEL_ASM
+               : "+v"(rv[0][0]), "+v"(rv[0][1]), "+v"(rv[0][2]), "+v"(rv[0][3]), "+v"(rv[1][0]), "+v"(rv[1][1]),
+                 "+v"(rv[1][2]), "+v"(rv[1][3])
+               : [sel] "s"(sel), [c0] "i"(C0), [c1] "i"(C1), [c2] "i"(C2)
+               : "memory", "scc");
 }
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
@@ -857,13 +882,13 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   prologue();
   if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  bool first = true, drain_all = false;
+  bool first = true;
   while (true) {
     if (!first) {
-      // the previous tile's NST stores were issued after this tile's prologue
-      // DMAs: waiting for all but the youngest NST (+ 4 stage-1 DMAs) lands stage 0
-      if (drain_all) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else if (nk > 1) {
+      // the previous tile's NST stores (and its R loads, already retired) were
+      // issued after this tile's prologue DMAs: all but the youngest NST (+ the
+      // 4 stage-1 DMAs) retired => stage 0 has landed
+      if (nk > 1) {
         if constexpr (NST == 32) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
       } else {
@@ -908,22 +933,18 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     // Loads are inline asm (hipcc would otherwise wait vmcnt(0) before their
     // first use while LDS-DMAs fly, draining the next tile's prologue); their
     // completion is counted here by hand, in issue order:
-    //   bias (16), R rows mi 0-1 (8), prologue DMAs (NP), then per mi: wait,
-    //   compute, stores S_mi, R rows mi + 2 (R epilogues only)
+    //   bias (16), R rows of mi 0-1 (8), prologue DMAs (NP = 12 / 8 / 0), then
+    //   per mi: wait, compute, 4 stores, R rows of mi + 2 (R epilogues only).
+    // Rows past M are clamped to M - 1 everywhere (their A rows were clamped by
+    // the DMA too), so they compute row M - 1's exact bytes and store them
+    // there again: every wave issues the same store count on every tile.
     const int64_t em0 = m0, en0 = n0;
     const int64_t row0 = em0 + wm * 128 + c16;      // + 16 mi
     const int64_t col0 = en0 + wn * 64 + 4 * q4;    // + 16 ni
     constexpr bool HR = PersistCfg<EPI>::kR;
-    f32x4 bv[4];
+    float bs[16];
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      if (bias) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bv[ni][r] = asm_load_f32(bias + col0 + 16 * ni + r);
-      } else {
-        bv[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
+    for (int i = 0; i < 16; ++i) bs[i] = bias ? asm_load_f32(bias + col0 + 16 * (i >> 2) + (i & 3)) : 0.f;
     uint2 rv[2][4];  // R rows of mi (ring of 2), R epilogues only
     auto loadR = [&](int mi) {
       const int64_t row = min(row0 + 16 * mi, M - 1);
@@ -936,31 +957,26 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     }
     const int tn = t + t_step;
     const bool more = tn < t_end;
-    const int np = more ? (nk > 1 ? 12 : 8) : 0;  // prologue DMAs issued below
+    // wave-uniform selector of the prologue size: 0 = none, 1 = 8 DMAs, 2 = 12
+    const int sel = __builtin_amdgcn_readfirstlane(more ? (nk > 1 ? 2 : 1) : 0);
     if (more) {  // the next tile's operands fly while this tile's epilogue runs
       setup(tn);
       prologue();
     }
-    const bool ragged = em0 + G2BM > M;  // some stores are skipped: exact counts do not hold
-    // bias (and R rows 0) landed: everything but the NP DMAs (+ R rows 1) done
-    if (ragged) wait_vm<0, HR>(bv, rv);
-    else if constexpr (HR) {
-      if (np == 12) wait_vm<16, HR>(bv, rv); else if (np == 8) wait_vm<12, HR>(bv, rv); else wait_vm<4, HR>(bv, rv);
-    } else {
-      if (np == 12) wait_vm<12, HR>(bv, rv); else if (np == 8) wait_vm<8, HR>(bv, rv); else wait_vm<0, HR>(bv, rv);
-    }
-    drain_all = ragged;
+    // bias (+ R rows of mi 0) landed; younger: the NP DMAs (+ R rows of mi 1)
+    if constexpr (HR) wait_sel<4, 12, 16, true>(sel, bs, rv);
+    else wait_sel<0, 8, 12, false>(sel, bs, rv);
+    f32x4 bv[4];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bv[i >> 2][i & 3] = bs[i];
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
-      const int64_t row = row0 + 16 * mi;
+      const int64_t row = min(row0 + 16 * mi, M - 1);
       if constexpr (HR) {
-        if (mi >= 1) {  // R rows mi landed; younger: stores of mi-1 (4), R rows mi+1 (4, mi <= 6) [+ NP at mi 1]
-          if (ragged) wait_vm<0, HR>(bv, rv);
-          else if (mi == 1) {
-            if (np == 12) wait_vm<20, HR>(bv, rv); else if (np == 8) wait_vm<16, HR>(bv, rv); else wait_vm<8, HR>(bv, rv);
-          } else if (mi <= 6) wait_vm<8, HR>(bv, rv);
-          else wait_vm<4, HR>(bv, rv);
-        }
+        // R rows of mi landed; younger: stores of mi - 1 (4) + R rows of mi + 1 (4, mi <= 6) [+ NP at mi 1]
+        if (mi == 1) wait_sel_r<8, 16, 20>(sel, rv);
+        else if (mi >= 2 && mi <= 6) wait_sel_r<8, 8, 8>(sel, rv);
+        else if (mi == 7) wait_sel_r<4, 4, 4>(sel, rv);
       }
       if constexpr (EPI == NR_EPI_GEGLU) {
         // W rows interleaved in 32-row (a, g) blocks: ni 0, 1 = a, ni 2, 3 = g
@@ -970,8 +986,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           float o[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = (acc[mi][ni][r] + bv[ni][r]) * gelu_erf(acc[mi][ni + 2][r] + bv[ni + 2][r]);
-          if (row < M)
-            *reinterpret_cast<uint2*>(C + row * ldc + ocol + 16 * ni) = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+          *reinterpret_cast<uint2*>(C + row * ldc + ocol + 16 * ni) = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
         }
         __builtin_amdgcn_sched_barrier(0);  // one row group at a time: bounds the erf temporaries' live ranges
       } else {
@@ -1022,12 +1037,10 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[ni][r] *= inv;
         }
-        if (row < M) {
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-            *reinterpret_cast<uint2*>(C + row * ldc + col0 + 16 * ni) =
-                uint2{pack_bf16x2(v[ni][0], v[ni][1]), pack_bf16x2(v[ni][2], v[ni][3])};
-        }
+        for (int ni = 0; ni < 4; ++ni)
+          *reinterpret_cast<uint2*>(C + row * ldc + col0 + 16 * ni) =
+              uint2{pack_bf16x2(v[ni][0], v[ni][1]), pack_bf16x2(v[ni][2], v[ni][3])};
         if constexpr (HR) {
           if (mi + 2 < 8) loadR(mi + 2);
         }
