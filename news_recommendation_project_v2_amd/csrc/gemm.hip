@@ -699,63 +699,31 @@ __global__ __launch_bounds__(512, 2) void gemm256p_group_kernel(GemmGroup g) {
 // so the stores drain under the next tile's first MFMA phases.
 template <int EPI>
 struct PersistCfg {
-  static constexpr int kStores = EPI == NR_EPI_GEGLU ? 16 : 32;  // 8-B stores per lane per tile
-  static constexpr bool kR = EPI == NR_EPI_RESADD || EPI == NR_EPI_DRELU;
+  static constexpr int kStores = EPI == NR_EPI_GEGLU ? 8 : 16;  // 16-B stores per lane per tile
 };
 
-// Epilogue loads hidden from hipcc's vmcnt bookkeeping (see gemm256t_kernel),
-// and the matching hand-counted wait, which names the loaded registers as
-// read-write operands so no consumer is scheduled above it (guide §5.7 (ii)).
-__device__ __forceinline__ float asm_load_f32(const float* p) {
-  float v;
-  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-__device__ __forceinline__ uint2 asm_load_b64(const void* p) {
-  uint2 v;
-  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-// s_waitcnt vmcnt(C[sel]) for a wave-uniform sel in {0, 1, 2}, as ONE asm
-// statement (a compiler-level branch between waits would make the register
-// allocator copy the loaded registers at the merge, reading them before the
-// data lands).  It names every register the epilogue's asm loads write, each
-// as the very variable the load returned, so no consumer is scheduled above it.
-#define NR_WAIT_SEL_ASM                                                                  \
-  "s_cmp_eq_u32 %[sel], 0\n\ts_cbranch_scc1 .Lnrw0_%=\n\ts_cmp_eq_u32 %[sel], 1\n\t"  \
-  "s_cbranch_scc1 .Lnrw1_%=\n\ts_waitcnt vmcnt(%c[c2])\n\ts_branch .Lnrwe_%=\n"        \
-  ".Lnrw0_%=:\n\ts_waitcnt vmcnt(%c[c0])\n\ts_branch .Lnrwe_%=\n"                     \
-  ".Lnrw1_%=:\n\ts_waitcnt vmcnt(%c[c1])\n.Lnrwe_%=:"
-template <int C0, int C1, int C2, bool HR>
-__device__ __forceinline__ void wait_sel(int sel, float (&bs)[16], uint2 (&rv)[2][4]) {
-  if constexpr (HR)
-    asm volatile(NR_WAIT_SEL_ASM
-                 : "+v"(bs[0]), "+v"(bs[1]), "+v"(bs[2]), "+v"(bs[3]), "+v"(bs[4]), "+v"(bs[5]), "+v"(bs[6]),
-                   "+v"(bs[7]), "+v"(bs[8]), "+v"(bs[9]), "+v"(bs[10]), "+v"(bs[11]), "+v"(bs[12]), "+v"(bs[13]),
-                   "+v"(bs[14]), "+v"(bs[15]), "+v"(rv[0][0]), "+v"(rv[0][1]), "+v"(rv[0][2]), "+v"(rv[0][3]),
-                   "+v"(rv[1][0]), "+v"(rv[1][1]), "+v"(rv[1][2]), "+v"(rv[1][3])
-                 : [sel] "s"(sel), [c0] "i"(C0), [c1] "i"(C1), [c2] "i"(C2)
-                 : "memory", "scc");
-  else
-    asm volatile(NR_WAIT_SEL_ASM
-                 : "+v"(bs[0]), "+v"(bs[1]), "+v"(bs[2]), "+v"(bs[3]), "+v"(bs[4]), "+v"(bs[5]), "+v"(bs[6]),
-                   "+v"(bs[7]), "+v"(bs[8]), "+v"(bs[9]), "+v"(bs[10]), "+v"(bs[11]), "+v"(bs[12]), "+v"(bs[13]),
-                   "+v"(bs[14]), "+v"(bs[15])
-                 : [sel] "s"(sel), [c0] "i"(C0), [c1] "i"(C1), [c2] "i"(C2)
-                 : "memory", "scc");
-}
-template <int C0, int C1, int C2>
-__device__ __forceinline__ void wait_sel_r(int sel, uint2 (&rv)[2][4]) {
-  asm volatile(NR_WAIT_SEL_ASM
-               : "+v"(rv[0][0]), "+v"(rv[0][1]), "+v"(rv[0][2]), "+v"(rv[0][3]), "+v"(rv[1][0]), "+v"(rv[1][1]),
-                 "+v"(rv[1][2]), "+v"(rv[1][3])
-               : [sel] "s"(sel), [c0] "i"(C0), [c1] "i"(C1), [c2] "i"(C2)
-               : "memory", "scc");
+// Row-segment store of two adjacent 16-column tiles (a = tile 0, b = tile 1) of
+// a swapped-operand 16x16 accumulator: lane (row l & 15, q = l >> 4) holds
+// columns 4q..4q+3 of each tile as packed bf16.  One v_permlane16_swap per dword
+// (lanes 16-31 / 48-63 of `a` <-> lanes 0-15 / 32-47 of `b`) leaves lanes with
+// even q holding tile 0, columns 8 (q / 2) .. +7, and lanes with odd q tile 1,
+// columns 8 (q / 2) .. +7: one 16-byte store per lane, 64 contiguous bytes per
+// row (guide T21, here with the 16-lane swap).  base = row start of tile 0.
+__device__ __forceinline__ void store_pair16(__bf16* base, uint2 a, uint2 b, int q) {
+  const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+  const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+  // after the swap every lane holds 8 consecutive columns as (a.x, a.y, b.x, b.y)
+  *reinterpret_cast<uint4*>(base + 16 * (q & 1) + 8 * (q >> 1)) = uint4{sx[0], sy[0], sx[1], sy[1]};
 }
 
-__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  return (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)a) |
-         ((uint32_t)__builtin_bit_cast(unsigned short, (__bf16)b) << 16);
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t v) {  // v_pk_max_i16 with 0
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2, v), i16x2{0, 0}));
 }
 
 template <int EPI>
@@ -768,7 +736,8 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   typedef __bf16 TI;
   constexpr int BK = 64, CE = 8;
   constexpr int NST = PersistCfg<EPI>::kStores;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE];
+  // operand stages + one 256-B bias slice per wave (LDS-DMA'd with the prologue)
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE + 8 * 256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int wmu = __builtin_amdgcn_readfirstlane(wm);
@@ -821,7 +790,11 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
       __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(sb + (128 * h + 16 * wave + 8 * j) * 128), 16, 0, 0);
     }
   };
-  auto prologue = [&]() {  // 8 DMAs (stage 0) + 4 (stage 1's B halves) per wave
+  unsigned char* bias_lds = smem + 2 * G2_STAGE + wave * 256;  // this wave's 64 bias floats
+  auto prologue = [&]() {  // 1 bias + 8 stage-0 DMAs + 4 (stage 1's B halves) per wave
+    // without a bias the DMA reads A (any valid bytes; the slice is then ignored)
+    const float* bsrc = bias ? bias + n0 + wn * 64 + lane : reinterpret_cast<const float*>(A) + lane;
+    __builtin_amdgcn_global_load_lds((g_void*)bsrc, (lds_void*)bias_lds, 4, 0, 0);
     dmaB(0, 0, 0);
     dmaB(1, 0, 0);
     dmaA(0, 0, 0);
@@ -877,6 +850,29 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   mma(QM, NI, FB);                                     \
   __builtin_amdgcn_s_setprio(0);                       \
   __builtin_amdgcn_s_barrier();
+  auto kstep = [&](int64_t kt) {
+    const int st = (int)(kt & 1), ns = st ^ 1;
+    const bool pre1 = kt + 1 < nk, pre2 = kt + 2 < nk;
+    readA(st, 0);
+    readB(st, 0, fb0);
+    if (pre1) dmaA(0, ns, kt + 1);
+    NR_PHASE_SYNC_MMA(0, 0, fb0)
+    readB(st, 1, fb1);
+    if (pre1) dmaA(1, ns, kt + 1);
+    NR_PHASE_SYNC_MMA(0, 1, fb1)
+    readA(st, 1);
+    if (pre2) dmaB(0, st, kt + 2);
+    NR_PHASE_SYNC_MMA(1, 1, fb1)
+    // P4: tile t+1 must have landed (B0 of t+2 may still fly)
+    if (pre2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (pre2) dmaB(1, st, kt + 2);
+    __builtin_amdgcn_s_setprio(1);
+    mma(1, 0, fb0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
 
   setup(t);
   prologue();
@@ -884,110 +880,101 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   bool first = true;
   while (true) {
+    // RESADD: the residual tile seeds the accumulators (acc = bias + R + A.W^T),
+    // loaded in the store layout (16 B per lane, see store_pair16) and brought
+    // to the accumulator layout by the same (involutive) v_permlane16_swap;
+    // issued before the stage-0 wait so its latency hides behind it
+    uint4 rq[8][2];
+    if constexpr (EPI == NR_EPI_RESADD) {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        const int64_t row = min(m0 + wm * 128 + c16 + 16 * mi, M - 1);
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          rq[mi][p] = *reinterpret_cast<const uint4*>(R + row * ldr + n0 + wn * 64 + 32 * p + 16 * (q4 & 1) +
+                                                      8 * (q4 >> 1));
+      }
+    }
     if (!first) {
       // the previous tile's NST stores (and its R loads, already retired) were
       // issued after this tile's prologue DMAs: all but the youngest NST (+ the
-      // 4 stage-1 DMAs) retired => stage 0 has landed
-      if (nk > 1) {
-        if constexpr (NST == 32) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      // 4 stage-1 DMAs) retired => the bias slice and stage 0 have landed
+      // (RESADD: + its 16 residual loads, issued just above)
+      if constexpr (EPI == NR_EPI_RESADD) {
+        if (nk > 1) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      } else if (nk > 1) {
+        if constexpr (NST == 16) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
       } else {
-        if constexpr (NST == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        if constexpr (NST == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       }
     }
     first = false;
     __builtin_amdgcn_s_barrier();
-    if (wmu == 1) __builtin_amdgcn_s_barrier();  // stagger the wave groups
+    // the accumulators start at the bias (acc = bias + A.W^T: no bias add in
+    // the epilogue); this wave's columns wn*64 + 16 ni + 4 q4 .. +3
+    f32x4 b4[4];
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
+    for (int ni = 0; ni < 4; ++ni)
+      b4[ni] = bias ? *reinterpret_cast<const f32x4*>(bias_lds + (16 * ni + 4 * q4) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
+    for (int mi = 0; mi < 8; ++mi) {
+      if constexpr (EPI == NR_EPI_RESADD) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[mi][ni][r] = 0.f;
-    for (int64_t kt = 0; kt < nk; ++kt) {
-      const int st = (int)(kt & 1), ns = st ^ 1;
-      const bool pre1 = kt + 1 < nk, pre2 = kt + 2 < nk;
-      readA(st, 0);
-      readB(st, 0, fb0);
-      if (pre1) dmaA(0, ns, kt + 1);
-      NR_PHASE_SYNC_MMA(0, 0, fb0)
-      readB(st, 1, fb1);
-      if (pre1) dmaA(1, ns, kt + 1);
-      NR_PHASE_SYNC_MMA(0, 1, fb1)
-      readA(st, 1);
-      if (pre2) dmaB(0, st, kt + 2);
-      NR_PHASE_SYNC_MMA(1, 1, fb1)
-      if (pre2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (pre2) dmaB(1, st, kt + 2);
-      __builtin_amdgcn_s_setprio(1);
-      mma(1, 0, fb0);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_s_barrier();
+        for (int p = 0; p < 2; ++p) {
+          const auto sx = __builtin_amdgcn_permlane16_swap(rq[mi][p].x, rq[mi][p].z, false, false);
+          const auto sy = __builtin_amdgcn_permlane16_swap(rq[mi][p].y, rq[mi][p].w, false, false);
+          const uint32_t w[2][2] = {{sx[0], sy[0]}, {sx[1], sy[1]}};  // tile 2p, tile 2p + 1
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t u = w[h][r >> 1];
+              acc[mi][2 * p + h][r] = b4[2 * p + h][r] + ((r & 1) ? bf16_hi(u) : bf16_lo(u));
+            }
+        }
+      } else {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = b4[ni];
+      }
     }
+    if (wmu == 1) __builtin_amdgcn_s_barrier();  // stagger the wave groups
+    for (int64_t kt = 0; kt < nk; ++kt) kstep(kt);
     if (wmu == 0) __builtin_amdgcn_s_barrier();  // re-align the groups: every stage read is retired
 
     // ---------------- epilogue of tile (m0, n0) ----------------
-    // Loads are inline asm (hipcc would otherwise wait vmcnt(0) before their
-    // first use while LDS-DMAs fly, draining the next tile's prologue); their
-    // completion is counted here by hand, in issue order:
-    //   bias (16), R rows of mi 0-1 (8), prologue DMAs (NP = 12 / 8 / 0), then
-    //   per mi: wait, compute, 4 stores, R rows of mi + 2 (R epilogues only).
-    // Rows past M are clamped to M - 1 everywhere (their A rows were clamped by
-    // the DMA too), so they compute row M - 1's exact bytes and store them
-    // there again: every wave issues the same store count on every tile.
+    // No loads: the bias and residual are already in the accumulators.  The
+    // next tile's prologue DMAs are issued first and land while this tile's
+    // values are computed and stored.  Rows past M are clamped to M - 1 (their
+    // A rows were clamped by the DMA too), so they compute row M - 1's exact
+    // bytes and store them there again: every wave issues the same store count
+    // on every tile, which the next tile's counted wait relies on.
     const int64_t em0 = m0, en0 = n0;
     const int64_t row0 = em0 + wm * 128 + c16;      // + 16 mi
     const int64_t col0 = en0 + wn * 64 + 4 * q4;    // + 16 ni
-    constexpr bool HR = PersistCfg<EPI>::kR;
-    float bs[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) bs[i] = bias ? asm_load_f32(bias + col0 + 16 * (i >> 2) + (i & 3)) : 0.f;
-    uint2 rv[2][4];  // R rows of mi (ring of 2), R epilogues only
-    auto loadR = [&](int mi) {
-      const int64_t row = min(row0 + 16 * mi, M - 1);
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) rv[mi & 1][ni] = asm_load_b64(R + row * ldr + col0 + 16 * ni);
-    };
-    if constexpr (HR) {
-      loadR(0);
-      loadR(1);
-    }
     const int tn = t + t_step;
     const bool more = tn < t_end;
-    // wave-uniform selector of the prologue size: 0 = none, 1 = 8 DMAs, 2 = 12
-    const int sel = __builtin_amdgcn_readfirstlane(more ? (nk > 1 ? 2 : 1) : 0);
     if (more) {  // the next tile's operands fly while this tile's epilogue runs
       setup(tn);
       prologue();
     }
-    // bias (+ R rows of mi 0) landed; younger: the NP DMAs (+ R rows of mi 1)
-    if constexpr (HR) wait_sel<4, 12, 16, true>(sel, bs, rv);
-    else wait_sel<0, 8, 12, false>(sel, bs, rv);
-    f32x4 bv[4];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) bv[i >> 2][i & 3] = bs[i];
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
       const int64_t row = min(row0 + 16 * mi, M - 1);
-      if constexpr (HR) {
-        // R rows of mi landed; younger: stores of mi - 1 (4) + R rows of mi + 1 (4, mi <= 6) [+ NP at mi 1]
-        if (mi == 1) wait_sel_r<8, 16, 20>(sel, rv);
-        else if (mi >= 2 && mi <= 6) wait_sel_r<8, 8, 8>(sel, rv);
-        else if (mi == 7) wait_sel_r<4, 4, 4>(sel, rv);
-      }
       if constexpr (EPI == NR_EPI_GEGLU) {
         // W rows interleaved in 32-row (a, g) blocks: ni 0, 1 = a, ni 2, 3 = g
-        const int64_t ocol = (en0 + wn * 64) / 2 + 4 * q4;
+        const int64_t ocol = (en0 + wn * 64) / 2;
+        uint2 pk[2];
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni) {
           float o[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (acc[mi][ni][r] + bv[ni][r]) * gelu_erf(acc[mi][ni + 2][r] + bv[ni + 2][r]);
-          *reinterpret_cast<uint2*>(C + row * ldc + ocol + 16 * ni) = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+          for (int r = 0; r < 4; ++r) o[r] = acc[mi][ni][r] * gelu_erf(acc[mi][ni + 2][r]);
+          pk[ni] = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
         }
+        store_pair16(C + row * ldc + ocol, pk[0], pk[1], q4);
         __builtin_amdgcn_sched_barrier(0);  // one row group at a time: bounds the erf temporaries' live ranges
       } else {
         float v[4][4];
@@ -995,20 +982,13 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
         for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float x = acc[mi][ni][r] + bv[ni][r];
-            if constexpr (EPI == NR_EPI_RELU) x = fmaxf(x, 0.f);
+            float x = acc[mi][ni][r];
             if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
               const uint64_t gi = (uint64_t)(row * N + col0 + 16 * ni + r);
               x = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(x, 0.f) * ea.scale;
             }
             if constexpr (EPI == NR_EPI_EXP) x = expf(x);
             if constexpr (EPI == NR_EPI_GELU) x = gelu_erf(x);
-            if constexpr (HR) {
-              const uint32_t w2 = r < 2 ? rv[mi & 1][ni].x : rv[mi & 1][ni].y;
-              const float rr = (r & 1) ? bf16_hi(w2) : bf16_lo(w2);
-              if constexpr (EPI == NR_EPI_RESADD) x += rr;
-              else x = rr > 0.f ? acc[mi][ni][r] * ea.scale : 0.f;  // DRELU: no bias
-            }
             v[ni][r] = x;
           }
         if constexpr (EPI == NR_EPI_SOFTMAX64) {
@@ -1037,13 +1017,16 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[ni][r] *= inv;
         }
+        uint2 pk[4];
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          *reinterpret_cast<uint2*>(C + row * ldc + col0 + 16 * ni) =
-              uint2{pack_bf16x2(v[ni][0], v[ni][1]), pack_bf16x2(v[ni][2], v[ni][3])};
-        if constexpr (HR) {
-          if (mi + 2 < 8) loadR(mi + 2);
+        for (int ni = 0; ni < 4; ++ni) {
+          pk[ni] = uint2{pack_bf16x2(v[ni][0], v[ni][1]), pack_bf16x2(v[ni][2], v[ni][3])};
+          // ReLU on the packed bf16: a set sign bit is a negative int16, so the
+          // signed max with 0 zeroes exactly the negative values (and -0)
+          if constexpr (EPI == NR_EPI_RELU) pk[ni] = uint2{relu_bf16x2(pk[ni].x), relu_bf16x2(pk[ni].y)};
         }
+        store_pair16(C + row * ldc + en0 + wn * 64, pk[0], pk[1], q4);
+        store_pair16(C + row * ldc + en0 + wn * 64 + 32, pk[2], pk[3], q4);
       }
     }
     if (!more) break;
@@ -1089,7 +1072,6 @@ static int launch_gemm256_t(int epi, int64_t M, int64_t N, int64_t K, const void
     case NR_EPI_RESADD: NR_T(NR_EPI_RESADD); break;
     case NR_EPI_GELU: NR_T(NR_EPI_GELU); break;
     case NR_EPI_RELU_DROPOUT: NR_T(NR_EPI_RELU_DROPOUT); break;
-    case NR_EPI_DRELU: NR_T(NR_EPI_DRELU); break;
     case NR_EPI_SOFTMAX64: NR_T(NR_EPI_SOFTMAX64); break;
     default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
   }
@@ -1159,7 +1141,10 @@ static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* 
                           void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
   EpiArgs eg = ea;
   eg.group_m = kGemmGroupM;
-  if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) return launch_gemm256_t(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
+  // persistent kernel for bf16 -> bf16 (DRELU, a training-only epilogue that needs its
+  // forward output at the END of the tile, stays on the one-tile-per-workgroup kernel)
+  if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2)
+    if (epi != NR_EPI_DRELU) return launch_gemm256_t(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
   if constexpr (sizeof(TI) == 2) return launch_gemm256_p16<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
   return launch_gemm256_p<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
 }
