@@ -690,30 +690,32 @@ __global__ __launch_bounds__(512, 2) void gemm256p_group_kernel(GemmGroup g) {
 // tile_of), so a CU never idles between tiles waiting for a new workgroup.
 // The main loop is gemm256p_body's 4-phase pipeline with the MFMA operands
 // swapped (acc = W fragment x A fragment): the 16x16 accumulator of lane l
-// then holds C[row l & 15][cols 4 (l >> 4) .. +3], four consecutive columns of
-// one row, which leave as ONE 8-byte store straight from registers (no LDS
-// slab, no workgroup barrier in the epilogue).  Tile boundary: the epilogue's
-// bias / residual loads are issued, then the next tile's prologue DMAs, then
-// the epilogue computes and stores while those DMAs land; the next tile waits
-// vmcnt(stores [+ its 4 stage-1 DMAs]) — one counter retires in issue order —
-// so the stores drain under the next tile's first MFMA phases.
-template <int EPI>
-struct PersistCfg {
-  static constexpr int kStores = EPI == NR_EPI_GEGLU ? 8 : 16;  // 16-B stores per lane per tile
-};
-
-// Row-segment store of two adjacent 16-column tiles (a = tile 0, b = tile 1) of
-// a swapped-operand 16x16 accumulator: lane (row l & 15, q = l >> 4) holds
-// columns 4q..4q+3 of each tile as packed bf16.  One v_permlane16_swap per dword
-// (lanes 16-31 / 48-63 of `a` <-> lanes 0-15 / 32-47 of `b`) leaves lanes with
-// even q holding tile 0, columns 8 (q / 2) .. +7, and lanes with odd q tile 1,
-// columns 8 (q / 2) .. +7: one 16-byte store per lane, 64 contiguous bytes per
-// row (guide T21, here with the 16-lane swap).  base = row start of tile 0.
-__device__ __forceinline__ void store_pair16(__bf16* base, uint2 a, uint2 b, int q) {
+// then holds C[row l & 15][cols 4 (l >> 4) .. +3], which leave straight from
+// registers (no LDS slab).
+// One operand stream across tiles: the K steps of a workgroup's consecutive
+// tiles form one sequence (stage = parity of the position in it), so the last
+// two K steps of a tile prefetch the next tile's first two steps and bias
+// slice exactly as they would K steps of their own.  The epilogue then runs with the
+// next tile's operands already resident: no prologue and no operand wait at a
+// tile boundary.  The two wave groups (skewed by one barrier in the main loop)
+// are realigned for the epilogue, so both groups' epilogues run at once (one
+// wave of each per SIMD), and re-skewed after it (measured against keeping
+// the skew across the boundary, which serialises the two epilogues: 2-8 %
+// faster, 17 % on softmax64; profiles/round2/gemm_persist).  Operand DMAs go
+// through buffer descriptors: the per-lane 32-bit offsets are fixed per tile,
+// the K offset rides in an SGPR (host: every operand < 4 GiB).
+__device__ __forceinline__ uint4 swap_pair16(uint2 a, uint2 b) {
+  // Row-segment of two adjacent 16-column tiles (a = tile 0, b = tile 1) of a
+  // swapped-operand 16x16 accumulator: lane (row l & 15, q = l >> 4) holds
+  // columns 4q..4q+3 of each tile as packed bf16.  One v_permlane16_swap per
+  // dword (lanes 16-31 / 48-63 of `a` <-> lanes 0-15 / 32-47 of `b`) leaves
+  // lanes with even q holding tile 0, columns 8 (q / 2) .. +7, and lanes with
+  // odd q tile 1, columns 8 (q / 2) .. +7: 16 contiguous bytes per lane at
+  // column 16 (q & 1) + 8 (q >> 1) (guide T21, here with the 16-lane swap).
+  // The swap pairs lanes of one row, and is its own inverse.
   const auto sx = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
   const auto sy = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
-  // after the swap every lane holds 8 consecutive columns as (a.x, a.y, b.x, b.y)
-  *reinterpret_cast<uint4*>(base + 16 * (q & 1) + 8 * (q >> 1)) = uint4{sx[0], sy[0], sx[1], sy[1]};
+  return uint4{sx[0], sy[0], sx[1], sy[1]};
 }
 
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -726,6 +728,13 @@ __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t v) {  // v_pk_max_i16 w
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2, v), i16x2{0, 0}));
 }
 
+// s_waitcnt immediates waiting on vmcnt only (gfx9 encoding: vmcnt [3:0] and
+// [15:14], expcnt [6:4] = 7, lgkmcnt [11:8] = 15).  Issued through the builtin,
+// not inline asm, so the compiler's own wait insertion sees them: it then knows
+// the older stores have retired and keeps its waits for the epilogue's
+// residual loads counted instead of vmcnt(0).
+constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78;
+
 template <int EPI>
 __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, int64_t K,
                                                           const __bf16* __restrict__ A, int64_t lda,
@@ -733,15 +742,13 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
                                                           const float* __restrict__ bias, const __bf16* R,
                                                           int64_t ldr, __bf16* C, int64_t ldc, EpiArgs ea,
                                                           int ntn, int ntm, int n_tiles) {
-  typedef __bf16 TI;
-  constexpr int BK = 64, CE = 8;
-  constexpr int NST = PersistCfg<EPI>::kStores;
-  // operand stages + one 256-B bias slice per wave (LDS-DMA'd with the prologue)
+  constexpr int BK = 64;
+  // operand stages + one 256-B bias slice per wave (LDS-DMA'd with the tile's step 0)
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE + 8 * 256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int wmu = __builtin_amdgcn_readfirstlane(wm);
-  const int64_t nk = K / BK;
+  const int nk = (int)(K / BK);  // >= 2 (host)
 
   // tile schedule: XCD group x = blockIdx % 8 owns a contiguous range of tile
   // ids; its ~32 workgroups run consecutive ids, which tile_of groups into
@@ -761,48 +768,63 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     t_step = G;
   }
   if (t >= t_end) return;  // workgroup-uniform
-
-  int64_t m0 = 0, n0 = 0;
-  auto setup = [&](int tile) {
+  auto tile_base = [&](int tile, uint32_t& mb, uint32_t& nb) {
     int mt, nt;
     tile_of(tile, ntn, ntm, ea.group_m, mt, nt);
-    m0 = (int64_t)mt * G2BM;
-    n0 = (int64_t)nt * G2BN;
+    mb = (uint32_t)mt * G2BM;
+    nb = (uint32_t)nt * G2BN;
   };
-  // DMA sources recomputed per issue from (m0, n0): lane l of wave w fills row
-  // 128h + 16w + 8j + l/8, 16-B chunk (l & 7) ^ ((row >> 1) & 7) of the image
+
+  // buffer descriptors over A, W and the bias, built from readfirstlane'd
+  // kernel arguments so the compiler can prove them wave-uniform (T20: else
+  // every buffer op gets a waterfall loop)
+  auto rsrc = [](const void* p, int64_t bytes) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    const int n = __builtin_amdgcn_readfirstlane((int)(bytes > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)bytes));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rA = rsrc(A, M * lda * 2), rW = rsrc(W, N * ldw * 2);
+  // lane l of wave w fills row 128 h + 16 w + 8 j + l / 8 of an operand half,
+  // 16-B chunk (l & 7) ^ ((row >> 1) & 7) of the LDS image (T2 swizzle on the
+  // source); rows past M are clamped to M - 1 (never stored)
   const int rl = 16 * wave + (lane >> 3);
-  auto cj = [&](int j) { return (lane & 7) ^ ((4 * j + (lane >> 4)) & 7); };
-  auto dmaA = [&](int h, int stage, int64_t kt) {
-    unsigned char* sa = smem + stage * G2_STAGE;
+  const uint32_t ldab = (uint32_t)lda * 2, ldwb = (uint32_t)ldw * 2, mlast = (uint32_t)(M - 1);
+  auto chunk = [&](int j) { return (uint32_t)(((lane & 7) ^ ((4 * j + (lane >> 4)) & 7)) * 16); };
+  uint32_t oA[2][2], oB[2][2];
+  auto set_offA = [&](uint32_t mb) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t row = min(m0 + 128 * h + 8 * j + rl, M - 1);
-      const TI* src = A + row * lda + cj(j) * CE + kt * BK;
-      __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(sa + (128 * h + 16 * wave + 8 * j) * 128), 16, 0, 0);
-    }
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) oA[h][j] = min(mb + (uint32_t)(128 * h + 8 * j + rl), mlast) * ldab + chunk(j);
   };
-  auto dmaB = [&](int h, int stage, int64_t kt) {
-    unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128;
+  auto set_offB = [&](uint32_t nb) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const TI* src = W + (n0 + 128 * h + 8 * j + rl) * ldw + cj(j) * CE + kt * BK;
-      __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)(sb + (128 * h + 16 * wave + 8 * j) * 128), 16, 0, 0);
-    }
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) oB[h][j] = (nb + (uint32_t)(128 * h + 8 * j + rl)) * ldwb + chunk(j);
+  };
+  auto dmaA = [&](int h, int stage, int kt) {
+    unsigned char* sa = smem + stage * G2_STAGE + (128 * h + 16 * wave) * 128;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sa + 8 * j * 128), 16, oA[h][j], kt * (BK * 2), 0, 0);
+  };
+  auto dmaB = [&](int h, int stage, int kt) {
+    unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128 + (128 * h + 16 * wave) * 128;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(sb + 8 * j * 128), 16, oB[h][j], kt * (BK * 2), 0, 0);
   };
   unsigned char* bias_lds = smem + 2 * G2_STAGE + wave * 256;  // this wave's 64 bias floats
-  auto prologue = [&]() {  // 1 bias + 8 stage-0 DMAs + 4 (stage 1's B halves) per wave
-    // without a bias the DMA reads A (any valid bytes; the slice is then ignored)
-    const float* bsrc = bias ? bias + n0 + wn * 64 + lane : reinterpret_cast<const float*>(A) + lane;
-    __builtin_amdgcn_global_load_lds((g_void*)bsrc, (lds_void*)bias_lds, 4, 0, 0);
-    dmaB(0, 0, 0);
-    dmaB(1, 0, 0);
-    dmaA(0, 0, 0);
-    dmaA(1, 0, 0);
-    if (nk > 1) {
-      dmaB(0, 1, 1);
-      dmaB(1, 1, 1);
-    }
+  // (a buffer op like the operands: a global_load_lds here would be a FLAT
+  // instruction, whose pending LDS write makes the compiler wait vmcnt(0))
+  const __amdgpu_buffer_rsrc_t rBias = rsrc(bias, N * 4);
+  auto dma_bias = [&](uint32_t nb) {
+    if (bias)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rBias, (lds_void*)bias_lds, 4, (nb + (uint32_t)(wn * 64 + lane)) * 4, 0,
+                                               0, 0);
   };
 
   // fragment reads (16x16x32 operand map: row lane & 15, k chunk 4 f + lane / 16)
@@ -850,122 +872,111 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   mma(QM, NI, FB);                                     \
   __builtin_amdgcn_s_setprio(0);                       \
   __builtin_amdgcn_s_barrier();
-  auto kstep = [&](int64_t kt) {
-    const int st = (int)(kt & 1), ns = st ^ 1;
-    const bool pre1 = kt + 1 < nk, pre2 = kt + 2 < nk;
+  // K step kt of the current tile (stage st).  All of step kt + 2 is
+  // prefetched into this stage as soon as its reads are done: B half 0 in P3
+  // (last B read: P2), B half 1 and both A halves in P4 (last A read: P3) --
+  // this tile's step, or past its end the next tile's steps 0 and 1 (with the
+  // next tile's bias slice ahead of step 0).  P4 then waits for step kt + 1
+  // with the whole of step kt + 2 still in flight: every DMA gets ~1.25 K
+  // steps to land (3+ half-tiles in flight, the 8-phase template's depth).
+  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {
+    const bool pf = kt + 2 < nk || more;
+    const int kf = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
     readA(st, 0);
     readB(st, 0, fb0);
-    if (pre1) dmaA(0, ns, kt + 1);
     NR_PHASE_SYNC_MMA(0, 0, fb0)
     readB(st, 1, fb1);
-    if (pre1) dmaA(1, ns, kt + 1);
     NR_PHASE_SYNC_MMA(0, 1, fb1)
     readA(st, 1);
-    if (pre2) dmaB(0, st, kt + 2);
+    if (pf) {
+      if (kt + 2 == nk) {
+        set_offA(nm0);
+        set_offB(nn0);
+        dma_bias(nn0);
+      }
+      dmaB(0, st, kf);
+    }
     NR_PHASE_SYNC_MMA(1, 1, fb1)
-    // P4: tile t+1 must have landed (B0 of t+2 may still fly)
-    if (pre2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (pf) {
+      dmaB(1, st, kf);
+      dmaA(0, st, kf);
+      dmaA(1, st, kf);
+      __builtin_amdgcn_s_waitcnt(kVmcnt8);  // step kt + 1 landed; kt + 2 (8 DMAs) may fly
+    } else {
+      __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    }
     __builtin_amdgcn_s_barrier();
-    if (pre2) dmaB(1, st, kt + 2);
     __builtin_amdgcn_s_setprio(1);
     mma(1, 0, fb0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   };
 
-  setup(t);
-  prologue();
-  if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  bool first = true;
+  uint32_t m0, n0;
+  tile_base(t, m0, n0);
+  set_offA(m0);
+  set_offB(n0);
+  // first tile: bias slice + steps 0 and 1 (stages 0 and 1)
+  dma_bias(n0);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    dmaB(0, k, k);
+    dmaB(1, k, k);
+    dmaA(0, k, k);
+    dmaA(1, k, k);
+  }
+  __builtin_amdgcn_s_waitcnt(kVmcnt8);
+  __builtin_amdgcn_s_barrier();
+  if (wmu == 1) __builtin_amdgcn_s_barrier();  // skew the wave groups by one barrier
+  int st = 0;
   while (true) {
-    // RESADD: the residual tile seeds the accumulators (acc = bias + R + A.W^T),
-    // loaded in the store layout (16 B per lane, see store_pair16) and brought
-    // to the accumulator layout by the same (involutive) v_permlane16_swap;
-    // issued before the stage-0 wait so its latency hides behind it
-    uint4 rq[8][2];
-    if constexpr (EPI == NR_EPI_RESADD) {
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi) {
-        const int64_t row = min(m0 + wm * 128 + c16 + 16 * mi, M - 1);
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-          rq[mi][p] = *reinterpret_cast<const uint4*>(R + row * ldr + n0 + wn * 64 + 32 * p + 16 * (q4 & 1) +
-                                                      8 * (q4 >> 1));
-      }
-    }
-    if (!first) {
-      // the previous tile's NST stores (and its R loads, already retired) were
-      // issued after this tile's prologue DMAs: all but the youngest NST (+ the
-      // 4 stage-1 DMAs) retired => the bias slice and stage 0 have landed
-      // (RESADD: + its 16 residual loads, issued just above)
-      if constexpr (EPI == NR_EPI_RESADD) {
-        if (nk > 1) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-      } else if (nk > 1) {
-        if constexpr (NST == 16) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      } else {
-        if constexpr (NST == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      }
-    }
-    first = false;
-    __builtin_amdgcn_s_barrier();
-    // the accumulators start at the bias (acc = bias + A.W^T: no bias add in
-    // the epilogue); this wave's columns wn*64 + 16 ni + 4 q4 .. +3
-    f32x4 b4[4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-      b4[ni] = bias ? *reinterpret_cast<const f32x4*>(bias_lds + (16 * ni + 4 * q4) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-      if constexpr (EPI == NR_EPI_RESADD) {
-#pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          const auto sx = __builtin_amdgcn_permlane16_swap(rq[mi][p].x, rq[mi][p].z, false, false);
-          const auto sy = __builtin_amdgcn_permlane16_swap(rq[mi][p].y, rq[mi][p].w, false, false);
-          const uint32_t w[2][2] = {{sx[0], sy[0]}, {sx[1], sy[1]}};  // tile 2p, tile 2p + 1
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const uint32_t u = w[h][r >> 1];
-              acc[mi][2 * p + h][r] = b4[2 * p + h][r] + ((r & 1) ? bf16_hi(u) : bf16_lo(u));
-            }
-        }
-      } else {
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = b4[ni];
-      }
-    }
-    if (wmu == 1) __builtin_amdgcn_s_barrier();  // stagger the wave groups
-    for (int64_t kt = 0; kt < nk; ++kt) kstep(kt);
-    if (wmu == 0) __builtin_amdgcn_s_barrier();  // re-align the groups: every stage read is retired
-
-    // ---------------- epilogue of tile (m0, n0) ----------------
-    // No loads: the bias and residual are already in the accumulators.  The
-    // next tile's prologue DMAs are issued first and land while this tile's
-    // values are computed and stored.  Rows past M are clamped to M - 1 (their
-    // A rows were clamped by the DMA too), so they compute row M - 1's exact
-    // bytes and store them there again: every wave issues the same store count
-    // on every tile, which the next tile's counted wait relies on.
-    const int64_t em0 = m0, en0 = n0;
-    const int64_t row0 = em0 + wm * 128 + c16;      // + 16 mi
-    const int64_t col0 = en0 + wn * 64 + 4 * q4;    // + 16 ni
     const int tn = t + t_step;
     const bool more = tn < t_end;
-    if (more) {  // the next tile's operands fly while this tile's epilogue runs
-      setup(tn);
-      prologue();
+    uint32_t nm0 = 0, nn0 = 0;
+    if (more) tile_base(tn, nm0, nn0);
+    // the accumulators start at the bias (acc = bias + A.W^T); this wave's
+    // columns wn*64 + 16 ni + 4 q4 .. +3
+    {
+      f32x4 b4[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        b4[ni] = bias ? *reinterpret_cast<const f32x4*>(bias_lds + (16 * ni + 4 * q4) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = b4[ni];
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+      kstep(kt, st, more, nm0, nn0);
+      st ^= 1;
+    }
+
+    if (wmu == 0) __builtin_amdgcn_s_barrier();  // realign: group 1 has finished its last MFMA phase
+    // ---------------- epilogue of tile (m0, n0) ----------------
+    // The next tile's first stage is resident or in flight; nothing here
+    // touches LDS or waits on the operand DMAs.  Rows past M are clamped to
+    // M - 1 (their A rows were clamped by the DMA too), so they compute row
+    // M - 1's exact bytes and store them there again: no divergent stores, so
+    // the compiler's counted waits for the residual stay exact.
+    const int64_t row0 = (int64_t)m0 + wm * 128 + c16;  // + 16 mi
+    const int64_t col0 = (int64_t)n0 + wn * 64;          // this wave's 64 columns
+    const int qo = 16 * (q4 & 1) + 8 * (q4 >> 1);        // lane's 8 columns after swap_pair16
+    uint4 rq[8][2];
+    if constexpr (EPI == NR_EPI_RESADD) {
+      // residual in the store layout (16 B per lane), all loads up front
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        const int64_t row = min(row0 + 16 * mi, M - 1);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) rq[mi][p] = *reinterpret_cast<const uint4*>(R + row * ldr + col0 + 32 * p + qo);
+        __builtin_amdgcn_sched_barrier(0);  // issue order = use order: counted waits vmcnt(14), not (0)
+      }
     }
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
       const int64_t row = min(row0 + 16 * mi, M - 1);
       if constexpr (EPI == NR_EPI_GEGLU) {
         // W rows interleaved in 32-row (a, g) blocks: ni 0, 1 = a, ni 2, 3 = g
-        const int64_t ocol = (en0 + wn * 64) / 2;
         uint2 pk[2];
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni) {
@@ -974,9 +985,25 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           for (int r = 0; r < 4; ++r) o[r] = acc[mi][ni][r] * gelu_erf(acc[mi][ni + 2][r]);
           pk[ni] = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
         }
-        store_pair16(C + row * ldc + ocol, pk[0], pk[1], q4);
+        const uint4 v = swap_pair16(pk[0], pk[1]);
+        *reinterpret_cast<uint4*>(C + row * ldc + col0 / 2 + qo) = v;
         __builtin_amdgcn_sched_barrier(0);  // one row group at a time: bounds the erf temporaries' live ranges
       } else {
+        if constexpr (EPI == NR_EPI_RESADD) {
+          // the residual to the accumulator layout by the same (involutive) swap
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const uint4 s = swap_pair16(uint2{rq[mi][p].x, rq[mi][p].y}, uint2{rq[mi][p].z, rq[mi][p].w});
+            const uint32_t w[2][2] = {{s.x, s.y}, {s.z, s.w}};  // tile 2p, tile 2p + 1
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const uint32_t u = w[h][r >> 1];
+                acc[mi][2 * p + h][r] += (r & 1) ? bf16_hi(u) : bf16_lo(u);
+              }
+          }
+        }
         float v[4][4];
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
@@ -984,7 +1011,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           for (int r = 0; r < 4; ++r) {
             float x = acc[mi][ni][r];
             if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
-              const uint64_t gi = (uint64_t)(row * N + col0 + 16 * ni + r);
+              const uint64_t gi = (uint64_t)(row * N + col0 + 16 * ni + 4 * q4 + r);
               x = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(x, 0.f) * ea.scale;
             }
             if constexpr (EPI == NR_EPI_EXP) x = expf(x);
@@ -1025,12 +1052,18 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           // signed max with 0 zeroes exactly the negative values (and -0)
           if constexpr (EPI == NR_EPI_RELU) pk[ni] = uint2{relu_bf16x2(pk[ni].x), relu_bf16x2(pk[ni].y)};
         }
-        store_pair16(C + row * ldc + en0 + wn * 64, pk[0], pk[1], q4);
-        store_pair16(C + row * ldc + en0 + wn * 64 + 32, pk[2], pk[3], q4);
+        const uint4 s0 = swap_pair16(pk[0], pk[1]), s1 = swap_pair16(pk[2], pk[3]);
+        __bf16* dst = C + row * ldc + col0 + qo;
+        *reinterpret_cast<uint4*>(dst) = s0;
+        *reinterpret_cast<uint4*>(dst + 32) = s1;
+        if constexpr (EPI == NR_EPI_RESADD) __builtin_amdgcn_sched_barrier(0);  // row groups in load order
       }
     }
     if (!more) break;
+    if (wmu == 1) __builtin_amdgcn_s_barrier();  // re-skew
     t = tn;
+    m0 = nm0;
+    n0 = nn0;
   }
 #undef NR_PHASE_SYNC_MMA
 }
@@ -1045,6 +1078,13 @@ static int num_cus() {
     n_cu = n >= 8 ? n / 8 * 8 : 8;
   }
   return n_cu;
+}
+
+// The persistent kernel's operand stream needs >= 2 K steps per tile and
+// addresses A and W through 32-bit buffer offsets.
+static bool persistent_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldw) {
+  constexpr int64_t kMax = 0xFFFFFFFFll;
+  return K >= 128 && M * lda * 2 <= kMax && N * ldw * 2 <= kMax;
 }
 
 static int launch_gemm256_t(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W,
@@ -1144,7 +1184,8 @@ static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* 
   // persistent kernel for bf16 -> bf16 (DRELU, a training-only epilogue that needs its
   // forward output at the END of the tile, stays on the one-tile-per-workgroup kernel)
   if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2)
-    if (epi != NR_EPI_DRELU) return launch_gemm256_t(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
+    if (epi != NR_EPI_DRELU && persistent_ok(M, N, K, lda, ldw))
+      return launch_gemm256_t(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
   if constexpr (sizeof(TI) == 2) return launch_gemm256_p16<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
   return launch_gemm256_p<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
 }

@@ -127,6 +127,46 @@ def test_gemm_bf16_256_epilogues(gpu_device, epi, out_dt):
     np.testing.assert_allclose(out.float().cpu().double().numpy(), ref.numpy(), rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("epi", ["none", "relu", "exp", "gelu", "resadd", "geglu", "softmax64"])
+def test_gemm_persistent_bf16_multi_tile(gpu_device, epi):
+    """The persistent bf16 -> bf16 kernel (gemm256t_kernel) at sizes where every
+    workgroup walks several tiles (the operand stream and its stage parity
+    cross tile boundaries, incl. an odd K-step count and the 2-step minimum)
+    and the last round is partial: full outputs vs float64 of the same bf16
+    operands."""
+    g = torch.Generator(device=gpu_device).manual_seed(5)
+    for M, N, K in [(70001, 1024, 256), (33000, 512, 128), (90000, 768, 192)]:
+        a = (torch.randn(M, K, device=gpu_device, generator=g) * 0.2).bfloat16()
+        w = (torch.randn(N, K, device=gpu_device, generator=g) * 0.1).bfloat16()
+        b = torch.randn(N, device=gpu_device, generator=g) * 0.1
+        ncols = N // 2 if epi == "geglu" else N
+        r = torch.randn(M, ncols, device=gpu_device, generator=g).bfloat16()
+        acc = a.double() @ w.double().T + b.double()
+        wk, bk = w, b
+        if epi == "relu":
+            ref = acc.clamp_min(0)
+        elif epi == "exp":
+            ref = acc.exp()
+        elif epi == "gelu":
+            ref = torch.nn.functional.gelu(acc)
+        elif epi == "resadd":
+            ref = acc + r.double()
+        elif epi == "geglu":
+            ref = acc[:, :N // 2] * torch.nn.functional.gelu(acc[:, N // 2:])
+            wk, bk = interleave_geglu_rows(w), interleave_geglu_rows(b)
+        elif epi == "softmax64":
+            ref = torch.softmax(acc.reshape(M, N // 64, 64), -1).reshape(M, N)
+        else:
+            ref = acc
+        del acc
+        out = ops.gemm(a, wk.contiguous(), bk.contiguous(), epilogue=epi,
+                       residual=r if epi == "resadd" else None, out_dtype=torch.bfloat16)
+        torch.cuda.synchronize()
+        err = (out.double() - ref).abs() - 1e-2 * ref.abs()
+        bad = int((err > 1e-2).sum())
+        assert bad == 0, (M, N, K, epi, bad, float(err.max()))
+
+
 def test_gemm_identity_asymmetric(gpu_device):
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     for dt in (torch.float32, torch.bfloat16):

@@ -4,10 +4,9 @@ the persistent bf16 kernel (gemm256t_kernel) accumulates s_memtime phase
 durations per workgroup in registers (wave 0) and writes them once at its end
 into a buffer set by lab_set_stamps(); link it with the other objects into
 tools/gemm_lab/libnewsrec_stamped.so.  Phases per tile:
-  main  = top barrier passed -> main loop done (realigned)
-  pre   = -> epilogue loads + next prologue issued + first counted wait done
+  main  = accumulators seeded -> last K step done
   epi   = -> epilogue computed, stores issued
-  top   = -> next tile's top wait + barriers passed
+  top   = -> next tile's accumulators seeded
 The stamps read the shader clock only (no memory traffic inside the loop)."""
 import re
 import subprocess
@@ -19,41 +18,33 @@ CSRC = REPO / "news_recommendation_project_v2_amd" / "csrc"
 OUT = Path(__file__).resolve().parent
 
 
-def patch(src: str, dma_probe: bool = False) -> str:
+def patch(src: str) -> str:
     def sub(old, new):
         nonlocal src
         assert src.count(old) == 1, old
         src = src.replace(old, new)
     sub('#include "nr_common.h"', '#include "nr_common.h"\n__device__ unsigned long long* g_lab_stamps = nullptr;')
-    sub("  bool first = true;\n",
-        "  bool first = true;\n  unsigned long long s_main = 0, s_pre = 0, s_epi = 0, s_top = 0, s_n = 0, tt0 = 0, tt3 = 0;\n"
-        "  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), ck0 = __builtin_amdgcn_s_memtime();\n")
-    sub("    if (wmu == 1) __builtin_amdgcn_s_barrier();  // stagger the wave groups\n",
-        "    if (wmu == 1) __builtin_amdgcn_s_barrier();  // stagger the wave groups\n"
-        "    tt0 = __builtin_amdgcn_s_memtime();\n    if (!first0) s_top += tt0 - tt3;\n    first0 = false;\n")
-    sub("  bool first = true;\n", "  bool first = true, first0 = true;\n")
+    sub("  int st = 0;\n  while (true) {\n",
+        "  int st = 0;\n  unsigned long long s_main = 0, s_epi = 0, s_top = 0, s_n = 0, tt0 = 0, tt2 = 0;\n"
+        "  bool first0 = true;\n"
+        "  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), ck0 = __builtin_amdgcn_s_memtime();\n"
+        "  while (true) {\n")
+    sub("    for (int kt = 0; kt < nk; ++kt) {\n      kstep(kt, st, more, nm0, nn0);",
+        "    tt0 = __builtin_amdgcn_s_memtime();\n    if (!first0) s_top += tt0 - tt2;\n    first0 = false;\n"
+        "    for (int kt = 0; kt < nk; ++kt) {\n      kstep(kt, st, more, nm0, nn0);")
     sub("    // ---------------- epilogue of tile (m0, n0) ----------------\n",
         "    const unsigned long long tt1 = __builtin_amdgcn_s_memtime();\n    s_main += tt1 - tt0;\n"
         "    // ---------------- epilogue of tile (m0, n0) ----------------\n")
-    sub("      setup(tn);\n      prologue();\n    }\n",
-        "      setup(tn);\n      prologue();\n    }\n"
-        "    const unsigned long long tt2 = __builtin_amdgcn_s_memtime();\n    s_pre += tt2 - tt1;\n")
-    sub("    if (!more) break;\n    t = tn;\n  }\n#undef NR_PHASE_SYNC_MMA\n}",
-        "    tt3 = __builtin_amdgcn_s_memtime();\n    s_epi += tt3 - tt2;\n    ++s_n;\n"
-        "    if (!more) break;\n    t = tn;\n  }\n"
+    sub("    if (!more) break;\n",
+        "    tt2 = __builtin_amdgcn_s_memtime();\n    s_epi += tt2 - tt1;\n    ++s_n;\n"
+        "    if (!more) break;\n")
+    sub("    n0 = nn0;\n  }\n",
+        "    n0 = nn0;\n  }\n"
         "  const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime(), ck1 = __builtin_amdgcn_s_memtime();\n"
         "  if (tid == 0 && g_lab_stamps) {\n"
         "    unsigned long long* o = g_lab_stamps + blockIdx.x * 8;\n"
-        "    o[0] = s_main; o[1] = s_pre; o[2] = s_epi; o[3] = s_top; o[4] = s_n; o[5] = ck1 - ck0; o[6] = rt1 - rt0;\n"
-        "  }\n#undef NR_PHASE_SYNC_MMA\n}")
-    if dma_probe:  # time from the next tile's prologue issue to its landing, with nothing else in flight
-        sub("    if (more) {  // the next tile's operands fly while this tile's epilogue runs\n      setup(tn);\n      prologue();\n    }\n",
-            "    if (more) {  // the next tile's operands fly while this tile's epilogue runs\n      setup(tn);\n"
-            "      asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
-            "      const unsigned long long ti = __builtin_amdgcn_s_memtime();\n      prologue();\n"
-            "      asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n      s_dma += __builtin_amdgcn_s_memtime() - ti;\n    }\n")
-        sub("unsigned long long s_main = 0,", "unsigned long long s_dma = 0, s_main = 0,")
-        sub("o[6] = rt1 - rt0;", "o[6] = rt1 - rt0; o[7] = s_dma;")
+        "    o[0] = s_main; o[1] = 0; o[2] = s_epi; o[3] = s_top; o[4] = s_n; o[5] = ck1 - ck0; o[6] = rt1 - rt0;\n"
+        "  }\n")
     src += '\nextern "C" int lab_set_stamps(void* p) {\n  return hipMemcpyToSymbol(HIP_SYMBOL(g_lab_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;\n}\n'
     return src
 
@@ -61,14 +52,13 @@ def patch(src: str, dma_probe: bool = False) -> str:
 def main():
     build = OUT / "build"
     build.mkdir(exist_ok=True)
-    probe = "--dma-probe" in sys.argv
-    (build / "gemm_stamped.hip").write_text(patch((CSRC / "gemm.hip").read_text(), probe))
+    (build / "gemm_stamped.hip").write_text(patch((CSRC / "gemm.hip").read_text()))
     inc = ["-I", str(CSRC)]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", *inc, "-c",
                     str(build / "gemm_stamped.hip"), "-o", str(build / "gemm_stamped.o")], check=True)
     objs = [str(p) for p in sorted((CSRC / "build").glob("*.o")) if p.name != "gemm.o"]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", str(build / "gemm_stamped.o"),
-                    *objs, "-o", str(OUT / ("libnewsrec_dmaprobe.so" if probe else "libnewsrec_stamped.so"))], check=True)
+                    *objs, "-o", str(OUT / "libnewsrec_stamped.so")], check=True)
     print("built")
 
 

@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Lab variants of the persistent GEMM (tool only, never shipped): patch a COPY
+of csrc/gemm.hip with one named change, link it with the other objects into
+tools/gemm_lab/libnewsrec_<name>.so for tools/gemm_ab.py.
+
+    python tools/gemm_lab/make_variant.py flatdma
+"""
+import subprocess
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[2]
+CSRC = REPO / "news_recommendation_project_v2_amd" / "csrc"
+OUT = Path(__file__).resolve().parent
+
+VARIANTS = {
+    # operand DMAs as global_load_lds (FLAT encoding) instead of buffer loads
+    "flatdma": [
+        ("__builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sa + 8 * j * 128), 16, oA[h][j], kt * (BK * 2), 0, 0);",
+         "__builtin_amdgcn_global_load_lds((g_void*)((const char*)A + oA[h][j] + kt * (BK * 2)), "
+         "(lds_void*)(sa + 8 * j * 128), 16, 0, 0);"),
+        ("__builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(sb + 8 * j * 128), 16, oB[h][j], kt * (BK * 2), 0, 0);",
+         "__builtin_amdgcn_global_load_lds((g_void*)((const char*)W + oB[h][j] + kt * (BK * 2)), "
+         "(lds_void*)(sb + 8 * j * 128), 16, 0, 0);"),
+    ],
+    # the P4 operand waits as opaque inline asm (the compiler no longer sees them)
+    "asmwait": [
+        ("    if (pb) __builtin_amdgcn_s_waitcnt(kVmcnt2);\n    else __builtin_amdgcn_s_waitcnt(kVmcnt0);",
+         '    if (pb) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");\n'
+         '    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");'),
+    ],
+    # DIAGNOSTIC (wrong results): no operand DMAs inside the K loop
+    "nodma": [
+        ("  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {\n    const int ns = st ^ 1;\n"
+         "    const bool pa = kt + 1 < nk || more, pb = kt + 2 < nk || more;",
+         "  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {\n    const int ns = st ^ 1;\n"
+         "    const bool pa = false, pb = false;"),
+    ],
+    # DIAGNOSTIC (wrong results): no fragment reads (MFMA on stale registers)
+    "noread": [
+        ("    readA(st, 0);\n    readB(st, 0, fb0);\n    if (pa) {", "    if (pa) {"),
+        ("    readB(st, 1, fb1);\n    if (pa) dmaA(1, ns, ka);", "    if (pa) dmaA(1, ns, ka);"),
+        ("    readA(st, 1);\n    if (pb) {", "    if (pb) {"),
+    ],
+    # no s_setprio around the MFMA phases
+    "noprio": [
+        ("  __builtin_amdgcn_s_setprio(1);                       \\\n  mma(QM, NI, FB);                                     \\\n"
+         "  __builtin_amdgcn_s_setprio(0);                       \\\n",
+         "  mma(QM, NI, FB);                                     \\\n"),
+    ],
+}
+
+
+def main():
+    name = sys.argv[1]
+    src = (CSRC / "gemm.hip").read_text()
+    for old, new in VARIANTS[name]:
+        assert src.count(old) == 1, old
+        src = src.replace(old, new)
+    build = OUT / "build"
+    build.mkdir(exist_ok=True)
+    (build / f"gemm_{name}.hip").write_text(src)
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I", str(CSRC), "-c",
+                    str(build / f"gemm_{name}.hip"), "-o", str(build / f"gemm_{name}.o")], check=True)
+    objs = [str(p) for p in sorted((CSRC / "build").glob("*.o")) if p.name != "gemm.o"]
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", str(build / f"gemm_{name}.o"),
+                    *objs, "-o", str(OUT / f"libnewsrec_{name}.so")], check=True)
+    print("built", name)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

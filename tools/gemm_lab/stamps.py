@@ -48,7 +48,6 @@ def main():
                **{f"{ph}_cyc": round(v) for ph, v in per.items()},
                **{f"{ph}_us": round(v / clock * 1e6, 3) for ph, v in per.items()},
                "main_per_ktile_us": round(per["main"] / clock * 1e6 / (k / 64), 4),
-               "dma_us": round(float((s[:, 7] / (tiles - 1).clamp_min(1)).mean()) / clock * 1e6, 3),
                "block_total_us": round(float((s[:, 5] / clock).mean()) * 1e6, 1)}
         print(json.dumps(res), flush=True)
 
