@@ -257,6 +257,29 @@ int nr_latent_transform(int dtype, int64_t n, const void* emb, int64_t emb_ld,
                         void* ws, int64_t ws_bytes, void* stream);
 
 /*
+ * The same transform for dtype == NR_BF16 with both LayerNorms folded into the
+ * GEMM that consumes them (no normalised rows are written):
+ *   LN(x) · Wᵀ = rstd ⊙ (x · W'ᵀ − mean ⊗ u) + c,
+ *   W' = W ∘ γ (bf16),  u_n = Σ_k W'_nk (of the bf16 W'),  c_n = Σ_k β_k W_nk (+ bias)
+ * with per-row (mean, rstd) from nr_row_stats.  Aq = A ∘ γ_q [512][1024],
+ * ucq = (u[512], c[512]) f32; W1f = W1i ∘ γ_f [8192][1024] (interleaved rows),
+ * ucf = (u[8192], c[8192]) f32 with c including b1i.  Bt, W2, b2 as above.
+ * NR_ERR_UNSUPPORTED for NR_F32 (the f32 parity path keeps nr_latent_transform).
+ */
+int nr_latent_transform_lnfold(int dtype, int64_t n, const void* emb, int64_t emb_ld, const void* Aq,
+                               const float* ucq, const void* Bt, const void* W1f, const float* ucf,
+                               const void* W2, const float* b2, void* table, void* ws, int64_t ws_bytes,
+                               void* stream);
+
+/*
+ * Per-row LayerNorm statistics out[r] = (mean, 1/sqrt(var + eps)) (f32 pairs,
+ * biased variance: torch.nn.LayerNorm, latent_attention.py:11-13) of rows
+ * [rows][1024] in `dtype`.
+ */
+int nr_row_stats(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps, float* out,
+                 void* stream);
+
+/*
  * Title encoder pieces (XLM-R-large / e5-large-instruct), packed varlen tokens.
  * Replaces transformers XLMRobertaEmbeddings.forward (word + token_type +
  * position embeddings, LayerNorm) and the self-attention core

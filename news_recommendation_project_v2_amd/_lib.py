@@ -56,6 +56,8 @@ SIGNATURES = {
     "nr_final_attn_transform": (_i, [_i, _l, _p, _l, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _l, _p]),
     "nr_latent_workspace_bytes": (_l, [_i, _l]),
     "nr_latent_transform": (_i, [_i, _l, _p, _l, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _l, _p]),
+    "nr_latent_transform_lnfold": (_i, [_i, _l, _p, _l, _p, _p, _p, _p, _p, _p, _p, _p, _p, _l, _p]),
+    "nr_row_stats": (_i, [_i, _l, _l, _p, _l, _f, _p, _p]),
     "nr_embed_ln": (_i, [_i, _l, _p, _p, _p, _p, _p, _p, _p, _f, _p, _p]),
     "nr_attention_varlen": (_i, [_i, ctypes.c_int32, _l, _p, _p, _p, _p, _p]),
     "nr_gather_rows": (_i, [_i, _i, _l, _l, _p, _l, _p, _p, _l, _p]),

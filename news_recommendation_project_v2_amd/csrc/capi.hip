@@ -131,3 +131,46 @@ extern "C" int nr_latent_transform(int dtype, int64_t n, const void* emb, int64_
   }
   return NR_OK;
 }
+
+// bf16: both LayerNorms applied inside the GEMM that consumes them
+// (gemm_lnfold_dispatch); only per-row (mean, rstd) pairs are written.
+//   sq = stats(e); P = softmax64(LN_q(e) Aᵀ) via (e, Aq, ucq, sq); h1 = e + P Btᵀ
+//   sf = stats(h1); f = GEGLU(LN_f(h1) W1iᵀ + b1i) via (h1, W1f, ucf, sf); h = h1 + f W2ᵀ + b2
+extern "C" int nr_latent_transform_lnfold(int dtype, int64_t n, const void* emb, int64_t emb_ld, const void* Aq,
+                                          const float* ucq, const void* Bt, const void* W1f, const float* ucf,
+                                          const void* W2, const float* b2, void* table, void* ws, int64_t ws_bytes,
+                                          void* stream) {
+  nr::clear_error();
+  if (dtype != NR_BF16) {
+    nr::set_error("nr_latent_transform_lnfold: bf16 only (f32 uses nr_latent_transform)");
+    return NR_ERR_UNSUPPORTED;
+  }
+  NR_CHECK_ARG(n >= 0, "nr_latent_transform_lnfold: n < 0");
+  if (n == 0) return NR_OK;
+  NR_CHECK_ARG(emb && Aq && ucq && Bt && W1f && ucf && W2 && b2 && table && ws,
+               "nr_latent_transform_lnfold: null pointer");
+  NR_CHECK_ARG(ws_bytes >= nr_latent_workspace_bytes(dtype, n), "nr_latent_transform_lnfold: workspace too small");
+  NR_CHECK_ARG(((uintptr_t)ws & 15) == 0, "nr_latent_transform_lnfold: workspace must be 16-byte aligned");
+  const int es = 2;
+  const int64_t D = 1024, S = 512, F = 4096;
+  const int64_t mc = n < nr::kChunk ? n : nr::kChunk;
+  hipStream_t st = (hipStream_t)stream;
+  // workspace: [stats_q | stats_f] in the unfused path's LN-output region
+  float* sq = (float*)ws;
+  float* sf = sq + 2 * mc;
+  char* wp = (char*)ws + mc * (D * es + S * 4);
+  char* wf = wp + mc * S * es;
+  for (int64_t r0 = 0; r0 < n; r0 += nr::kChunk) {
+    const int64_t m = (n - r0) < nr::kChunk ? (n - r0) : nr::kChunk;
+    const char* e = (const char*)emb + r0 * emb_ld * es;
+    char* h = (char*)table + r0 * D * es;
+    int rc;
+    if ((rc = nr::row_stats_dispatch(dtype, m, D, e, emb_ld, 1e-5f, sq, st))) return rc;
+    if ((rc = nr::gemm_lnfold_dispatch(NR_EPI_SOFTMAX64, m, S, D, e, emb_ld, Aq, D, sq, ucq, wp, S, st))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RESADD, m, D, S, wp, S, Bt, S, nullptr, e, emb_ld, h, D, st))) return rc;
+    if ((rc = nr::row_stats_dispatch(dtype, m, D, h, D, 1e-5f, sf, st))) return rc;
+    if ((rc = nr::gemm_lnfold_dispatch(NR_EPI_GEGLU, m, 2 * F, D, h, D, W1f, D, sf, ucf, wf, F, st))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RESADD, m, D, F, wf, F, W2, F, b2, h, D, h, D, st))) return rc;
+  }
+  return NR_OK;
+}

@@ -52,6 +52,8 @@ struct EpiArgs {
   uint32_t thr;   // drop iff drop_hash(seed, row * N + col) < thr  (thr = p * 2^32)
   float scale;    // 1 / (1 - p)
   int group_m = 1;  // 256x256 tile order: >1 groups group_m M-tiles (see tile_of)
+  const float* ln_stats = nullptr;  // LNF epilogue: [M] (mean, rstd) pairs
+  const float* ln_uc = nullptr;     // LNF epilogue: u [N] then c [N]
 };
 
 template <typename TO>
@@ -733,9 +735,15 @@ __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t v) {  // v_pk_max_i16 w
 // not inline asm, so the compiler's own wait insertion sees them: it then knows
 // the older stores have retired and keeps its waits for the epilogue's
 // residual loads counted instead of vmcnt(0).
-constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78;
+constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78, kVmcnt11 = 0x0F7B;
 
-template <int EPI>
+// LNF (LayerNorm folded into the epilogue): per tile, every wave's (u, c)
+// column slices (2 x 256 B) and the tile's 256 row stats (2 KiB), in two
+// slots (tile parity): tile t + 1's slot is filled by the DMAs that prefetch
+// its first K step while tile t's epilogue still reads slot t.
+constexpr int kLnSlot = 8 * 512 + 256 * 8;
+
+template <int EPI, bool LNF = false>
 __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, int64_t K,
                                                           const __bf16* __restrict__ A, int64_t lda,
                                                           const __bf16* __restrict__ W, int64_t ldw,
@@ -744,7 +752,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
                                                           int ntn, int ntm, int n_tiles) {
   constexpr int BK = 64;
   // operand stages + one 256-B bias slice per wave (LDS-DMA'd with the tile's step 0)
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE + 8 * 256];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE + 8 * 256 + (LNF ? 2 * kLnSlot : 0)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int wmu = __builtin_amdgcn_readfirstlane(wm);
@@ -826,6 +834,23 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rBias, (lds_void*)bias_lds, 4, (nb + (uint32_t)(wn * 64 + lane)) * 4, 0,
                                                0, 0);
   };
+  // LNF: 3 single-dword DMAs per wave (u slice, c slice, 32 of the tile's row stats)
+  unsigned char* ln_lds = smem + 2 * G2_STAGE + 8 * 256;
+  const __amdgpu_buffer_rsrc_t rUC = rsrc(ea.ln_uc, LNF ? 2 * N * 4 : 0);
+  const __amdgpu_buffer_rsrc_t rST = rsrc(ea.ln_stats, LNF ? M * 8 : 0);
+  auto dma_ln = [&](int slot, uint32_t mb, uint32_t nb) {
+    if constexpr (LNF) {
+      unsigned char* base = ln_lds + slot * kLnSlot;
+      const uint32_t cu = (nb + (uint32_t)(wn * 64 + lane)) * 4;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rUC, (lds_void*)(base + wave * 512), 4, cu, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rUC, (lds_void*)(base + wave * 512 + 256), 4, cu + (uint32_t)N * 4, 0, 0,
+                                               0);
+      const uint32_t row = min(mb + (uint32_t)(32 * wave + (lane >> 1)), mlast);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rST, (lds_void*)(base + 8 * 512 + wave * 256), 4,
+                                               row * 8 + (uint32_t)(lane & 1) * 4, 0, 0, 0);
+    }
+  };
+  int lslot = 0;  // LNF slot of the current tile
 
   // fragment reads (16x16x32 operand map: row lane & 15, k chunk 4 f + lane / 16)
   const int c16 = lane & 15, q4 = lane >> 4;
@@ -901,7 +926,13 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
       dmaB(1, st, kf);
       dmaA(0, st, kf);
       dmaA(1, st, kf);
-      __builtin_amdgcn_s_waitcnt(kVmcnt8);  // step kt + 1 landed; kt + 2 (8 DMAs) may fly
+      if (LNF && kt + 2 == nk) {
+        // the next tile's LN slices after its step-0 DMAs: they get a whole K step
+        dma_ln(lslot ^ 1, nm0, nn0);
+        __builtin_amdgcn_s_waitcnt(kVmcnt11);
+      } else {
+        __builtin_amdgcn_s_waitcnt(kVmcnt8);  // step kt + 1 landed; kt + 2 (8 DMAs) may fly
+      }
     } else {
       __builtin_amdgcn_s_waitcnt(kVmcnt0);
     }
@@ -916,7 +947,8 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   tile_base(t, m0, n0);
   set_offA(m0);
   set_offB(n0);
-  // first tile: bias slice + steps 0 and 1 (stages 0 and 1)
+  // first tile: LN slices, bias slice + steps 0 and 1 (stages 0 and 1)
+  dma_ln(0, m0, n0);
   dma_bias(n0);
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -955,12 +987,24 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     // ---------------- epilogue of tile (m0, n0) ----------------
     // The next tile's first stage is resident or in flight; nothing here
     // touches LDS or waits on the operand DMAs.  Rows past M are clamped to
-    // M - 1 (their A rows were clamped by the DMA too), so they compute row
-    // M - 1's exact bytes and store them there again: no divergent stores, so
-    // the compiler's counted waits for the residual stay exact.
+    // M - 1 (their A rows were clamped by the DMA too) for every load, but do
+    // not store: with an in-place residual (R == C, the latent ff2) another
+    // wave group's duplicate store of row M - 1 could land before this
+    // group's residual load of it and add the residual twice.
     const int64_t row0 = (int64_t)m0 + wm * 128 + c16;  // + 16 mi
     const int64_t col0 = (int64_t)n0 + wn * 64;          // this wave's 64 columns
     const int qo = 16 * (q4 & 1) + 8 * (q4 >> 1);        // lane's 8 columns after swap_pair16
+    // LNF: this lane's 16 columns' (u, c) and the tile's row stats (slot lslot)
+    f32x4 lu[4], lc[4];
+    const unsigned char* ln_st = ln_lds + lslot * kLnSlot + 8 * 512;
+    if constexpr (LNF) {
+      const unsigned char* uc = ln_lds + lslot * kLnSlot + wave * 512;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        lu[ni] = *reinterpret_cast<const f32x4*>(uc + (16 * ni + 4 * q4) * 4);
+        lc[ni] = *reinterpret_cast<const f32x4*>(uc + 256 + (16 * ni + 4 * q4) * 4);
+      }
+    }
     uint4 rq[8][2];
     if constexpr (EPI == NR_EPI_RESADD) {
       // residual in the store layout (16 B per lane), all loads up front
@@ -975,6 +1019,15 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
       const int64_t row = min(row0 + 16 * mi, M - 1);
+      const bool live = row0 + 16 * mi < M;  // clamped duplicates of row M - 1 never store
+      if constexpr (LNF) {
+        // LN(a) . w = rstd (a . (w o gamma) - mean u) + c   (row stats of the A row)
+        const float2 ms = *reinterpret_cast<const float2*>(ln_st + (wm * 128 + c16 + 16 * mi) * 8);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[mi][ni][r] = fmaf(ms.y, fmaf(-ms.x, lu[ni][r], acc[mi][ni][r]), lc[ni][r]);
+      }
       if constexpr (EPI == NR_EPI_GEGLU) {
         // W rows interleaved in 32-row (a, g) blocks: ni 0, 1 = a, ni 2, 3 = g
         uint2 pk[2];
@@ -986,7 +1039,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           pk[ni] = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
         }
         const uint4 v = swap_pair16(pk[0], pk[1]);
-        *reinterpret_cast<uint4*>(C + row * ldc + col0 / 2 + qo) = v;
+        if (live) *reinterpret_cast<uint4*>(C + row * ldc + col0 / 2 + qo) = v;
         __builtin_amdgcn_sched_barrier(0);  // one row group at a time: bounds the erf temporaries' live ranges
       } else {
         if constexpr (EPI == NR_EPI_RESADD) {
@@ -1054,13 +1107,16 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
         }
         const uint4 s0 = swap_pair16(pk[0], pk[1]), s1 = swap_pair16(pk[2], pk[3]);
         __bf16* dst = C + row * ldc + col0 + qo;
-        *reinterpret_cast<uint4*>(dst) = s0;
-        *reinterpret_cast<uint4*>(dst + 32) = s1;
+        if (live) {
+          *reinterpret_cast<uint4*>(dst) = s0;
+          *reinterpret_cast<uint4*>(dst + 32) = s1;
+        }
         if constexpr (EPI == NR_EPI_RESADD) __builtin_amdgcn_sched_barrier(0);  // row groups in load order
       }
     }
     if (!more) break;
     if (wmu == 1) __builtin_amdgcn_s_barrier();  // re-skew
+    lslot ^= 1;
     t = tn;
     m0 = nm0;
     n0 = nn0;
@@ -1188,6 +1244,44 @@ static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* 
       return launch_gemm256_t(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
   if constexpr (sizeof(TI) == 2) return launch_gemm256_p16<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
   return launch_gemm256_p<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
+}
+
+// LayerNorm-folded persistent launch (bf16 in/out; the bf16 latent transform).
+int gemm_lnfold_dispatch(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W,
+                         int64_t ldw, const float* stats, const float* uc, void* C, int64_t ldc, hipStream_t s) {
+  NR_CHECK_ARG(epi == NR_EPI_SOFTMAX64 || epi == NR_EPI_GEGLU, "nr_gemm_lnfold: epilogue %d unsupported", epi);
+  NR_CHECK_ARG(M >= 0 && N > 0 && K > 0, "nr_gemm_lnfold: bad shape");
+  if (M == 0) return NR_OK;
+  NR_CHECK_ARG(A && W && C && stats && uc, "nr_gemm_lnfold: null pointer");
+  if (N % G2BN != 0 || K % 64 != 0 || !persistent_ok(M, N, K, lda, ldw) || M * 8 > 0xFFFFFFFFll) {
+    set_error("nr_gemm_lnfold: unsupported shape M=%lld N=%lld K=%lld", (long long)M, (long long)N, (long long)K);
+    return NR_ERR_UNSUPPORTED;
+  }
+  const int64_t ncols = epi == NR_EPI_GEGLU ? N / 2 : N;
+  NR_CHECK_ARG(lda >= K && ldw >= K && lda % 8 == 0 && ldw % 8 == 0 && ldc >= ncols && ldc % 8 == 0 &&
+                   ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)C & 15) == 0 &&
+                   ((uintptr_t)stats & 7) == 0 && ((uintptr_t)uc & 3) == 0,
+               "nr_gemm_lnfold: operands must be 16-byte aligned with 16-byte row strides");
+  const int ntn = (int)(N / G2BN);
+  const int64_t ntm = (M + G2BM - 1) / G2BM;
+  NR_CHECK_ARG(ntm * ntn <= (1ll << 30), "nr_gemm_lnfold: too many tiles");
+  const int nt = (int)(ntm * ntn), ncu = num_cus();
+  const dim3 grid((unsigned)(nt < ncu ? nt : ncu));
+  EpiArgs ea{0, 0, 1.f};
+  ea.group_m = kGemmGroupM;
+  ea.ln_stats = stats;
+  ea.ln_uc = uc;
+  const __bf16* a = (const __bf16*)A;
+  const __bf16* w = (const __bf16*)W;
+  __bf16* c = (__bf16*)C;
+  if (epi == NR_EPI_GEGLU)
+    hipLaunchKernelGGL((gemm256t_kernel<NR_EPI_GEGLU, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, nullptr,
+                       nullptr, 0, c, ldc, ea, ntn, (int)ntm, nt);
+  else
+    hipLaunchKernelGGL((gemm256t_kernel<NR_EPI_SOFTMAX64, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw,
+                       nullptr, nullptr, 0, c, ldc, ea, ntn, (int)ntm, nt);
+  NR_CHECK_LAUNCH("nr_gemm_lnfold");
+  return NR_OK;
 }
 
 template <typename TI, typename TO>

@@ -33,6 +33,12 @@ int softmax64_dispatch(int64_t rows, int64_t groups, const float* x, int64_t ldx
                        int64_t ldy, hipStream_t s);
 int pool_rows_dispatch(int pooler, int dtype, const void* table, int64_t ld, const int64_t* off, int64_t n_seg,
                        float* users, hipStream_t s);
+int row_stats_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps, float* out,
+                       hipStream_t s);
+// bf16 persistent GEMM with a LayerNorm folded into its epilogue (epi NR_EPI_SOFTMAX64 or
+// NR_EPI_GEGLU): C = epi(rstd_m * (A W^T - mean_m u_n) + c_n); stats [M] (mean, rstd), uc [2][N]
+int gemm_lnfold_dispatch(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W,
+                         int64_t ldw, const float* stats, const float* uc, void* C, int64_t ldc, hipStream_t s);
 int inv_norm_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps,
                       float* out, hipStream_t s);
 

@@ -4,8 +4,6 @@
 // reductions are 64-lane butterflies (no LDS).
 #include "nr_common.h"
 
-#include <stdlib.h>
-
 namespace nr {
 
 // Lane-local load of 4 consecutive elements at element offset `e` (f32 or bf16).
@@ -148,6 +146,41 @@ __global__ __launch_bounds__(256) void softmax64_kernel(int64_t items, int64_t g
   else y[row * ldy + grp * 64 + lane] = (TO)o;
 }
 
+// Per-row LayerNorm statistics (mean, rstd) with the LayerNorm kernel's exact
+// arithmetic (two passes over the register-resident row, biased variance):
+// the bf16 latent transform applies LN inside the next GEMM's epilogue
+// (gemm256t_kernel LNF) instead of writing the normalised rows.
+template <typename T, int DIM>
+__global__ __launch_bounds__(256) void row_stats_kernel(int64_t rows, const T* __restrict__ x, int64_t ldx,
+                                                        float eps, float2* __restrict__ out) {
+  constexpr int E = 16 / (int)sizeof(T);
+  constexpr int NJ = DIM / (64 * E);
+  static_assert(DIM % (64 * E) == 0, "row_stats: DIM must be a multiple of 64 lanes x 16 B");
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += nw) {
+    float v[NJ][E];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      load16<T>(x + row * ldx + (j * 64 + lane) * E, v[j]);
+#pragma unroll
+      for (int t = 0; t < E; ++t) s += v[j][t];
+    }
+    const float mean = wave_sum(s) / (float)DIM;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int t = 0; t < E; ++t) {
+        const float d = v[j][t] - mean;
+        q = fmaf(d, d, q);
+      }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)DIM + eps);
+    if (lane == 0) out[row] = make_float2(mean, rstd);
+  }
+}
+
 template <typename T, int DIM>
 __global__ __launch_bounds__(256) void inv_norm_kernel(int64_t rows, const T* __restrict__ x,
                                                        int64_t ldx, float eps,
@@ -172,7 +205,7 @@ template <typename TI, typename TO>
 static int launch_ln(int64_t rows, int64_t dim, const void* x, int64_t ldx, const float* g,
                      const float* b, float eps, void* y, int64_t ldy, hipStream_t s) {
   const int64_t nb = (rows + 3) / 4;
-  static const int64_t cap = getenv("NR_LN_GRID") ? atoll(getenv("NR_LN_GRID")) : 1024;  // tuning knob (measured best for bf16 at 72k rows)
+  constexpr int64_t cap = 1024;  // grid cap (measured best for bf16 at 72k rows)
   const dim3 grid((unsigned)(cap > 0 && nb > cap ? cap : nb));  // rows grid-strided over <= cap blocks
 #define NR_LN_CASE(D)                                                                      \
   case D:                                                                                  \
@@ -323,6 +356,27 @@ int gather_ln_dispatch(int dti, int64_t n, int64_t dim, const void* x, int64_t l
   return NR_OK;
 }
 
+int row_stats_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps, float* out,
+                       hipStream_t s) {
+  NR_CHECK_ARG(dtype == NR_F32 || dtype == NR_BF16, "nr_row_stats: bad dtype");
+  NR_CHECK_ARG(dim == 1024, "nr_row_stats: dim %lld unsupported (1024 only)", (long long)dim);
+  NR_CHECK_ARG(rows >= 0 && ldx >= dim && (ldx * (dtype == NR_F32 ? 4 : 2)) % 16 == 0 && ((uintptr_t)x & 15) == 0 &&
+                   ((uintptr_t)out & 7) == 0,
+               "nr_row_stats: rows must be 16-byte aligned, out 8-byte aligned");
+  if (rows == 0) return NR_OK;
+  NR_CHECK_ARG(x && out, "nr_row_stats: null pointer");
+  const int64_t nb = (rows + 3) / 4;
+  const dim3 grid((unsigned)(nb > 2048 ? 2048 : nb));
+  if (dtype == NR_F32)
+    hipLaunchKernelGGL((row_stats_kernel<float, 1024>), grid, dim3(256), 0, s, rows, (const float*)x, ldx, eps,
+                       (float2*)out);
+  else
+    hipLaunchKernelGGL((row_stats_kernel<__bf16, 1024>), grid, dim3(256), 0, s, rows, (const __bf16*)x, ldx, eps,
+                       (float2*)out);
+  NR_CHECK_LAUNCH("nr_row_stats");
+  return NR_OK;
+}
+
 }  // namespace nr
 
 extern "C" int nr_gather_layernorm(int dtype_in, int64_t n, int64_t dim, const void* x, int64_t ldx,
@@ -351,4 +405,10 @@ extern "C" int nr_row_inv_norm(int dtype, int64_t rows, int64_t dim, const void*
                                float eps, float* out, void* stream) {
   nr::clear_error();
   return nr::inv_norm_dispatch(dtype, rows, dim, x, ldx, eps, out, (hipStream_t)stream);
+}
+
+extern "C" int nr_row_stats(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps, float* out,
+                            void* stream) {
+  nr::clear_error();
+  return nr::row_stats_dispatch(dtype, rows, dim, x, ldx, eps, out, (hipStream_t)stream);
 }

@@ -75,6 +75,23 @@ def interleave_geglu_rows(w: torch.Tensor, block: int = 32) -> torch.Tensor:
     return torch.stack([a, g], dim=1).reshape(two_f, *w.shape[1:])
 
 
+def lnfold_weights(w: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, bias: Optional[torch.Tensor],
+                   tag: str) -> Dict[str, torch.Tensor]:
+    """Weights that apply LayerNorm(gamma, beta) inside the GEMM that consumes it
+    (nr_latent_transform_lnfold, bf16): for a row a with LN stats (mean, rstd),
+        LN(a) . w_n + b_n = rstd (a . w'_n - mean u_n) + c_n,
+        w' = w o gamma (rounded to bf16),  u_n = sum_k w'_nk,  c_n = beta . w_n + b_n,
+    u taken from the ROUNDED w' (float64 sums) so a constant row maps exactly to c.
+    Returns {"W<tag>": bf16 [N, K], "uc<tag>": f32 [2, N]}."""
+    w64 = w.to(torch.float64)
+    wf = (w64 * gamma.to(torch.float64)[None, :]).to(torch.bfloat16)
+    u = wf.to(torch.float64).sum(1)
+    c = w64 @ beta.to(torch.float64)
+    if bias is not None:
+        c = c + bias.to(torch.float64)
+    return {f"W{tag}_ln": wf.contiguous(), f"uc{tag}": torch.stack([u, c]).to(torch.float32).contiguous()}
+
+
 class LatentAttentionModel(torch.nn.Module):
     """forward(embeddings [B, L, D], attention_mask [B, L] | None).
 
@@ -148,6 +165,11 @@ class LatentAttentionModel(torch.nn.Module):
             for name, t in fw.items():
                 tgt = dtype if name in ("A", "Bt", "W1i", "W2") else torch.float32
                 w[name] = t.to(tgt).to(dev).contiguous()
+            if dtype == torch.bfloat16:
+                for name, t in lnfold_weights(fw["A"], fw["lnq_g"], fw["lnq_b"], None, "q").items():
+                    w[name] = t.to(dev).contiguous()
+                for name, t in lnfold_weights(fw["W1i"], fw["lnf_g"], fw["lnf_b"], fw["b1i"], "f").items():
+                    w[name] = t.to(dev).contiguous()
             self._hip_cache = {key: w}
         return w
 

@@ -161,6 +161,17 @@ def row_inv_norm(x: torch.Tensor, eps: float = 1e-8, out: Optional[torch.Tensor]
     return out
 
 
+def row_stats(x: torch.Tensor, eps: float = 1e-5, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-row LayerNorm statistics [rows, 2] f32 = (mean, 1/sqrt(biased var + eps))."""
+    dev = _dev(x, out)
+    rows, dim = x.shape
+    if out is None:
+        out = torch.empty((rows, 2), dtype=torch.float32, device=dev)
+    _lib.call("nr_row_stats", _dtype(x, "x"), rows, dim, _ptr(x), _rowmajor(x, "x"), ctypes.c_float(eps),
+              _ptr(out), _stream(dev))
+    return out
+
+
 def _check_csr(idx: torch.Tensor, off: torch.Tensor, name: str) -> None:
     if idx.dtype != torch.int32 or not idx.is_contiguous():
         raise _lib.NewsRecHIPError(f"{name}_idx must be contiguous int32")
@@ -283,6 +294,12 @@ def latent_transform(emb: torch.Tensor, w: dict, out: Optional[torch.Tensor] = N
     for k in ("A", "Bt", "W1i", "W2"):
         if w[k].dtype != emb.dtype or not w[k].is_contiguous():
             raise _lib.NewsRecHIPError(f"latent_transform: {k} must be contiguous {emb.dtype}")
+    if dt == _lib.NR_BF16 and "Wq_ln" in w:
+        # both LayerNorms folded into the GEMMs that consume them (latent_attention.lnfold_weights)
+        _lib.call("nr_latent_transform_lnfold", dt, n, _ptr(emb), _rowmajor(emb, "emb"), _ptr(w["Wq_ln"]),
+                  _ptr(w["ucq"]), _ptr(w["Bt"]), _ptr(w["Wf_ln"]), _ptr(w["ucf"]), _ptr(w["W2"]), _ptr(w["b2"]),
+                  _ptr(out), _ptr(workspace), need, _stream(dev))
+        return out
     _lib.call("nr_latent_transform", dt, n, _ptr(emb), _rowmajor(emb, "emb"), _ptr(w["lnq_g"]), _ptr(w["lnq_b"]),
               _ptr(w["A"]), _ptr(w["Bt"]), _ptr(w["lnf_g"]), _ptr(w["lnf_b"]), _ptr(w["W1i"]), _ptr(w["b1i"]),
               _ptr(w["W2"]), _ptr(w["b2"]), _ptr(out), _ptr(workspace), need, _stream(dev))

@@ -167,6 +167,30 @@ def test_gemm_persistent_bf16_multi_tile(gpu_device, epi):
         assert bad == 0, (M, N, K, epi, bad, float(err.max()))
 
 
+@pytest.mark.parametrize("M", [1, 300, 5003, 70001])
+def test_gemm_persistent_inplace_resadd_ragged(gpu_device, M):
+    """In-place residual (C == R, the latent ff2: h = h + f W2^T + b2) with a
+    ragged last tile: the clamped duplicates of row M - 1 must not store (a
+    duplicate store landing before another wave group's residual load added the
+    residual twice to the last row when M - 1 sat in the tile's first 128 rows),
+    and nothing past row M is written."""
+    g = torch.Generator(device=gpu_device).manual_seed(M)
+    N, K = 1024, 512
+    a = (torch.randn(M, K, device=gpu_device, generator=g) * 0.2).bfloat16()
+    w = (torch.randn(N, K, device=gpu_device, generator=g) * 0.1).bfloat16()
+    b = torch.randn(N, device=gpu_device, generator=g) * 0.1
+    buf = torch.full((M + 300, N), 7.0, device=gpu_device, dtype=torch.bfloat16)
+    buf[:M] = torch.randn(M, N, device=gpu_device, generator=g).bfloat16()
+    r0 = buf[:M].double()
+    h = buf[:M]
+    ops.gemm(a, w, b, epilogue="resadd", residual=h, out=h)
+    torch.cuda.synchronize()
+    ref = a.double() @ w.double().T + b.double() + r0
+    err = ((h.double() - ref).abs() - 1e-2 * ref.abs()).max(1).values
+    assert float(err.max()) < 1e-2, (M, int(err.argmax()), float(err.max()))
+    assert bool((buf[M:] == 7.0).all())
+
+
 def test_gemm_identity_asymmetric(gpu_device):
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     for dt in (torch.float32, torch.bfloat16):

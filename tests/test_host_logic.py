@@ -9,7 +9,7 @@ import torch
 from conftest import REPO, golden, unflat
 from news_recommendation_project_v2_amd import data_utils, evaluation, synthetic
 from news_recommendation_project_v2_amd import weights as W
-from news_recommendation_project_v2_amd.latent_attention import LatentAttentionModel, interleave_geglu_rows
+from news_recommendation_project_v2_amd.latent_attention import LatentAttentionModel, interleave_geglu_rows, lnfold_weights
 from oracle import data_ref, pool_ref
 
 
@@ -121,6 +121,32 @@ def test_latent_fold_equals_reference_algebra():
     f = (z[:, :, 0] * torch.nn.functional.gelu(z[:, :, 1])).reshape(6, 4096)
     h = h1 + f @ fw["W2"].T + fw["b2"]
     np.testing.assert_allclose(h.numpy(), want.numpy(), rtol=0, atol=1e-10)
+
+
+def test_lnfold_weights_reproduce_layernorm_gemm():
+    """LN(a) . w_n + b_n == rstd (a . w'_n - mean u_n) + c_n  (nr_latent_transform_lnfold's
+    epilogue algebra) in float64 with the bf16-rounded w' = w o gamma, to bf16
+    weight-rounding accuracy; and exactly c_n for a constant row (u from the rounded w')."""
+    g = torch.Generator().manual_seed(3)
+    w = torch.randn(256, 1024, generator=g, dtype=torch.float64) * 0.03
+    gamma = 1 + 0.2 * torch.randn(1024, generator=g, dtype=torch.float64)
+    beta = 0.1 * torch.randn(1024, generator=g, dtype=torch.float64)
+    b = 0.05 * torch.randn(256, generator=g, dtype=torch.float64)
+    f = lnfold_weights(w, gamma, beta, b, "x")
+    wf, uc = f["Wx_ln"].double(), f["ucx"].double()
+    a = torch.randn(8, 1024, generator=g, dtype=torch.float64) * 2 + 0.7  # offset mean
+    mean, var = a.mean(1, keepdim=True), a.var(1, unbiased=False, keepdim=True)
+    rstd = 1 / torch.sqrt(var + 1e-5)
+    want = torch.nn.functional.layer_norm(a, (1024,), gamma, beta, 1e-5) @ w.T + b
+    got = rstd * (a @ wf.T - mean * uc[0]) + uc[1]
+    # the only difference is bf16 rounding of w o gamma (relative 2^-9 per weight)
+    assert (got - want).abs().max() < 2e-2 * want.abs().max()
+    wexact = (w * gamma[None, :]).to(torch.bfloat16).double() / gamma[None, :]
+    # exact identity: the gamma part through the rounded weights, c from the unrounded ones
+    want_r = torch.nn.functional.layer_norm(a, (1024,), gamma, beta, 1e-5) @ wexact.T + b + (w - wexact) @ beta
+    np.testing.assert_allclose(got.numpy(), want_r.numpy(), rtol=0, atol=1e-6)  # u, c stored f32
+    np.testing.assert_allclose((0.37 * wf.sum(1) - 0.37 * uc[0]).numpy(), 0.0, atol=1e-6)
+    assert f["Wx_ln"].dtype == torch.bfloat16 and f["ucx"].shape == (2, 256) and f["ucx"].dtype == torch.float32
 
 
 def test_interleave_geglu_rows():
