@@ -102,6 +102,25 @@ def main():
             err[lab] = float((outs[lab][rows].double() - ref).abs().max())
         fns = {lab: (lambda lib=lib, o=outs[lab]: run(lib, a, w, b, epi, r, o)) for lab, lib in libs.items()}
         fns["torch"] = lambda: torch.matmul(a, w.T)
+        # the same op as a hipBLASLt user runs it: addmm (bias in the GEMM) + torch's epilogue kernels
+        b16 = b.to(torch.bfloat16)
+        wt = w.T
+        if epi == "relu":
+            fns["torch_epi"] = lambda: torch.relu_(torch.addmm(b16, a, wt))
+        elif epi == "exp":
+            fns["torch_epi"] = lambda: torch.exp_(torch.addmm(b16, a, wt))
+        elif epi == "resadd":
+            fns["torch_epi"] = lambda: torch.addmm(b16, a, wt).add_(r)
+        elif epi == "softmax64":
+            fns["torch_epi"] = lambda: torch.softmax(torch.addmm(b16, a, wt).view(args.m, -1, 64), -1)
+        elif epi == "geglu":
+            def _geglu():
+                x = torch.addmm(b16, a, wt)
+                xa, xg = x.chunk(2, dim=-1)
+                return xa * torch.nn.functional.gelu(xg)
+            fns["torch_epi"] = _geglu
+        else:
+            fns["torch_epi"] = lambda: torch.addmm(b16, a, wt)
         times = {lab: [] for lab in fns}
         for _ in range(args.rounds):
             for lab, fn in fns.items():
