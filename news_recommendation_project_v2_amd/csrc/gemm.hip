@@ -794,10 +794,13 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
   };
   const __amdgpu_buffer_rsrc_t rA = rsrc(A, M * lda * 2), rW = rsrc(W, N * ldw * 2);
-  // lane l of wave w fills row 128 h + 16 w + 8 j + l / 8 of an operand half,
+  // DMA units are the quarters the phases finish reading: A unit q = rows
+  // 64 q .. +63 of both wave-group halves (lane l of wave w: row
+  // 128 (w >> 2) + 64 q + 16 (w & 3) + 8 j + l / 8), B unit q = rows 32 q .. +31
+  // of all four wn slices (row 64 (w >> 1) + 32 q + 16 (w & 1) + 8 j + l / 8);
   // 16-B chunk (l & 7) ^ ((row >> 1) & 7) of the LDS image (T2 swizzle on the
   // source); rows past M are clamped to M - 1 (never stored)
-  const int rl = 16 * wave + (lane >> 3);
+  const int qa = (wave >> 2) * 128 + (wave & 3) * 16, qb = (wave >> 1) * 64 + (wave & 1) * 16;
   const uint32_t ldab = (uint32_t)lda * 2, ldwb = (uint32_t)ldw * 2, mlast = (uint32_t)(M - 1);
   auto chunk = [&](int j) { return (uint32_t)(((lane & 7) ^ ((4 * j + (lane >> 4)) & 7)) * 16); };
   uint32_t oA[2][2], oB[2][2];
@@ -805,22 +808,22 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) oA[h][j] = min(mb + (uint32_t)(128 * h + 8 * j + rl), mlast) * ldab + chunk(j);
+      for (int j = 0; j < 2; ++j) oA[h][j] = min(mb + (uint32_t)(qa + 64 * h + 8 * j + (lane >> 3)), mlast) * ldab + chunk(j);
   };
   auto set_offB = [&](uint32_t nb) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) oB[h][j] = (nb + (uint32_t)(128 * h + 8 * j + rl)) * ldwb + chunk(j);
+      for (int j = 0; j < 2; ++j) oB[h][j] = (nb + (uint32_t)(qb + 32 * h + 8 * j + (lane >> 3))) * ldwb + chunk(j);
   };
   auto dmaA = [&](int h, int stage, int kt) {
-    unsigned char* sa = smem + stage * G2_STAGE + (128 * h + 16 * wave) * 128;
+    unsigned char* sa = smem + stage * G2_STAGE + (qa + 64 * h) * 128;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sa + 8 * j * 128), 16, oA[h][j], kt * (BK * 2), 0, 0);
   };
   auto dmaB = [&](int h, int stage, int kt) {
-    unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128 + (128 * h + 16 * wave) * 128;
+    unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128 + (qb + 32 * h) * 128;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(sb + 8 * j * 128), 16, oB[h][j], kt * (BK * 2), 0, 0);
@@ -898,12 +901,14 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   __builtin_amdgcn_s_setprio(0);                       \
   __builtin_amdgcn_s_barrier();
   // K step kt of the current tile (stage st).  All of step kt + 2 is
-  // prefetched into this stage as soon as its reads are done: B half 0 in P3
-  // (last B read: P2), B half 1 and both A halves in P4 (last A read: P3) --
-  // this tile's step, or past its end the next tile's steps 0 and 1 (with the
-  // next tile's bias slice ahead of step 0).  P4 then waits for step kt + 1
-  // with the whole of step kt + 2 still in flight: every DMA gets ~1.25 K
-  // steps to land (3+ half-tiles in flight, the 8-phase template's depth).
+  // prefetched into this stage, each quarter one phase after its last read
+  // (both wave groups' reads of phase p retire before the barrier instance
+  // the leading group passes to enter phase p + 1): A0 + B0 in P2 (read in
+  // P1), B1 in P3 (read in P2), A1 in P4 (read in P3) -- this tile's step, or
+  // past its end the next tile's steps 0 and 1 (with the next tile's bias
+  // slice ahead of step 0).  P4 then waits for step kt + 1 with the whole of
+  // step kt + 2 still in flight (+0.4..2.4 % over issuing it in P3/P4 as
+  // halves, profiles/round2/gemm_quarters_ab.jsonl).
   auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {
     const bool pf = kt + 2 < nk || more;
     const int kf = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
@@ -911,20 +916,20 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     readB(st, 0, fb0);
     NR_PHASE_SYNC_MMA(0, 0, fb0)
     readB(st, 1, fb1);
-    NR_PHASE_SYNC_MMA(0, 1, fb1)
-    readA(st, 1);
     if (pf) {
       if (kt + 2 == nk) {
         set_offA(nm0);
         set_offB(nn0);
         dma_bias(nn0);
       }
+      dmaA(0, st, kf);
       dmaB(0, st, kf);
     }
+    NR_PHASE_SYNC_MMA(0, 1, fb1)
+    readA(st, 1);
+    if (pf) dmaB(1, st, kf);
     NR_PHASE_SYNC_MMA(1, 1, fb1)
     if (pf) {
-      dmaB(1, st, kf);
-      dmaA(0, st, kf);
       dmaA(1, st, kf);
       if (LNF && kt + 2 == nk) {
         // the next tile's LN slices after its step-0 DMAs: they get a whole K step

@@ -14,6 +14,54 @@ CSRC = REPO / "news_recommendation_project_v2_amd" / "csrc"
 OUT = Path(__file__).resolve().parent
 
 VARIANTS = {
+    # operand DMA units cut into the quarters each phase finishes reading (A: one
+    # 64-row qm quarter of both wave-group halves, B: one 32-row qn quarter of
+    # all four wn slices), issued P2: A0+B0, P3: B1, P4: A1 (was P3: B0, P4: B1+A0+A1)
+    "quarters": [
+        ("  const int rl = 16 * wave + (lane >> 3);\n",
+         "  const int rl = 16 * wave + (lane >> 3);\n"
+         "  const int qa = (wave >> 2) * 128 + (wave & 3) * 16, qb = (wave >> 1) * 64 + (wave & 1) * 16;\n"),
+        ("oA[h][j] = min(mb + (uint32_t)(128 * h + 8 * j + rl), mlast) * ldab + chunk(j);",
+         "oA[h][j] = min(mb + (uint32_t)(qa + 64 * h + 8 * j + (lane >> 3)), mlast) * ldab + chunk(j);"),
+        ("oB[h][j] = (nb + (uint32_t)(128 * h + 8 * j + rl)) * ldwb + chunk(j);",
+         "oB[h][j] = (nb + (uint32_t)(qb + 32 * h + 8 * j + (lane >> 3))) * ldwb + chunk(j);"),
+        ("    unsigned char* sa = smem + stage * G2_STAGE + (128 * h + 16 * wave) * 128;\n#pragma unroll\n    for (int j = 0; j < 2; ++j)\n      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA,",
+         "    unsigned char* sa = smem + stage * G2_STAGE + (qa + 64 * h) * 128;\n#pragma unroll\n    for (int j = 0; j < 2; ++j)\n      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA,"),
+        ("    unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128 + (128 * h + 16 * wave) * 128;\n#pragma unroll\n    for (int j = 0; j < 2; ++j)\n      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW,",
+         "    unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128 + (qb + 32 * h) * 128;\n#pragma unroll\n    for (int j = 0; j < 2; ++j)\n      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW,"),
+        ("""    readB(st, 1, fb1);
+    NR_PHASE_SYNC_MMA(0, 1, fb1)
+    readA(st, 1);
+    if (pf) {
+      if (kt + 2 == nk) {
+        set_offA(nm0);
+        set_offB(nn0);
+        dma_bias(nn0);
+      }
+      dmaB(0, st, kf);
+    }
+    NR_PHASE_SYNC_MMA(1, 1, fb1)
+    if (pf) {
+      dmaB(1, st, kf);
+      dmaA(0, st, kf);
+      dmaA(1, st, kf);""",
+         """    readB(st, 1, fb1);
+    if (pf) {
+      if (kt + 2 == nk) {
+        set_offA(nm0);
+        set_offB(nn0);
+        dma_bias(nn0);
+      }
+      dmaA(0, st, kf);
+      dmaB(0, st, kf);
+    }
+    NR_PHASE_SYNC_MMA(0, 1, fb1)
+    readA(st, 1);
+    if (pf) dmaB(1, st, kf);
+    NR_PHASE_SYNC_MMA(1, 1, fb1)
+    if (pf) {
+      dmaA(1, st, kf);"""),
+    ],
     # operand DMAs as global_load_lds (FLAT encoding) instead of buffer loads
     "flatdma": [
         ("__builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sa + 8 * j * 128), 16, oA[h][j], kt * (BK * 2), 0, 0);",
