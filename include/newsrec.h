@@ -72,6 +72,14 @@ int nr_version(void);
  * config.py:19 for the library's own state. */
 int nr_init(int device);
 
+/* Workgroups of the persistent bf16 GEMM launches (one per CU by default).
+ * For callers that run the transform on a CU-masked stream beside other
+ * work (hipExtStreamCreateWithCUMask): set it to the stream's CU count.
+ * n = 0 restores the default; otherwise n must be a positive multiple of 8
+ * (the kernel maps blockIdx % 8 to an XCD).  Process-wide, not thread-safe
+ * against concurrent launches. */
+int nr_set_persistent_workgroups(int n);
+
 /* Thread-local message of the last failed call ("" if none). */
 const char* nr_last_error(void);
 

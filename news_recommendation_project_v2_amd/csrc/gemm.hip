@@ -1129,7 +1129,22 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
 #undef NR_PHASE_SYNC_MMA
 }
 
+// Workgroups of a persistent GEMM launch: the device's CU count rounded down
+// to a multiple of the 8 XCDs, unless the caller has set a budget for a
+// CU-masked stream (nr_set_persistent_workgroups).
+static int g_persist_wgs = 0;
+
+extern "C" int nr_set_persistent_workgroups(int n) {
+  if (n < 0 || n % 8) {
+    set_error("nr_set_persistent_workgroups: n=%d must be 0 or a positive multiple of 8", n);
+    return NR_ERR_INVALID;
+  }
+  g_persist_wgs = n;
+  return NR_OK;
+}
+
 static int num_cus() {
+  if (g_persist_wgs) return g_persist_wgs;
   static int n_cu = 0;
   if (!n_cu) {
     int dev = 0;

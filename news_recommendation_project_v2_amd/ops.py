@@ -61,6 +61,12 @@ def _dtype(t: torch.Tensor, name: str) -> int:
     return _DT[t.dtype]
 
 
+def set_persistent_workgroups(n: int = 0) -> None:
+    """Workgroups of the persistent bf16 GEMM launches (0 = one per CU): set it
+    to the CU count of a CU-masked stream the transform runs on."""
+    _lib.call("nr_set_persistent_workgroups", int(n))
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
          epilogue: str = "none", residual: Optional[torch.Tensor] = None,
          out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
