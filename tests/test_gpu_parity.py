@@ -390,6 +390,44 @@ def test_full_size_mind_large_properties(gpu_device):
         np.testing.assert_allclose(s[co[i]:co[i + 1]], ref.cpu().numpy(), rtol=0, atol=2e-5)
 
 
+@pytest.mark.parametrize("pooler", ["final", "latent"])
+def test_full_size_transform_vs_oracle(gpu_device, pooler):
+    """The per-news transform at the MIND-large-dev size (N = 72,023: 282
+    M-tiles, a ragged last tile, the persistent bf16 GEMM's multi-tile walk)
+    checked row by row against the oracle's per-item reference math (not the
+    engine's own output): 640 sampled rows incl. the first and the last 128
+    (tile edges) computed on the CPU in f32.  f32 path: within 2e-5 of each
+    row's scale; bf16 path: every row's cosine with the f32 reference > 0.9999,
+    except FinalAttention's weights exp(w): with |w| <= ~0.1 they sit at 1 +- a
+    few bf16 ulps (2^-8), so w = log of them is held to |dw| <= 8e-3 (a CPU
+    emulation of the bf16 chain, bf16 operands and f32 accumulation, is
+    4.2e-3 off the f32 reference; its row cosine 0.9967)."""
+    n = synthetic.SHAPES["mind_large_dev"][0]
+    table = W.news_table(1234, n, 1024, name="mind_large")
+    m = _model(pooler, gpu_device, 1234)
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    rng = np.random.default_rng(5)
+    rows = np.unique(np.concatenate([np.arange(128), np.arange(n - 128, n), rng.choice(n, 384, replace=False)]))
+    ref = pool_ref.per_news_tables(pooler, sd, table[torch.as_tensor(rows)]).double()
+    for dt in (torch.float32, torch.bfloat16):
+        eng = PoolScoreEngine(m, dtype=dt, device=gpu_device).load_news(table)
+        got = eng.transform()[torch.as_tensor(rows, device=gpu_device)].double().cpu()
+        parts = [(got, ref)] if pooler == "latent" else \
+            [(got[:, :1024], ref[:, :1024]), (got[:, 1024:].log(), ref[:, 1024:].log())]
+        for pi, (g, r) in enumerate(parts):
+            assert torch.isfinite(g).all()
+            if dt == torch.float32:
+                err = ((g - r).abs().amax(1) / r.abs().amax(1).clamp_min(1e-6)).max().item()
+                assert err <= 2e-5, (pooler, err)
+            elif pi == 1:
+                assert (g - r).abs().max().item() <= 8e-3, (pooler, (g - r).abs().max().item())
+            else:
+                cos = torch.nn.functional.cosine_similarity(g, r, dim=1)
+                assert cos.min().item() > 0.9999, (pooler, cos.min().item(), int(rows[int(cos.argmin())]))
+        del eng
+        torch.cuda.empty_cache()
+
+
 def test_eval_script_synthetic_end_to_end(gpu_device, tmp_path, monkeypatch):
     """scripts/eval.py runs (pipeline -> scores -> ranks -> metrics -> jsonl)."""
     import json
