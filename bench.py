@@ -349,6 +349,14 @@ def cpu_leg(args, dev) -> tuple:
             cpu_m = data_ref.score(pool_ref.dense_ranks(cpu_scores, sub.cand_len), grouped_y)
             parity[pooler] = {"impressions": done, "candidates": ncand,
                               "cpu_ref": {k: cpu_m[k] for k in ("auc", "mrr", "ndcg5", "ndcg10")}}
+            # the floor a bf16 table sets: the same CPU reference (f32 math) on the news
+            # table rounded to bf16 -- what storing the inputs in bf16 alone moves the AUC
+            _, _, _, s16 = cpu_reference(pooler, sub, table_c.bfloat16().float(), float("inf"))
+            m16 = data_ref.score(pool_ref.dense_ranks(s16, sub.cand_len), grouped_y)
+            parity[pooler]["cpu_ref_bf16_table"] = {
+                "auc": m16["auc"], "auc_abs_diff": abs(m16["auc"] - cpu_m["auc"]),
+                "max_abs_score_diff": float(np.abs(s16 - cpu_scores).max()),
+                "note": "CPU reference, f32 math, news table rounded to bf16: the AUC shift of bf16 inputs alone"}
             for dt in ("fp32", "bf16"):
                 eng = PoolScoreEngine(make_model(pooler, dev), dtype=DTYPES[dt], device=dev).load_news(table_d)
                 eng.load_impressions(sub.hist_idx, sub.hist_len, sub.cand_idx, sub.cand_len)

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""A/B timing of nr_pool_score builds (tools/pool_lab variants) on the headline
+workload (MIND-large-dev shape, latent + final, bf16), interleaved rounds in ONE
+process, HIP events; every build's scores are compared with the first's.
+
+    python tools/pool_ab.py --libs base=tools/pool_lab/libnewsrec_base.so wg64=... [--rounds 5]
+
+Tool only: the libraries are loaded with ctypes from their paths.
+"""
+import argparse
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO))
+
+from news_recommendation_project_v2_amd import synthetic  # noqa: E402
+from news_recommendation_project_v2_amd import weights as W  # noqa: E402
+from news_recommendation_project_v2_amd.engine import PoolScoreEngine  # noqa: E402
+
+POOL = {"final": 0, "latent": 1}
+
+
+def load(path):
+    lib = ctypes.CDLL(str(path))
+    _p, _i, _l = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    lib.nr_pool_score.restype = _i
+    lib.nr_pool_score.argtypes = [_i, _i, _l, _p, _l, _p, _l, _p, _p, _p, _p, _p, _l, _p, _p, _p]
+    lib.nr_last_error.restype = ctypes.c_char_p
+    return lib
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", nargs="+", required=True)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--poolers", default="latent,final")
+    ap.add_argument("--zipf", type=float, default=0.0)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    libs = {k: load(v) for k, v in (s.split("=", 1) for s in args.libs)}
+    n_news, n_imp = synthetic.SHAPES["mind_large_dev"]
+    imps = synthetic.mind_impressions(n_news, n_imp, seed=1234, zipf=args.zipf or None)
+    g = torch.Generator(device=dev).manual_seed(1234)
+    table = torch.randn((n_news, 1024), generator=g, device=dev)
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    for pooler in args.poolers.split(","):
+        from bench import make_model
+        eng = PoolScoreEngine(make_model(pooler, dev), dtype=torch.bfloat16, device=dev).load_news(table)
+        eng.load_impressions(imps.hist_idx, imps.hist_len, imps.cand_idx, imps.cand_len)
+        eng.hist_table = eng.transform()
+        eng.inv_norms()
+        k = 2 if pooler == "final" else 1
+        byt = imps.n_cand * (2048 + 12) + imps.n_hist * (k * 2048 + 4) + imps.n_imp * 16
+        outs = {n: torch.empty(imps.n_cand, dtype=torch.float32, device=dev) for n in libs}
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+        def call(name):
+            rc = libs[name].nr_pool_score(POOL[pooler], 1, 1024, p(eng.hist_table), eng.hist_table.shape[1],
+                                          p(eng.cand_table), 1024, p(eng.cand_inv), p(eng.hist_idx), p(eng.hist_off),
+                                          p(eng.cand_idx), p(eng.cand_off), imps.n_imp, p(outs[name]), None, s)
+            if rc != 0:
+                raise RuntimeError(libs[name].nr_last_error().decode())
+
+        times = {n: [] for n in libs}
+        for n in libs:
+            call(n)
+        torch.cuda.synchronize()
+        for _ in range(args.rounds):
+            for n in libs:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.reps):
+                    call(n)
+                e1.record()
+                torch.cuda.synchronize()
+                times[n].append(e0.elapsed_time(e1) / args.reps)
+        first = next(iter(libs))
+        for n in libs:
+            ms = float(np.median(times[n]))
+            print(json.dumps({"pooler": pooler, "zipf": args.zipf, "lib": n, "median_ms": round(ms, 4),
+                              "min_ms": round(min(times[n]), 4), "GBs": round(byt / ms / 1e6, 1),
+                              "max_diff_vs_first": float((outs[n] - outs[first]).abs().max())}), flush=True)
+        del eng
+
+
+if __name__ == "__main__":
+    main()
