@@ -103,11 +103,15 @@ class LatentAttentionModel(torch.nn.Module):
 
     def __init__(self):
         super().__init__()
-        if EMBEDDING_DIM == 4096:  # latent_attention.py:91-97
-            num_latents, latent_dim, heads, dim_head = 32, REDUCED_DIM, 2, 32
-        else:
-            num_latents, latent_dim, heads, dim_head = (LATENT_NUM_LATENTS, REDUCED_DIM, LATENT_CROSS_HEADS,
-                                                        LATENT_CROSS_DIM_HEAD)
+        if EMBEDDING_DIM != 1024:
+            # the reference's EMBEDDING_DIM == 4096 branch (latent_attention.py:91-97: 32
+            # latents, 2 heads of 32, the NV-Embed experiment) is out of scope:
+            # nr_pool_score and the transforms are built for D = 1024 only, so refuse here
+            # rather than construct a model every kernel would reject
+            raise NotImplementedError(f"LatentAttentionModel: EMBEDDING_DIM={EMBEDDING_DIM}; the HIP path "
+                                      "supports 1024 (the e5-large-instruct / XLM-R-large width) only")
+        num_latents, latent_dim, heads, dim_head = (LATENT_NUM_LATENTS, REDUCED_DIM, LATENT_CROSS_HEADS,
+                                                    LATENT_CROSS_DIM_HEAD)
         dim = REDUCED_DIM
         self.cross_attend_blocks = torch.nn.ModuleList([
             PreNorm(latent_dim, Attention(latent_dim, dim, heads=heads, dim_head=dim_head), context_dim=dim),
