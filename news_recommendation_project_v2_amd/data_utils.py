@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import json
 from pathlib import Path
-from typing import Any, Callable, Optional, Sequence
+from typing import Any, Callable, Iterable, Optional, Sequence
 
 import numpy as np
 import torch
@@ -209,6 +209,12 @@ def to_csr(rev_index: np.ndarray, len_list: np.ndarray, device=None):
     if device is not None:
         idx, off = idx.to(device), off.to(device)
     return idx, off
+
+
+def eval_collate_fn(input: Iterable[str], tokenizer, max_len: int):
+    """Tokenise a batch of texts, right-padded to the batch's longest and
+    truncated at max_len (data_utils.py:471-482)."""
+    return tokenizer(list(input), max_length=max_len, padding=True, truncation=True, return_tensors="pt")
 
 
 class NewsTextDataset(Dataset):

@@ -191,3 +191,53 @@ def get_latent_attention_model(model_path: Optional[Path] = None) -> LatentAtten
 
 def normalize(x: torch.Tensor) -> torch.Tensor:
     return F.normalize(x, p=2, dim=1)
+
+
+# ---------------------------------------------------------------- title encoder API
+# The reference's encoder entry points (modeling_utils.py:62-103, 282-323), kept
+# by name and argument meaning over the packed-varlen HIP encoder (encoder.py):
+# the HF model object becomes an ``XLMREncoder``; batches stay the tokenizer's
+# right-padded ``input_ids`` / ``attention_mask``; pooling happens on the device.
+
+def output_pool(model):
+    """Pooling function of an encoder (modeling_utils.py:62-75): average_pool for
+    the XLM-R architecture (e5-large-instruct), the only one on the HIP path;
+    Qwen2 / NewModel / NV-Embed are out of scope and raise."""
+    from .encoder import XLMREncoder
+    if isinstance(model, XLMREncoder):
+        return average_pool
+    raise NotImplementedError(f"output_pool: {type(model).__name__} is not an XLM-R encoder on the HIP path")
+
+
+def get_model_and_tokenizer(path: str, device=DEVICE, dtype: torch.dtype = torch.float32):
+    """(encoder, tokenizer) for a LOCAL XLM-R directory (modeling_utils.py:92-103;
+    no hub download).  ``dtype`` is the compute dtype of the HIP encoder (f32 for
+    BASELINE config 2; bf16 for throughput)."""
+    from transformers import AutoTokenizer
+
+    from .encoder import XLMREncoder
+    model = XLMREncoder.from_pretrained_dir(path, dtype=dtype, device=torch.device(device))
+    return model, AutoTokenizer.from_pretrained(path)
+
+
+def get_text_embed_eval(model, input_dataloader) -> torch.Tensor:
+    """average_pool(last_hidden_state) of every batch, concatenated on the host
+    (modeling_utils.py:282-300).  Each batch is a mapping with right-padded
+    ``input_ids`` and ``attention_mask`` (eval_collate_fn's BatchEncoding); the
+    padded slots are dropped and the sequences run packed through
+    nr_encoder_forward, so only [B, 1024] leaves the device."""
+    output_pool(model)  # architecture check, as the reference selects its pool here
+    out = [model.encode_padded(inputs["input_ids"], inputs["attention_mask"]).cpu() for inputs in input_dataloader]
+    return torch.cat(out) if out else torch.zeros((0, EMBEDDING_DIM))
+
+
+def get_embed_from_model(model, text_dataset, text_maxlen: int, text_collate_fn,
+                         batch_size: int = 1024) -> torch.Tensor:
+    """modeling_utils.py:304-323: a sequential DataLoader over the texts, then
+    get_text_embed_eval.  The reference sizes its batch by a GPU-OOM probe; here
+    the batch only sets how many sequences the host tokenises at a time (the
+    device works on packed tokens in chunks of ``model.max_tokens``)."""
+    from torch.utils.data import DataLoader
+    del text_maxlen  # applied by text_collate_fn (eval_collate_fn's max_len)
+    loader = DataLoader(text_dataset, batch_size=batch_size, collate_fn=text_collate_fn, shuffle=False)
+    return get_text_embed_eval(model, loader)
