@@ -4,8 +4,9 @@ The reference has no distributed code; this is the one
 parallel strategy the hot path needs:
   phase A  each rank runs the per-news pooler transform on a contiguous
            1/world slice of the news table (MFMA GEMMs, no communication);
-  phase B  ONE all_gather_into_tensor of the [N/world, k*1024] slices
-           (RCCL ncclAllGather over xGMI) gives every GPU the full table;
+  phase B  the all-gather of the [N/world, k*1024] slices (RCCL ncclAllGather
+           over xGMI) gives every GPU the full table; the shard is transformed
+           in two chunks and chunk 0's all-gather overlaps chunk 1's transform;
   phase C  impressions are split into contiguous, cost-balanced ranges and
            pooled + scored with no further communication.
 Scores stay on their rank; ``gather_scores`` concatenates them in impression
@@ -47,10 +48,30 @@ def partition_by_cost(hist_len: np.ndarray, cand_len: np.ndarray, world: int, ta
     return np.maximum.accumulate(b).astype(np.int64)
 
 
-class ShardedTable:
-    """Phase A + B: sharded per-news transform and the one-time all-gather."""
+# the shard's transform is cut in two (rows permitting) so that the all-gather of
+# the first half runs on the communicator's stream while the second half is
+# transformed.  Measured price of the cut alone (tools/chunk_probe.py, latent
+# bf16, profiles/round2/overlap/chunks.jsonl): +0.07 ms at 36 k shard rows
+# (N = 2), +0.05 at 18 k (N = 4), +0.19 at 9 k (N = 8, where the chain's
+# K = 4096 GEMM is one tile round either way) -- against half of the
+# all-gather (74 / 110 / 129 MB inbound per GPU at N = 2 / 4 / 8 over 1 / 3 /
+# 7 xGMI links).  So: two chunks for shards of >= 2 x CHUNK_MIN_ROWS rows.
+CHUNK_MIN_ROWS = 8192
+# CUs left to RCCL's kernels while the persistent GEMMs of an overlapped chunk
+# run (a persistent GEMM workgroup holds a whole CU)
+RCCL_CUS = 16
 
-    def __init__(self, engine: PoolScoreEngine, rank: int, world: int, group=None):
+
+class ShardedTable:
+    """Phase A + B: sharded per-news transform and the one-time all-gather.
+
+    With ``chunks`` > 1 (default 2 at world > 1 when each half has at least
+    CHUNK_MIN_ROWS rows) the shard's rows are transformed chunk by chunk and
+    each chunk is all-gathered asynchronously (``dist.all_gather`` into the
+    rank-major table's row ranges) while the next chunk is transformed; the
+    persistent GEMMs of the chunks then run on all but RCCL_CUS CUs."""
+
+    def __init__(self, engine: PoolScoreEngine, rank: int, world: int, group=None, chunks: Optional[int] = None):
         self.eng, self.rank, self.world, self.group = engine, rank, world, group
         n = engine.hist_src.shape[0]
         self.rows = shard_rows(n, world)
@@ -73,8 +94,36 @@ class ShardedTable:
         in_place = world == 1 or not _host_staged(group)
         self.local = self.full[rank * self.rows:(rank + 1) * self.rows] if in_place else \
             torch.empty((self.rows, width), dtype=engine.dtype, device=engine.device)
+        if chunks is None:
+            chunks = 2 if world > 1 and self.rows >= 2 * CHUNK_MIN_ROWS else 1
+        self.chunks = max(1, min(int(chunks), self.rows))
+        self.bounds = [round(c * self.rows / self.chunks) for c in range(self.chunks + 1)]
+
+    def _overlapped(self) -> None:
+        """Transform chunk c, then all-gather it asynchronously (byte views: any
+        dtype, any backend) while chunk c + 1 is transformed."""
+        from . import ops
+        reserve = self.full.is_cuda and self.chunks > 1
+        if reserve:
+            ncu = torch.cuda.get_device_properties(self.full.device).multi_processor_count
+            ops.set_persistent_workgroups(max(8, (ncu - RCCL_CUS) // 8 * 8))
+        works = []
+        try:
+            for a, b in zip(self.bounds[:-1], self.bounds[1:]):
+                self.eng.transform(rows=slice(self.lo + a, self.lo + b), out=self.local[a:b], src=self.src)
+                outs = [self.full[r * self.rows + a:r * self.rows + b].view(torch.uint8) for r in range(self.world)]
+                works.append(dist.all_gather(outs, self.local[a:b].view(torch.uint8), group=self.group, async_op=True))
+        finally:
+            if reserve:
+                ops.set_persistent_workgroups(0)
+        for w in works:
+            w.wait()
 
     def build(self) -> torch.Tensor:
+        if self.world > 1 and not (_host_staged(self.group) and self.local.is_cuda):
+            self._overlapped()
+            self.eng.hist_table = self.full
+            return self.full
         self.eng.transform(rows=slice(self.lo, self.lo + self.rows), out=self.local, src=self.src)
         if self.world > 1:
             if _host_staged(self.group) and self.local.is_cuda:
@@ -83,8 +132,6 @@ class ShardedTable:
                 dist.all_gather_into_tensor(host.view(torch.uint8), self.local.cpu().view(torch.uint8),
                                             group=self.group)
                 self.full.copy_(host)
-            else:
-                dist.all_gather_into_tensor(self.full, self.local, group=self.group)
         self.eng.hist_table = self.full
         return self.full
 

@@ -44,14 +44,15 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_news, q):
+def _worker(rank, world, port, n_news, q, chunks=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         table = torch.arange(n_news * 1024, dtype=torch.float32).reshape(n_news, 1024) / 1000.0
         eng = StubEngine(table.clone())
-        st = ShardedTable(eng, rank, world)
+        st = ShardedTable(eng, rank, world, chunks=chunks)
+        assert st.chunks == (chunks or 1)
         full = st.build()
         ok_table = (torch.equal(full[:n_news], table * 2 + 1) and eng.hist_table is full
                     and torch.equal(eng.hist_src, table))  # the engine's source table is not modified
@@ -63,13 +64,16 @@ def _worker(rank, world, port, n_news, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_news", [10, 11])
-def test_sharded_table_and_gather_gloo(n_news):
+@pytest.mark.parametrize("n_news,chunks", [(10, None), (11, None), (11, 2), (23, 3)])
+def test_sharded_table_and_gather_gloo(n_news, chunks):
+    """chunks > 1: the shard is transformed chunk by chunk, each chunk
+    all-gathered asynchronously into the rank-major table (the overlapped path
+    RCCL ranks take; ragged chunk sizes and a zero-padded last shard)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_news, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_news, q, chunks)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]

@@ -526,3 +526,30 @@ def test_train_v3_and_save_emb_scripts_synthetic(gpu_device, tmp_path, monkeypat
     q = torch.load(tmp_path / "emb" / "query_MINDsmall_dev.pt", weights_only=True)
     assert t.shape == q.shape and t.shape[1] == 1024
     assert torch.allclose(t.norm(dim=1), torch.ones(t.shape[0]), atol=1e-4)
+
+
+@pytest.mark.parametrize("pooler", ["final", "latent"])
+def test_sharded_table_overlapped_rccl_single_rank(gpu_device, pooler, tmp_path):
+    """The overlapped transform / all-gather path RCCL ranks take (chunks
+    transformed with the persistent GEMMs on all but RCCL_CUS CUs, each chunk
+    all-gathered asynchronously on the communicator's stream), run on a real
+    one-rank RCCL group (two RCCL ranks cannot share the box's one GPU): the
+    gathered table equals the one-shot transform bit for bit, and the
+    persistent-workgroup budget is restored afterwards."""
+    import torch.distributed as dist
+    from news_recommendation_project_v2_amd.distributed import ShardedTable
+    dist.init_process_group("nccl", init_method=f"file://{tmp_path / 'store'}", rank=0, world_size=1,
+                            device_id=gpu_device)
+    try:
+        table = W.news_table(7, 20011, 1024, name="overlap")
+        eng = PoolScoreEngine(_model(pooler, gpu_device, 7), dtype=torch.bfloat16, device=gpu_device).load_news(table)
+        want = eng.transform().clone()
+        st = ShardedTable(eng, 0, 1, chunks=3)
+        st._overlapped()
+        torch.cuda.synchronize()
+        assert torch.equal(st.full[:20011], want)
+        again = eng.transform()  # the knob is back at one workgroup per CU
+        torch.cuda.synchronize()
+        assert torch.equal(again, want)
+    finally:
+        dist.destroy_process_group()
