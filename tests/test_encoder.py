@@ -176,3 +176,41 @@ def test_reference_encoder_api_padded_batches(gpu_device):
     np.testing.assert_allclose(emb.numpy(), g["emb_mean"], rtol=1e-4, atol=1e-4)
     with pytest.raises(NotImplementedError):
         mu.output_pool(torch.nn.Linear(2, 2))
+
+
+@pytest.mark.gpu
+def test_integration_md_encoder_binding_runs_against_hf(gpu_device):
+    """The reference-side ctypes binding of get_text_embed_eval that
+    INTEGRATION.md shows (executed from the document itself) reproduces the
+    transformers XLMRobertaModel + average_pool the reference runs
+    (modeling_utils.py:282-300), on a random 2-layer XLM-R-shaped model."""
+    import re
+    from pathlib import Path
+    from transformers import XLMRobertaConfig, XLMRobertaModel
+    from news_recommendation_project_v2_amd import _lib
+    from news_recommendation_project_v2_amd.modeling_utils import average_pool
+    doc = (Path(__file__).resolve().parents[1] / "INTEGRATION.md").read_text()
+    block = re.search(r"```python\n(# reference: src/news_rec_utils/modeling_utils.py\n.*?)```", doc, re.S).group(1)
+    block = block.replace("/path/to/news_recommendation_project_v2_amd/libnewsrec_hip.so", str(_lib.LIB_PATH))
+    ns = {}
+    exec(compile(block, "INTEGRATION.md", "exec"), ns)
+    torch.manual_seed(0)
+    cfg = XLMRobertaConfig(vocab_size=1000, hidden_size=1024, num_hidden_layers=2, num_attention_heads=16,
+                           intermediate_size=4096, max_position_embeddings=514, layer_norm_eps=1e-5,
+                           type_vocab_size=1, pad_token_id=1)
+    model = XLMRobertaModel(cfg, add_pooling_layer=False).eval()
+    rng = np.random.default_rng(0)
+    lens = [5, 17, 9, 30]
+    batches = []
+    for chunk in (lens[:2], lens[2:]):
+        L = max(chunk)
+        ids = torch.ones((len(chunk), L), dtype=torch.long)
+        mask = torch.zeros((len(chunk), L), dtype=torch.long)
+        for r, n in enumerate(chunk):
+            ids[r, :n] = torch.as_tensor(rng.integers(3, 1000, n))
+            mask[r, :n] = 1
+        batches.append({"input_ids": ids, "attention_mask": mask})
+    got = ns["get_text_embed_eval"](model, batches)
+    with torch.no_grad():
+        want = torch.cat([average_pool(model(**b).last_hidden_state, b["attention_mask"]) for b in batches])
+    np.testing.assert_allclose(got.numpy(), want.numpy(), rtol=0, atol=1e-4)
