@@ -553,3 +553,25 @@ def test_sharded_table_overlapped_rccl_single_rank(gpu_device, pooler, tmp_path)
         assert torch.equal(again, want)
     finally:
         dist.destroy_process_group()
+
+
+def test_integration_md_pool_binding_matches_oracle(gpu_device):
+    """The reference-side ctypes replacement of get_cos_sim_scores that
+    INTEGRATION.md shows (executed from the document) gives the oracle's
+    FinalAttention scores within 1e-4 (f32) -- for a model left on the CPU too."""
+    import re
+    from pathlib import Path
+    from news_recommendation_project_v2_amd import _lib
+    doc = (Path(__file__).resolve().parents[1] / "INTEGRATION.md").read_text()
+    block = re.search(r"```python\n(# reference: src/news_rec_utils/data_model_helper.py\n.*?)```", doc, re.S).group(1)
+    ns = {}
+    exec(compile(block.replace("/path/to/news_recommendation_project_v2_amd/libnewsrec_hip.so", str(_lib.LIB_PATH)),
+                 "INTEGRATION.md", "exec"), ns)
+    imps = synthetic.mind_impressions(600, 150, seed=3)
+    table = W.news_table(3, imps.n_news, 1024, name="integ")
+    m = FinalAttention(1024, 4096)
+    m.load_state_dict(W.final_attention_state_dict(3))
+    got = ns["get_cos_sim_scores"](imps.hist_idx, imps.hist_len, imps.cand_idx, imps.cand_len, table, m.eval())
+    ref = pool_ref.cos_sim_scores("final", {k: v.detach() for k, v in m.state_dict().items()}, imps.hist_idx,
+                                  imps.hist_len, imps.cand_idx, imps.cand_len, table)
+    np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=0, atol=1e-4)
