@@ -549,12 +549,28 @@ def main():
                           "pool_score_GBs": round(ps_bytes(im, args.pooler, es) / (st[2] * 1e-3) / 1e9, 1)}
             del r, tb, im
             torch.cuda.empty_cache()
+        # MIND's user structure: ~256 k users' histories repeated over 376 k impressions
+        # (synthetic.MIND_LARGE_DEV_USERS, an assumption); the engine then pools each
+        # distinct history once (automatic at >= 15 % repeats), the fused pass beside it
+        im = synthetic.mind_impressions(n_news, n_imp, seed=1234, users=synthetic.MIND_LARGE_DEV_USERS)
+        sh = {"users": synthetic.MIND_LARGE_DEV_USERS, "impressions": im.n_imp, "candidates": im.n_cand}
+        for tag, mode in (("distinct_histories_pooled_once", None), ("fused_per_impression", False)):
+            r = Run(args.pooler, args.dtype, im, table, dev, rank, world)
+            r.eng.load_impressions(im.hist_idx, im.hist_len, im.cand_idx, im.cand_len, dedupe=mode)
+            d = timed(r.step, 3, 1, world, dev, host_reduce) / 3
+            sh[tag] = {"value": round(im.n_cand / d, 1), "ms_per_step": round(d * 1e3, 3)}
+            sh["repeated_history_share"] = round(r.eng.shared_history_share, 4) if mode is None else \
+                sh.get("repeated_history_share")
+            del r
+            torch.cuda.empty_cache()
+        extra["shared_histories"] = sh
+        del im
         extra["metrics_ms"] = round(metrics_ms(head), 3)
         # PCIe-side costs (never part of `value`): the CSR index upload incl. its host-side
         # offsets (load_impressions is idempotent) and the score download
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        head.eng.load_impressions(imps.hist_idx, imps.hist_len, imps.cand_idx, imps.cand_len)
+        head.eng.load_impressions(imps.hist_idx, imps.hist_len, imps.cand_idx, imps.cand_len, dedupe=False)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         head.scores.cpu()

@@ -207,6 +207,20 @@ int nr_pool_score(int pooler, int dtype, int64_t dim, const void* hist_table, in
                   void* stream);
 
 /*
+ * Candidate scoring against stored user vectors: score_c = (u . e_c) /
+ * max(|u|, 1e-8) * cand_inv_norm[c] with u = users[user_idx[i]] (f32 rows of
+ * dim), for impressions that share a history (MIND: one history per user
+ * across the user's impressions).  users is the `users` output of an
+ * nr_pool_score pooling-only call (cand_off NULL) over the DISTINCT histories;
+ * the scores are then bit-identical to nr_pool_score's fused pass, which
+ * re-gathers a shared history once per impression.  Same tables, CSR and
+ * dim rules as nr_pool_score.
+ */
+int nr_score_users(int dtype, int64_t dim, const float* users, const int32_t* user_idx, const void* cand_table,
+                   int64_t cand_ld, const float* cand_inv_norm, const int32_t* cand_idx, const int64_t* cand_off,
+                   int64_t n_imp, float* scores, void* stream);
+
+/*
  * Dense descending rank per impression: ranks[c] = 1 + number of distinct
  * scores of the same impression that are strictly greater.  Bit-exact
  * restatement of scipy.stats.rankdata(-x, method="dense") used by

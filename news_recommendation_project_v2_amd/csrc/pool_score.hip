@@ -102,13 +102,17 @@ __device__ __forceinline__ float reduce4(const float (&d)[4], int lane) {
   return b;
 }
 
-template <typename T, int POOL, int DIM>
+// FROM_USERS: the user vector of impression i is row uidx[i] of a table of
+// user vectors this kernel wrote earlier (users output of a pooling-only
+// launch over the distinct histories), instead of its own history gather; the
+// candidate pass is the same code, so the scores are bit-identical.
+template <typename T, int POOL, int DIM, bool FROM_USERS = false>
 __global__ __launch_bounds__(256) void pool_score_kernel(
     const T* __restrict__ htab, int64_t hld, const T* __restrict__ ctab, int64_t cld,
     const float* __restrict__ cinv, const int32_t* __restrict__ hidx,
     const int64_t* __restrict__ hoff, const int32_t* __restrict__ cidx,
     const int64_t* __restrict__ coff, int64_t n_imp, float* __restrict__ scores,
-    float* __restrict__ users) {
+    float* __restrict__ users, const int32_t* __restrict__ uidx) {
   using F = RowFmt<T, DIM>;
   constexpr int NL = F::NL, EPL = F::EPL;
   constexpr int R = PoolCfg<T, POOL>::R;
@@ -118,6 +122,12 @@ __global__ __launch_bounds__(256) void pool_score_kernel(
   const int64_t imp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (imp >= n_imp) return;  // wave-uniform
 
+  float u[EPL];
+  if constexpr (FROM_USERS) {
+    const float* ur = users + (int64_t)uidx[imp] * DIM;
+#pragma unroll
+    for (int i = 0; i < EPL; ++i) u[i] = ur[elem_pos<T, DIM>(i, lane)];
+  } else {
   float acc[EPL];
   float den[EPL];
 #pragma unroll
@@ -177,7 +187,6 @@ __global__ __launch_bounds__(256) void pool_score_kernel(
   }
 
   // ---------------- user vector ----------------
-  float u[EPL];
   if constexpr (POOL == NR_POOL_FINAL) {
     // modeling_utils.py:224-228: w = exp(w)*m; w /= (sum w + 1e-10); sum x*w
 #pragma unroll
@@ -197,16 +206,16 @@ __global__ __launch_bounds__(256) void pool_score_kernel(
 #pragma unroll
     for (int i = 0; i < EPL; ++i) u[i] = u[i] / den1;
   }
-  float ss = 0.f;
-#pragma unroll
-  for (int i = 0; i < EPL; ++i) ss = fmaf(u[i], u[i], ss);
-  const float inv_u = 1.0f / fmaxf(sqrtf(wave_sum(ss)), 1e-8f);
-
   if (users != nullptr) {
     float* ur = users + imp * DIM;
 #pragma unroll
     for (int i = 0; i < EPL; ++i) ur[elem_pos<T, DIM>(i, lane)] = u[i];
   }
+  }  // !FROM_USERS
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) ss = fmaf(u[i], u[i], ss);
+  const float inv_u = 1.0f / fmaxf(sqrtf(wave_sum(ss)), 1e-8f);
 
   // ---------------- candidate scoring ----------------
   if (coff == nullptr) return;  // pooling only
@@ -245,15 +254,15 @@ __global__ __launch_bounds__(256) void pool_score_kernel(
   }
 }
 
-template <typename T, int POOL>
+template <typename T, int POOL, bool FROM_USERS = false>
 static int launch_pool_score(const void* ht, int64_t hld, const void* ct, int64_t cld,
                              const float* cinv, const int32_t* hidx, const int64_t* hoff,
                              const int32_t* cidx, const int64_t* coff, int64_t n_imp,
-                             float* scores, float* users, hipStream_t s) {
+                             float* scores, float* users, hipStream_t s, const int32_t* uidx = nullptr) {
   const int64_t blocks = (n_imp + 3) / 4;
-  hipLaunchKernelGGL((pool_score_kernel<T, POOL, 1024>), dim3((unsigned)blocks), dim3(256), 0, s,
+  hipLaunchKernelGGL((pool_score_kernel<T, POOL, 1024, FROM_USERS>), dim3((unsigned)blocks), dim3(256), 0, s,
                      (const T*)ht, hld, (const T*)ct, cld, cinv, hidx, hoff, cidx, coff, n_imp,
-                     scores, users);
+                     scores, users, uidx);
   NR_CHECK_LAUNCH("nr_pool_score");
   return NR_OK;
 }
@@ -318,4 +327,31 @@ extern "C" int nr_pool_score(int pooler, int dtype, int64_t dim, const void* his
   if (pooler == NR_POOL_FINAL)
     return nr::launch_pool_score<__bf16, NR_POOL_FINAL>(hist_table, hist_ld, cand_table, cand_ld, cand_inv_norm, hist_idx, hist_off, cand_idx, cand_off, n_imp, scores, users, s);
   return nr::launch_pool_score<__bf16, NR_POOL_LATENT>(hist_table, hist_ld, cand_table, cand_ld, cand_inv_norm, hist_idx, hist_off, cand_idx, cand_off, n_imp, scores, users, s);
+}
+
+extern "C" int nr_score_users(int dtype, int64_t dim, const float* users, const int32_t* user_idx,
+                              const void* cand_table, int64_t cand_ld, const float* cand_inv_norm,
+                              const int32_t* cand_idx, const int64_t* cand_off, int64_t n_imp, float* scores,
+                              void* stream) {
+  nr::clear_error();
+  if (dim != 1024) {
+    nr::set_error("nr_score_users: dim %lld unsupported (1024 only)", (long long)dim);
+    return NR_ERR_UNSUPPORTED;
+  }
+  NR_CHECK_ARG(dtype == NR_F32 || dtype == NR_BF16, "nr_score_users: bad dtype %d", dtype);
+  NR_CHECK_ARG(n_imp >= 0, "nr_score_users: n_imp < 0");
+  if (n_imp == 0) return NR_OK;
+  NR_CHECK_ARG(users && user_idx && cand_table && cand_inv_norm && cand_idx && cand_off && scores,
+               "nr_score_users: null pointer");
+  NR_CHECK_ARG(cand_ld >= dim && cand_ld % (dtype == NR_F32 ? 4 : 8) == 0 && ((uintptr_t)cand_table & 15) == 0,
+               "nr_score_users: cand_table must be 16-byte aligned with 16-byte row strides");
+  hipStream_t s = (hipStream_t)stream;
+  // the pooler only shaped the stored user vectors; the scoring pass is pooler-independent
+  if (dtype == NR_F32)
+    return nr::launch_pool_score<float, NR_POOL_MEAN, true>(nullptr, 0, cand_table, cand_ld, cand_inv_norm, nullptr,
+                                                            nullptr, cand_idx, cand_off, n_imp, scores,
+                                                            const_cast<float*>(users), s, user_idx);
+  return nr::launch_pool_score<__bf16, NR_POOL_MEAN, true>(nullptr, 0, cand_table, cand_ld, cand_inv_norm, nullptr,
+                                                           nullptr, cand_idx, cand_off, n_imp, scores,
+                                                           const_cast<float*>(users), s, user_idx);
 }

@@ -175,6 +175,54 @@ def lengths_to_offsets(lengths: np.ndarray) -> np.ndarray:
     return off
 
 
+_H1, _H2 = np.uint64(0x9E3779B97F4A7C15), np.uint64(0xC2B2AE3D27D4EB4F)
+
+
+def distinct_segments(idx: np.ndarray, lens: np.ndarray):
+    """Group identical segments of a CSR index array (same length, same ids in
+    the same order): MIND repeats a user's history on every impression of that
+    user.  Returns (group [n] int64, first [g] int64): segment i equals segment
+    first[group[i]], groups numbered by first occurrence.  Two 64-bit
+    polynomial hashes keyed with the length find candidates; every segment is
+    then compared element by element with its group's first segment, so the
+    grouping is exact (a hash collision falls back to no grouping)."""
+    idx = np.asarray(idx, dtype=np.int64)
+    lens = np.asarray(lens, dtype=np.int64)
+    n = len(lens)
+    if n == 0:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    off = lengths_to_offsets(lens)
+    seg = np.repeat(np.arange(n), lens)
+    pos = np.arange(len(idx), dtype=np.int64) - off[:-1][seg]
+    maxl = int(lens.max())
+    p1, p2 = np.ones(max(maxl, 1), np.uint64), np.ones(max(maxl, 1), np.uint64)
+    with np.errstate(over="ignore"):
+        for k in range(1, maxl):
+            p1[k] = p1[k - 1] * _H1
+            p2[k] = p2[k - 1] * _H2
+        v = idx.astype(np.uint64) + np.uint64(1)
+        h1, h2 = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+        nz = lens > 0
+        if nz.any():
+            h1[nz] = np.add.reduceat(v * p1[pos], off[:-1][nz])
+            h2[nz] = np.add.reduceat(v * p2[pos], off[:-1][nz])
+    order = np.lexsort((np.arange(n), h2, h1, lens))  # ties keep segment order: first occurrence leads
+    k_l, k_1, k_2 = lens[order], h1[order], h2[order]
+    new = np.ones(n, bool)
+    new[1:] = (k_l[1:] != k_l[:-1]) | (k_1[1:] != k_1[:-1]) | (k_2[1:] != k_2[:-1])
+    gsorted = np.cumsum(new) - 1
+    first_of_g = order[new]                      # first occurrence of each group (sorted-key order)
+    renum = np.empty(len(first_of_g), np.int64)  # renumber groups by first occurrence
+    renum[np.argsort(first_of_g, kind="stable")] = np.arange(len(first_of_g))
+    group = np.empty(n, np.int64)
+    group[order] = renum[gsorted]
+    first = np.sort(first_of_g)
+    rep_pos = off[:-1][first[group]][seg] + pos
+    if not np.array_equal(idx, idx[rep_pos]):    # a hash collision: do not group
+        return np.arange(n, dtype=np.int64), np.arange(n, dtype=np.int64)
+    return group, first
+
+
 def rank_group_preds(pred_scores: np.ndarray, imp_counts: np.ndarray) -> np.ndarray:
     """Per-impression dense descending ranks (data_utils.py:414-415), computed by
     the HIP kernel ``nr_dense_rank`` and grouped into an object array of int64

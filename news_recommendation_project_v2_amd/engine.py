@@ -20,7 +20,13 @@ import numpy as np
 import torch
 
 from . import ops
-from .data_utils import lengths_to_offsets
+from .data_utils import distinct_segments, lengths_to_offsets
+
+# below this share of impressions that repeat an earlier impression's history,
+# the fused pass (which re-gathers a shared history per impression) moves fewer
+# bytes than pooling the distinct histories into f32 user rows (+4 KiB written
+# and +4 KiB read per user row): break-even ~ 2 x 4 KiB / (33 x 2 KiB) ~ 0.12
+DEDUPE_MIN_SHARE = 0.15
 
 
 class PoolScoreEngine:
@@ -47,16 +53,35 @@ class PoolScoreEngine:
             self.hist_src = self.cand_table
         return self
 
-    def load_impressions(self, hist_idx, hist_len, cand_idx, cand_len):
+    def load_impressions(self, hist_idx, hist_len, cand_idx, cand_len, dedupe: Optional[bool] = None):
+        """Upload the CSR index arrays.  ``dedupe`` (default: automatic) pools
+        each DISTINCT history once (MIND repeats a user's history on every
+        impression of that user) and scores the candidates against the stored
+        user rows: same scores bit for bit, fewer gathered bytes once at least
+        DEDUPE_MIN_SHARE of the impressions repeat a history."""
         dev = self.device
-        self.hist_idx = torch.as_tensor(np.ascontiguousarray(hist_idx, dtype=np.int32)).to(dev)
+        if len(hist_len) != len(cand_len):
+            raise ValueError("Number of rows should be consistent")  # data_model_helper.py:183-185
+        hist_idx = np.ascontiguousarray(hist_idx, dtype=np.int32)
+        hist_len = np.asarray(hist_len, dtype=np.int64)
+        self.hist_idx = torch.as_tensor(hist_idx).to(dev)
         self.hist_off = torch.as_tensor(lengths_to_offsets(hist_len)).to(dev)
         self.cand_idx = torch.as_tensor(np.ascontiguousarray(cand_idx, dtype=np.int32)).to(dev)
         self.cand_off = torch.as_tensor(lengths_to_offsets(cand_len)).to(dev)
         self.n_cand = int(np.asarray(cand_len, dtype=np.int64).sum())
         self.n_imp = len(cand_len)
-        if len(hist_len) != len(cand_len):
-            raise ValueError("Number of rows should be consistent")  # data_model_helper.py:183-185
+        self.user_idx = None
+        self.shared_history_share = 0.0
+        if dedupe is not False and self.n_imp:
+            group, first = distinct_segments(hist_idx, hist_len)
+            self.shared_history_share = 1.0 - len(first) / self.n_imp
+            if dedupe or self.shared_history_share >= DEDUPE_MIN_SHARE:
+                ho, ulen = lengths_to_offsets(hist_len), hist_len[first]
+                uoff = lengths_to_offsets(ulen)
+                rows = np.repeat(ho[:-1][first], ulen) + (np.arange(int(uoff[-1])) - np.repeat(uoff[:-1], ulen))
+                self.uhist_idx = torch.as_tensor(hist_idx[rows]).to(dev)
+                self.uhist_off = torch.as_tensor(uoff).to(dev)
+                self.user_idx = torch.as_tensor(group.astype(np.int32)).to(dev)
         return self
 
     # ------------------------------------------------------------ stages
@@ -85,6 +110,11 @@ class PoolScoreEngine:
         return self.cand_inv
 
     def pool_score(self, want_users: bool = False, scores: Optional[torch.Tensor] = None):
+        if self.user_idx is not None:  # distinct histories pooled once, then scored per impression
+            users = ops.pool_users(self.pooler, self.hist_table, self.uhist_idx, self.uhist_off)
+            s = ops.score_users(users, self.user_idx, self.cand_table, self.cand_inv, self.cand_idx, self.cand_off,
+                                self.n_cand, scores=scores)
+            return s, (users[self.user_idx.long()] if want_users else None)
         return ops.pool_score(self.pooler, self.hist_table, self.cand_table, self.cand_inv, self.hist_idx,
                               self.hist_off, self.cand_idx, self.cand_off, self.n_cand, want_users=want_users,
                               scores=scores)

@@ -224,6 +224,43 @@ def pool_score(pooler: str, hist_table: torch.Tensor, cand_table: torch.Tensor, 
     return scores, users
 
 
+def pool_users(pooler: str, hist_table: torch.Tensor, hist_idx: torch.Tensor, hist_off: torch.Tensor) -> torch.Tensor:
+    """Pooling only (nr_pool_score with no candidates): users [n, D] f32, one
+    row per history segment."""
+    dev = _dev(hist_table, hist_idx, hist_off)
+    _check_csr(hist_idx, hist_off, "hist")
+    n, dim = hist_off.numel() - 1, hist_table.shape[1] if pooler != "final" else hist_table.shape[1] // 2
+    users = torch.empty((n, dim), dtype=torch.float32, device=dev)
+    if n == 0:
+        return users
+    hidx = hist_idx if hist_idx.numel() else torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("nr_pool_score", POOLERS[pooler], _dtype(hist_table, "hist_table"), dim, _ptr(hist_table),
+              _rowmajor(hist_table, "hist_table"), None, 0, None, _ptr(hidx), _ptr(hist_off), None, None, n, None,
+              _ptr(users), _stream(dev))
+    return users
+
+
+def score_users(users: torch.Tensor, user_idx: torch.Tensor, cand_table: torch.Tensor, cand_inv_norm: torch.Tensor,
+                cand_idx: torch.Tensor, cand_off: torch.Tensor, n_cand: int,
+                scores: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Scores of every impression's candidates against users[user_idx[i]]
+    (nr_score_users); bit-identical to the fused pool_score pass."""
+    dev = _dev(users, user_idx, cand_table, cand_inv_norm, cand_idx, cand_off, scores)
+    _check_csr(cand_idx, cand_off, "cand")
+    if users.dtype != torch.float32 or not users.is_contiguous() or user_idx.dtype != torch.int32:
+        raise _lib.NewsRecHIPError("score_users: users contiguous f32, user_idx int32")
+    if user_idx.numel() != cand_off.numel() - 1:
+        raise _lib.NewsRecHIPError("score_users: one user index per impression")
+    if scores is None:
+        scores = torch.empty(n_cand, dtype=torch.float32, device=dev)
+    if n_cand == 0 or user_idx.numel() == 0:
+        return scores
+    _lib.call("nr_score_users", _dtype(cand_table, "cand_table"), cand_table.shape[1], _ptr(users), _ptr(user_idx),
+              _ptr(cand_table), _rowmajor(cand_table, "cand_table"), _ptr(cand_inv_norm), _ptr(cand_idx),
+              _ptr(cand_off), user_idx.numel(), _ptr(scores), _stream(dev))
+    return scores
+
+
 def dense_rank(scores: torch.Tensor, cand_off: torch.Tensor, check: bool = True) -> torch.Tensor:
     """Per-impression dense descending ranks (int32), scipy rankdata(-x, 'dense')."""
     dev = _dev(scores, cand_off)

@@ -63,9 +63,28 @@ class Impressions:
         return [self.labels[co[i]:co[i + 1]].astype(np.int64) for i in range(self.n_imp)]
 
 
+# MIND-large dev: 376,471 impressions of ~256 k users (public dataset statistics,
+# an assumption here): a user's history repeats on each of the user's impressions
+MIND_LARGE_DEV_USERS = 255_990
+
+
 def mind_impressions(n_news: int, n_imp: int, seed: int = 1234, mean_hist: float = 33.0,
                      mean_cand: float = 37.0, max_hist: int = 600, max_cand: int = 300,
-                     min_cand: int = 2, zipf: Optional[float] = None) -> Impressions:
+                     min_cand: int = 2, zipf: Optional[float] = None, users: Optional[int] = None) -> Impressions:
+    """``users``: draw that many histories and give every impression one of
+    them (each user at least once, the rest uniformly), as MIND repeats a
+    user's history on all of that user's impressions; None: one independent
+    history per impression (the survey's recipe, the headline workload)."""
+    if users is not None:
+        base = mind_impressions(n_news, n_imp, seed, mean_hist, mean_cand, max_hist, max_cand, min_cand, zipf)
+        rng = np.random.default_rng(seed + 7)
+        u = min(int(users), n_imp)
+        pick = np.concatenate([rng.permutation(u), rng.integers(0, u, n_imp - u)]).astype(np.int64)
+        ho = base.hist_off()  # user k owns impression k's history of the base draw
+        hl = base.hist_len[pick]
+        rows = np.repeat(ho[:-1][pick], hl) + (np.arange(int(hl.sum())) - np.repeat(np.cumsum(hl) - hl, hl))
+        return Impressions(n_news, base.hist_idx[rows], hl.astype(np.int32), base.cand_idx, base.cand_len,
+                           base.labels)
     rng = np.random.default_rng(seed)
     hist_len = np.clip(rng.geometric(1.0 / mean_hist, n_imp), 1, max_hist).astype(np.int32)
     cand_len = np.clip(rng.geometric(1.0 / mean_cand, n_imp), min_cand, max_cand).astype(np.int32)

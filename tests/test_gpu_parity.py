@@ -575,3 +575,37 @@ def test_integration_md_pool_binding_matches_oracle(gpu_device):
     ref = pool_ref.cos_sim_scores("final", {k: v.detach() for k, v in m.state_dict().items()}, imps.hist_idx,
                                   imps.hist_len, imps.cand_idx, imps.cand_len, table)
     np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=0, atol=1e-4)
+
+
+@pytest.mark.parametrize("pooler", ["final", "latent"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_shared_history_dedupe_bit_identical(gpu_device, pooler, dtype):
+    """Impressions that repeat a user's history (MIND's structure): the engine
+    pools each distinct history once (nr_pool_score pooling-only) and scores
+    against the stored user rows (nr_score_users).  Scores and users are bit
+    for bit the fused pass's, incl. empty / 64 / 65-slot histories, and the
+    f32 scores are the oracle's within 1e-4."""
+    imps = synthetic.mind_impressions(700, 500, seed=9, users=180)
+    hl = imps.hist_len.copy()
+    hl[[3, 40]] = [0, 65]  # ragged edges: an empty history and one past a 64-row index block
+    ho = imps.hist_off()
+    hidx = np.concatenate([imps.hist_idx[ho[i]:ho[i] + hl[i]] if i != 40 else
+                           np.resize(imps.hist_idx[ho[40]:ho[41]], 65) for i in range(imps.n_imp)]).astype(np.int32)
+    table = W.news_table(9, 700, 1024, name="dedupe")
+    m = _model(pooler, gpu_device, 9)
+    out = {}
+    for mode in (False, None):
+        eng = PoolScoreEngine(m, dtype=dtype, device=gpu_device).load_news(table)
+        eng.load_impressions(hidx, hl, imps.cand_idx, imps.cand_len, dedupe=mode)
+        assert (eng.user_idx is not None) == (mode is None)
+        s, u = eng.step(want_users=True)
+        torch.cuda.synchronize()
+        out[mode] = (s.cpu(), u.cpu(), eng.shared_history_share)
+    assert out[None][2] > 0.5
+    torch.testing.assert_close(out[None][0], out[False][0], rtol=0, atol=0, equal_nan=True)
+    torch.testing.assert_close(out[None][1], out[False][1], rtol=0, atol=0, equal_nan=True)
+    if dtype == torch.float32:
+        sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+        ref = pool_ref.cos_sim_scores(pooler, sd, hidx, hl, imps.cand_idx, imps.cand_len, table).numpy()
+        sel = np.repeat(hl > 0, imps.cand_len)  # an empty history: 0/0 in the reference's pooler too
+        np.testing.assert_allclose(out[None][0].numpy()[sel], ref[sel], rtol=0, atol=1e-4)
