@@ -42,11 +42,21 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--poolers", default="latent,final")
     ap.add_argument("--zipf", type=float, default=0.0)
+    ap.add_argument("--order", choices=["given", "cost_desc", "cost_asc"], default="given",
+                    help="impression order of the CSR arrays (the kernel runs impressions in launch order)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     libs = {k: load(v) for k, v in (s.split("=", 1) for s in args.libs)}
     n_news, n_imp = synthetic.SHAPES["mind_large_dev"]
     imps = synthetic.mind_impressions(n_news, n_imp, seed=1234, zipf=args.zipf or None)
+    if args.order != "given":
+        cost = imps.hist_len.astype(np.int64) + imps.cand_len
+        perm = np.argsort(-cost if args.order == "cost_desc" else cost, kind="stable")
+        ho, co = imps.hist_off(), imps.cand_off()
+        hrows = np.concatenate([np.arange(ho[i], ho[i + 1]) for i in perm])
+        crows = np.concatenate([np.arange(co[i], co[i + 1]) for i in perm])
+        imps = synthetic.Impressions(imps.n_news, imps.hist_idx[hrows], imps.hist_len[perm], imps.cand_idx[crows],
+                                     imps.cand_len[perm], imps.labels[crows])
     g = torch.Generator(device=dev).manual_seed(1234)
     table = torch.randn((n_news, 1024), generator=g, device=dev)
     p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
@@ -84,7 +94,7 @@ def main():
         first = next(iter(libs))
         for n in libs:
             ms = float(np.median(times[n]))
-            print(json.dumps({"pooler": pooler, "zipf": args.zipf, "lib": n, "median_ms": round(ms, 4),
+            print(json.dumps({"pooler": pooler, "zipf": args.zipf, "order": args.order, "lib": n, "median_ms": round(ms, 4),
                               "min_ms": round(min(times[n]), 4), "GBs": round(byt / ms / 1e6, 1),
                               "max_diff_vs_first": float((outs[n] - outs[first]).abs().max())}), flush=True)
         del eng
