@@ -29,6 +29,18 @@ from .data_utils import distinct_segments, lengths_to_offsets
 DEDUPE_MIN_SHARE = 0.15
 
 
+def _may_repeat(hist_idx: np.ndarray, hist_len: np.ndarray) -> bool:
+    """Cheap bound before the exact grouping: repeated histories share (length,
+    first id, last id), so if fewer than DEDUPE_MIN_SHARE of the impressions
+    repeat such a triple, fewer repeat a whole history."""
+    off = lengths_to_offsets(hist_len)
+    nz = hist_len > 0
+    first = np.where(nz, hist_idx[np.minimum(off[:-1], max(len(hist_idx) - 1, 0))] if len(hist_idx) else 0, -1)
+    last = np.where(nz, hist_idx[np.maximum(off[1:] - 1, 0)] if len(hist_idx) else 0, -1)
+    key = (hist_len.astype(np.int64) << 42) ^ (first.astype(np.int64) + 1 << 21) ^ (last.astype(np.int64) + 1)
+    return 1.0 - len(np.unique(key)) / len(hist_len) >= DEDUPE_MIN_SHARE
+
+
 class PoolScoreEngine:
     def __init__(self, model: torch.nn.Module, dtype: torch.dtype = torch.float32,
                  device: Optional[torch.device] = None):
@@ -72,7 +84,7 @@ class PoolScoreEngine:
         self.n_imp = len(cand_len)
         self.user_idx = None
         self.shared_history_share = 0.0
-        if dedupe is not False and self.n_imp:
+        if dedupe is not False and self.n_imp and (dedupe or _may_repeat(hist_idx, hist_len)):
             group, first = distinct_segments(hist_idx, hist_len)
             self.shared_history_share = 1.0 - len(first) / self.n_imp
             if dedupe or self.shared_history_share >= DEDUPE_MIN_SHARE:
