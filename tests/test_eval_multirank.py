@@ -1,4 +1,4 @@
-"""scripts/eval.py over 2 ranks (BASELINE config 4 path: impressions partitioned
+"""scripts/eval.py over 2 and 4 ranks (BASELINE config 4 path: impressions partitioned
 by cost, news-table transform sharded and all-gathered, scores gathered back)
 gives exactly the single-rank metrics.  The ranks run with the gloo backend and
 share the test box's one GPU (RCCL needs one GPU per rank; the 8-GPU RCCL run is
@@ -29,15 +29,15 @@ def _last_record(d: Path) -> dict:
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pooler", ["final", "latent"])
-def test_eval_two_ranks_matches_one(tmp_path, pooler):
+@pytest.mark.parametrize("pooler,ranks", [("final", 2), ("latent", 2), ("latent", 4)])
+def test_eval_two_ranks_matches_one(tmp_path, pooler, ranks):
     env = dict(os.environ, NR_DIST_BACKEND="gloo", PYTHONPATH=str(REPO), OMP_NUM_THREADS="4")
     args = ["scripts/eval.py", "--synthetic", "--num-impressions", "700", "--splits", "MINDsmall_dev",
             "--pooler", pooler]
     one = subprocess.run([sys.executable, *args, "--log-dir", str(tmp_path / "one")], cwd=REPO, env=env,
                          capture_output=True, text=True, timeout=240)
     assert one.returncode == 0, one.stderr[-3000:]
-    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
                           "--master-addr", "127.0.0.1", "--master-port", str(_port()), *args,
                           "--log-dir", str(tmp_path / "two")], cwd=REPO, env=env, capture_output=True, text=True,
                          timeout=240)
