@@ -180,8 +180,13 @@ def score_device(ranks, labels, offsets) -> dict:
     ties = np.nonzero(tie.cpu().numpy())[0]
     if len(ties):
         rh, yh, oh = r.cpu().numpy(), y.cpu().numpy(), o.cpu().numpy()
-        for i in ties:
-            a, b = oh[i], oh[i + 1]
-            _, m[i, 1], m[i, 2], m[i, 3] = _row_metrics(yh[a:b], rh[a:b])
+        with np.errstate(invalid="ignore", divide="ignore"):
+            for i in ties:  # the reference's numpy calls (evaluation.py:50-53), AUC stays the device's
+                a, b = oh[i], oh[i + 1]
+                y_true = np.asarray(yh[a:b], dtype="float32")
+                y_score = np.array([1.0 / v for v in rh[a:b]], dtype=np.float64)
+                m[i, 1] = mrr_score(y_true, y_score)
+                m[i, 2] = ndcg_score(y_true, y_score, 5)
+                m[i, 3] = ndcg_score(y_true, y_score, 10)
     return {"auc": np.mean(m[:, 0]).item(), "mrr": np.mean(m[:, 1]).item(), "ndcg5": np.mean(m[:, 2]).item(),
             "ndcg10": np.mean(m[:, 3]).item(), "num_samples": int(len(m))}
