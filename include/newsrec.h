@@ -121,6 +121,19 @@ int nr_gemm_drelu(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K, 
                   void* stream);
 
 /*
+ * Split-K fixup: C[r][c] = epi(sum_{s < parts} P[s][r][c] + bias[c]) over `rows` x N
+ * (P: f32 [parts][rows][N], the K-slice partials of nr_gemm_grouped).  For the
+ * last, partial round of 256x256 tiles of a GEMM (config-5 training at M % 4096
+ * small): those rows run as `parts` K-slices side by side instead of one tile
+ * per CU.  epilogue NR_EPI_NONE, NR_EPI_RELU_DROPOUT (mask of row row0 + r, p as
+ * nr_gemm_relu_dropout, `scale` ignored) or NR_EPI_DRELU (R = forward output,
+ * C = R > 0 ? v * scale : 0).  bias nullable.
+ */
+int nr_splitk_fixup(int dtype_out, int epilogue, int64_t rows, int64_t N, int parts, const float* partials,
+                    const float* bias, const void* R, int64_t ldr, void* C, int64_t ldc, int64_t row0,
+                    uint64_t seed, float p, float scale, void* stream);
+
+/*
  * n independent C_i[M_i, N_i] = A_i · W_iᵀ (no bias, no epilogue) in ONE launch
  * over the union of the problems' 256x256 tiles (bf16 or exact-f32 in, f32 or bf16 out).
  * For problems too small to fill the 256 CUs alone: the config-5 weight-grad

@@ -52,6 +52,7 @@ SIGNATURES = {
     "nr_row_inv_norm": (_i, [_i, _l, _l, _p, _l, _f, _p, _p]),
     "nr_pool_score": (_i, [_i, _i, _l, _p, _l, _p, _l, _p, _p, _p, _p, _p, _l, _p, _p, _p]),
     "nr_score_users": (_i, [_i, _l, _p, _p, _p, _l, _p, _p, _p, _l, _p, _p]),
+    "nr_splitk_fixup": (_i, [_i, _i, _l, _l, _i, _p, _p, _p, _l, _p, _l, _l, ctypes.c_uint64, _f, _f, _p]),
     "nr_dense_rank": (_i, [_p, _p, _l, _p, _p, _p]),
     "nr_impression_metrics": (_i, [_p, _p, _p, _l, _p, _p, _p, _p]),
     "nr_final_attn_workspace_bytes": (_l, [_i, _l]),

@@ -443,6 +443,33 @@ using namespace nr;
     else if (dto == NR_F32) { typedef __bf16 TI; typedef float TO; __VA_ARGS__; }           \
     else { typedef __bf16 TI; typedef __bf16 TO; __VA_ARGS__; }                            \
   } while (0)
+// ----------------------------------------------------------------- split-K fixup
+// C[r][c] = epi(sum_s P[s][r][c] + bias[c]) for the rows of a GEMM that were
+// computed as `parts` K-slices (nr_gemm_grouped, f32 partials), with the
+// epilogues of the training GEMMs: ReLU + dropout (same counter-hash mask as
+// the GEMM kernels: drop_hash(seed, (row0 + r) * N + c)) and the relu/dropout
+// backward (R > 0 ? v * scale : 0).  4 columns per thread.
+template <int EPI, typename TO>
+__global__ __launch_bounds__(256) void splitk_fixup_kernel(int64_t rows, int64_t N, int parts, const float* __restrict__ P,
+                                                           const float* __restrict__ bias, const TO* __restrict__ R,
+                                                           int64_t ldr, TO* __restrict__ C, int64_t ldc, int64_t row0,
+                                                           uint64_t seed, uint32_t thr, float scale) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // quad index
+  const int64_t nq = N / 4;
+  if (q >= rows * nq) return;
+  const int64_t r = q / nq, c = (q % nq) * 4;
+  f32x4 v = *reinterpret_cast<const f32x4*>(P + r * N + c);
+  for (int s = 1; s < parts; ++s) v += *reinterpret_cast<const f32x4*>(P + ((int64_t)s * rows + r) * N + c);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float x = v[k] + (bias ? bias[c + k] : 0.f);
+    if constexpr (EPI == NR_EPI_RELU_DROPOUT)
+      x = drop_hash(seed, (uint64_t)((row0 + r) * N + c + k)) < thr ? 0.f : fmaxf(x, 0.f) * scale;
+    if constexpr (EPI == NR_EPI_DRELU) x = ldf(R + r * ldr + c + k) > 0.f ? x * scale : 0.f;
+    stf(C + r * ldc + c + k, x);
+  }
+}
+
 #define NR_DT1(dt, ...)                                       \
   do {                                                        \
     if (dt == NR_F32) { typedef float T; __VA_ARGS__; }       \
@@ -608,5 +635,36 @@ extern "C" int nr_adamw(int64_t n, float* p, const float* g, float* m, float* v,
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v,
                      (__bf16*)p_bf16, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, max_norm, sumsq);
   NR_CHECK_LAUNCH("nr_adamw");
+  return NR_OK;
+}
+
+extern "C" int nr_splitk_fixup(int dtype_out, int epilogue, int64_t rows, int64_t N, int parts, const float* partials,
+                               const float* bias, const void* R, int64_t ldr, void* C, int64_t ldc, int64_t row0,
+                               uint64_t seed, float p, float scale, void* stream) {
+  clear_error();
+  NR_CHECK_ARG(NR_OKDT(dtype_out) && rows >= 0 && N > 0 && N % 4 == 0 && parts >= 1 && ldc >= N && row0 >= 0,
+               "nr_splitk_fixup: bad args");
+  NR_CHECK_ARG(epilogue == NR_EPI_NONE || epilogue == NR_EPI_RELU_DROPOUT || epilogue == NR_EPI_DRELU,
+               "nr_splitk_fixup: epilogue %d unsupported", epilogue);
+  NR_CHECK_ARG(p >= 0.f && p < 1.f, "nr_splitk_fixup: dropout p outside [0, 1)");
+  if (rows == 0) return NR_OK;
+  NR_CHECK_ARG(partials && C && (epilogue != NR_EPI_DRELU || (R && ldr >= N)), "nr_splitk_fixup: null pointer");
+  NR_CHECK_ARG(((uintptr_t)partials & 15) == 0, "nr_splitk_fixup: partials must be 16-byte aligned");
+  // dropout threshold and scale exactly as nr_gemm_relu_dropout forms them
+  const double t = (double)p * 4294967296.0;
+  const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  if (epilogue == NR_EPI_RELU_DROPOUT) scale = 1.0f / (1.0f - p);
+  const int64_t quads = rows * (N / 4);
+  NR_CHECK_ARG((quads + 255) / 256 <= 0x7fffffff, "nr_splitk_fixup: too many rows");
+  const dim3 grid((unsigned)((quads + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+#define NR_FIX(E)                                                                                                   \
+  NR_DT1(dtype_out, hipLaunchKernelGGL((splitk_fixup_kernel<E, T>), grid, dim3(256), 0, s, rows, N, parts, partials, \
+                                       bias, (const T*)R, ldr, (T*)C, ldc, row0, seed, thr, scale))
+  if (epilogue == NR_EPI_RELU_DROPOUT) NR_FIX(NR_EPI_RELU_DROPOUT);
+  else if (epilogue == NR_EPI_DRELU) NR_FIX(NR_EPI_DRELU);
+  else NR_FIX(NR_EPI_NONE);
+#undef NR_FIX
+  NR_CHECK_LAUNCH("nr_splitk_fixup");
   return NR_OK;
 }

@@ -483,6 +483,25 @@ def gemm_drelu(a: torch.Tensor, w: torch.Tensor, y: torch.Tensor, scale: float,
     return out
 
 
+def splitk_fixup(partials: torch.Tensor, out: torch.Tensor, epilogue: str = "none", bias: Optional[torch.Tensor] = None,
+                 residual: Optional[torch.Tensor] = None, row0: int = 0, seed: int = 0, p: float = 0.0,
+                 scale: float = 1.0) -> torch.Tensor:
+    """out = epi(partials.sum(0) + bias) for K-slice partials [parts, rows, N] f32
+    (nr_splitk_fixup): epilogue "none", "relu_dropout" (mask rows row0..) or
+    "drelu" (residual = the forward output)."""
+    dev = _dev(partials, out, bias, residual)
+    epi = {"none": _lib.NR_EPI_NONE, "relu_dropout": _lib.NR_EPI_RELU_DROPOUT, "drelu": _lib.NR_EPI_DRELU}[epilogue]
+    if partials.dtype != torch.float32 or not partials.is_contiguous() or partials.dim() != 3:
+        raise _lib.NewsRecHIPError("splitk_fixup: partials must be contiguous f32 [parts, rows, N]")
+    parts, rows, N = partials.shape
+    if tuple(out.shape) != (rows, N):
+        raise _lib.NewsRecHIPError("splitk_fixup: out must be [rows, N]")
+    _lib.call("nr_splitk_fixup", _dt(out, "out"), epi, rows, N, parts, _ptr(partials), _ptr(bias), _ptr(residual),
+              _rowmajor(residual, "residual") if residual is not None else 0, _ptr(out), _rowmajor(out, "out"), row0,
+              ctypes.c_uint64(seed & (2**64 - 1)), ctypes.c_float(p), ctypes.c_float(scale), _stream(dev))
+    return out
+
+
 def gather_rows(src: torch.Tensor, idx: Optional[torch.Tensor], n: Optional[int] = None,
                 out_dtype: Optional[torch.dtype] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     dev = _dev(src, idx, out)

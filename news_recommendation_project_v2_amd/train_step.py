@@ -86,6 +86,8 @@ class FinalAttentionTrainStep:
             raise NewsRecHIPError("training supports NUM_HIDDEN_LAYERS == 1 (config.py:35)")
         self.device = device or torch.device("cuda")
         self.dtype = dtype
+        # CUs the persistent GEMMs spread one 256x256 tile round over (multiple of the 8 XCDs)
+        self._ncu = torch.cuda.get_device_properties(self.device).multi_processor_count // 8 * 8
         self.lr, self.betas, self.eps, self.wd, self.max_norm = lr, betas, eps, weight_decay, max_norm
         self.p = dropout
         self.seed = seed
@@ -140,6 +142,44 @@ class FinalAttentionTrainStep:
             self._ws[name] = t
         return t[:n].view(shape)
 
+    def _tail_rows(self, M: int, N: int, K: int) -> int:
+        """Rows of a bf16 GEMM that fill whole rounds of 256x256 tiles over the CUs
+        (the rest, a few tiles that would hold one CU each for a full tile time,
+        run as K-slices instead); M when no such split pays."""
+        if self.dtype != torch.bfloat16 or N % 256 or K % 512 or M % 256 == 0:
+            return M
+        ncu = self._ncu
+        ntn = N // 256
+        if ncu % ntn:
+            return M
+        m_main = M // (256 * (ncu // ntn)) * (256 * (ncu // ntn))
+        tail_tiles = -(-(M - m_main) // 256) * ntn
+        return m_main if m_main > 0 and tail_tiles * 4 <= ncu else M
+
+    def _relu_gemm(self, a: torch.Tensor, w: torch.Tensor, out: torch.Tensor, *, bias=None, seed: int = 0,
+                   y: Optional[torch.Tensor] = None, scale: float = 1.0) -> torch.Tensor:
+        """gemm_relu_dropout (y None) or gemm_drelu (y = forward output).  When the
+        last round of 256x256 tiles would be a few tiles (M just past a multiple
+        of 16 M-tiles at N = 4096: M = 8,320 -> 512 + 16 tiles, the 16 costing a
+        whole tile time), those rows run as 8 K-slices in one grouped launch plus
+        nr_splitk_fixup (sum + bias + the same epilogue / dropout mask)."""
+        M, K = a.shape
+        N = w.shape[0]
+        mm = self._tail_rows(M, N, K)
+        if mm > 0:
+            if y is None:
+                ops.gemm_relu_dropout(a[:mm], w, bias, seed, self.p, out=out[:mm])
+            else:
+                ops.gemm_drelu(a[:mm], w, y[:mm], scale, out=out[:mm])
+        if mm == M:
+            return out
+        parts, kk = 8, K // 8
+        P = self._buf("splitk_P", (parts, M - mm, N), torch.float32)
+        ops.gemm_grouped([(a[mm:, i * kk:(i + 1) * kk], w[:, i * kk:(i + 1) * kk], P[i]) for i in range(parts)])
+        ops.splitk_fixup(P, out[mm:], "relu_dropout" if y is None else "drelu", bias=bias,
+                         residual=None if y is None else y[mm:], row0=mm, seed=seed, p=self.p, scale=scale)
+        return out
+
     def W(self, i: int) -> torch.Tensor:
         return self.cviews[f"linear{i}.weight"]
 
@@ -170,13 +210,12 @@ class FinalAttentionTrainStep:
         idx.fill_(-1)
         idx[:Hs].copy_(batch.hist_idx)
         S = ops.gather_rows(E, idx, out_dtype=dt, out=self._buf("S", (Hp, D), dt))
-        X1 = ops.gemm_relu_dropout(S, self.W(1), self.b(1), self.layer_seed(1), self.p, out=self._buf("X1", (Hp, H), dt))
-        X2 = ops.gemm_relu_dropout(X1, self.W(2), self.b(2), self.layer_seed(2), self.p,
-                                   out=self._buf("X2", (Hp, H), dt))
+        X1 = self._relu_gemm(S, self.W(1), self._buf("X1", (Hp, H), dt), bias=self.b(1), seed=self.layer_seed(1))
+        X2 = self._relu_gemm(X1, self.W(2), self._buf("X2", (Hp, H), dt), bias=self.b(2), seed=self.layer_seed(2))
         XP = self._buf("XP", (Hp, 2 * D), dt)
         X = XP[:, :D]
         ops.gemm(X2, self.W(3), self.b(3), out=X)
-        Y = ops.gemm_relu_dropout(X, self.W(4), self.b(4), self.layer_seed(3), self.p, out=self._buf("Y", (Hp, H), dt))
+        Y = self._relu_gemm(X, self.W(4), self._buf("Y", (Hp, H), dt), bias=self.b(4), seed=self.layer_seed(3))
         ops.gemm(Y, self.W(5), None, epilogue="exp", out=XP[:, D:])
         users, z = ops.final_pool_fwd(XP, batch.hist_off)
         # ---- loss + backward
@@ -190,7 +229,7 @@ class FinalAttentionTrainStep:
         T = lambda src, name: ops.transpose(src, out=self._buf(name, (src.shape[1], src.shape[0]), dt))
         # linear5 (no bias): logits = Y W5ᵀ
         W5t = T(self.W(5), "W5t")
-        dY = ops.gemm_drelu(dL, W5t, Y, scale, out=self._buf("dY", (Hp, H), dt))     # = dZ4
+        dY = self._relu_gemm(dL, W5t, self._buf("dY", (Hp, H), dt), y=Y, scale=scale)     # = dZ4
         self._wgrad(dL, Y, "linear5.weight")
         # linear4: Y = dropout(relu(X W4ᵀ + b4))
         W4t = T(self.W(4), "W4t")
@@ -199,12 +238,12 @@ class FinalAttentionTrainStep:
         ops.col_sum(dY, self.gviews["linear4.bias"])
         # linear3: X = X2 W3ᵀ + b3
         W3t = T(self.W(3), "W3t")
-        dZ2 = ops.gemm_drelu(dX, W3t, X2, scale, out=self._buf("dZ2", (Hp, H), dt))
+        dZ2 = self._relu_gemm(dX, W3t, self._buf("dZ2", (Hp, H), dt), y=X2, scale=scale)
         self._wgrad(dX, X2, "linear3.weight")
         ops.col_sum(dX, self.gviews["linear3.bias"])
         # linear2
         W2t = T(self.W(2), "W2t")
-        dZ1 = ops.gemm_drelu(dZ2, W2t, X1, scale, out=self._buf("dZ1", (Hp, H), dt))
+        dZ1 = self._relu_gemm(dZ2, W2t, self._buf("dZ1", (Hp, H), dt), y=X1, scale=scale)
         self._wgrad(dZ2, X1, "linear2.weight")
         ops.col_sum(dZ2, self.gviews["linear2.bias"])
         # linear1
