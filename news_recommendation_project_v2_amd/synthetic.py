@@ -110,16 +110,16 @@ def mind_shaped(name: str = "mind_large_dev", seed: int = 1234, **kw) -> Impress
 
 
 def to_behaviors(imps: Impressions, with_labels: bool = True, news_prefix: str = "N"):
-    """Render as MIND behaviours strings (History, Impressions) for parser tests."""
+    """Render as MIND behaviours strings (History, Impressions) for parser tests
+    (token strings built once per news id, then joined per row)."""
     ho, co = imps.hist_off(), imps.cand_off()
-    hist, impr = [], []
-    for i in range(imps.n_imp):
-        h = imps.hist_idx[ho[i]:ho[i + 1]]
-        hist.append(" ".join(f"{news_prefix}{x}" for x in h) if len(h) else None)
-        c = imps.cand_idx[co[i]:co[i + 1]]
-        lab = imps.labels[co[i]:co[i + 1]]
-        if with_labels:
-            impr.append(" ".join(f"{news_prefix}{x}-{int(y)}" for x, y in zip(c, lab)))
-        else:
-            impr.append(" ".join(f"{news_prefix}{x}" for x in c))
+    names = np.array([f"{news_prefix}{i}" for i in range(imps.n_news)], dtype=object)
+    hist_tok = names[imps.hist_idx]
+    if with_labels:
+        lab = [np.array([f"{news_prefix}{i}-{y}" for i in range(imps.n_news)], dtype=object) for y in (0, 1)]
+        cand_tok = np.where(imps.labels.astype(bool), lab[1][imps.cand_idx], lab[0][imps.cand_idx])
+    else:
+        cand_tok = names[imps.cand_idx]
+    hist = [" ".join(hist_tok[ho[i]:ho[i + 1]]) if ho[i + 1] > ho[i] else None for i in range(imps.n_imp)]
+    impr = [" ".join(cand_tok[co[i]:co[i + 1]]) for i in range(imps.n_imp)]
     return hist, impr
