@@ -101,8 +101,13 @@ class ShardedTable:
 
     def _overlapped(self) -> None:
         """Transform chunk c, then all-gather it asynchronously (byte views: any
-        dtype, any backend) while chunk c + 1 is transformed."""
+        dtype, any backend) while chunk c + 1 is transformed.  One chunk: the
+        in-place all_gather_into_tensor (no staging buffer, no copies)."""
         from . import ops
+        if self.chunks == 1:
+            self.eng.transform(rows=slice(self.lo, self.lo + self.rows), out=self.local, src=self.src)
+            dist.all_gather_into_tensor(self.full.view(torch.uint8), self.local.view(torch.uint8), group=self.group)
+            return
         reserve = self.full.is_cuda and self.chunks > 1
         if reserve:
             ncu = torch.cuda.get_device_properties(self.full.device).multi_processor_count

@@ -528,8 +528,8 @@ def test_train_v3_and_save_emb_scripts_synthetic(gpu_device, tmp_path, monkeypat
     assert torch.allclose(t.norm(dim=1), torch.ones(t.shape[0]), atol=1e-4)
 
 
-@pytest.mark.parametrize("pooler", ["final", "latent"])
-def test_sharded_table_overlapped_rccl_single_rank(gpu_device, pooler, tmp_path):
+@pytest.mark.parametrize("pooler,chunks", [("final", 3), ("latent", 3), ("latent", 1)])
+def test_sharded_table_overlapped_rccl_single_rank(gpu_device, pooler, chunks, tmp_path):
     """The overlapped transform / all-gather path RCCL ranks take (chunks
     transformed with the persistent GEMMs on all but RCCL_CUS CUs, each chunk
     all-gathered asynchronously on the communicator's stream), run on a real
@@ -544,7 +544,7 @@ def test_sharded_table_overlapped_rccl_single_rank(gpu_device, pooler, tmp_path)
         table = W.news_table(7, 20011, 1024, name="overlap")
         eng = PoolScoreEngine(_model(pooler, gpu_device, 7), dtype=torch.bfloat16, device=gpu_device).load_news(table)
         want = eng.transform().clone()
-        st = ShardedTable(eng, 0, 1, chunks=3)
+        st = ShardedTable(eng, 0, 1, chunks=chunks)
         st._overlapped()
         torch.cuda.synchronize()
         assert torch.equal(st.full[:20011], want)
