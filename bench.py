@@ -366,6 +366,9 @@ def cpu_leg(args, dev) -> tuple:
                 d["max_abs_score_diff"] = float(np.abs(s.cpu().numpy() - cpu_scores).max())
                 d["auc_abs_diff"] = abs(g["auc"] - cpu_m["auc"])
                 d["auc_equal_4dp"] = round(g["auc"], 4) == round(cpu_m["auc"], 4)
+                if dt == "bf16":  # against the CPU reference fed the same bf16-rounded table
+                    d["auc_abs_diff_vs_bf16_table_ref"] = abs(g["auc"] - m16["auc"])
+                    d["max_abs_score_diff_vs_bf16_table_ref"] = float(np.abs(s.cpu().numpy() - s16).max())
                 parity[pooler][f"gpu_{dt}"] = d
                 del eng
     head = out[args.pooler][f"first_{args.cpu_impressions}"]
