@@ -32,6 +32,9 @@ SHAPES = [  # (name, N, K, epilogue)
     ("latent.B 512->1024 resadd", 1024, 512, "resadd"),
     ("latent.ff1 1024->8192 geglu", 8192, 1024, "geglu"),
     ("latent.ff2 4096->1024 resadd", 1024, 4096, "resadd"),
+    # epilogue-cost probes: the ff1 shape without GEGLU, and with a plain GELU
+    ("probe.ff1shape 1024->8192 none", 8192, 1024, "none"),
+    ("probe.ff1shape 1024->8192 gelu", 8192, 1024, "gelu"),
 ]
 
 
