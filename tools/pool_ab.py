@@ -20,7 +20,6 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
 from news_recommendation_project_v2_amd import synthetic  # noqa: E402
-from news_recommendation_project_v2_amd import weights as W  # noqa: E402
 from news_recommendation_project_v2_amd.engine import PoolScoreEngine  # noqa: E402
 
 POOL = {"final": 0, "latent": 1}
