@@ -90,6 +90,11 @@ VARIANTS = {
         ("    readB(st, 1, fb1);\n    if (pa) dmaA(1, ns, ka);", "    if (pa) dmaA(1, ns, ka);"),
         ("    readA(st, 1);\n    if (pb) {", "    if (pb) {"),
     ],
+    # tile order: M-tiles per group of the persistent schedule (tile_of), 4 shipped
+    "gm1": [("constexpr int kGemmGroupM = 4;", "constexpr int kGemmGroupM = 1;")],
+    "gm2": [("constexpr int kGemmGroupM = 4;", "constexpr int kGemmGroupM = 2;")],
+    "gm8": [("constexpr int kGemmGroupM = 4;", "constexpr int kGemmGroupM = 8;")],
+    "gm16": [("constexpr int kGemmGroupM = 4;", "constexpr int kGemmGroupM = 16;")],
     # no s_setprio around the MFMA phases
     "noprio": [
         ("  __builtin_amdgcn_s_setprio(1);                       \\\n  mma(QM, NI, FB);                                     \\\n"
