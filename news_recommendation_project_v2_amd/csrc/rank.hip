@@ -15,6 +15,64 @@ namespace nr {
 
 constexpr int RANK_MAXC = 2048;
 
+// Impressions of up to RANK_REG_BLOCKS x 64 candidates (every MIND impression:
+// at most ~300): the values stay in registers, lane l owning candidates
+// 64 b + l, and every other value is broadcast with v_readlane (no LDS, so
+// the kernel runs at full occupancy).  Larger ones are left to the LDS kernel.
+constexpr int RANK_REG_BLOCKS = 5;
+
+__global__ __launch_bounds__(256) void dense_rank_reg_kernel(const float* __restrict__ scores,
+                                                             const int64_t* __restrict__ coff, int64_t n_imp,
+                                                             int32_t* __restrict__ ranks) {
+  constexpr int RB = RANK_REG_BLOCKS;
+  const int lane = threadIdx.x & 63;
+  const int64_t imp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (imp >= n_imp) return;  // wave-uniform
+  const int64_t c0 = coff[imp];
+  const int64_t cc = coff[imp + 1] - c0;
+  if (cc > 64 * RB || cc <= 0) return;
+  const int c = (int)cc, nb = (c + 63) / 64;
+  float v[RB];
+  int first[RB], r[RB];
+#pragma unroll
+  for (int b = 0; b < RB; ++b) {
+    v[b] = b < nb && b * 64 + lane < c ? scores[c0 + b * 64 + lane] : 0.f;
+    first[b] = 1;
+    r[b] = 1;
+  }
+  // pass 1: candidate i is the first occurrence of its value
+#pragma unroll
+  for (int bk = 0; bk < RB; ++bk) {
+    if (bk >= nb) break;
+    const int kend = min(64, c - bk * 64);
+    for (int k = 0; k < kend; ++k) {
+      const float sk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[bk]), k));
+#pragma unroll
+      for (int bi = 0; bi < RB; ++bi)
+        if (bi < nb && bk * 64 + k < bi * 64 + lane && sk == v[bi]) first[bi] = 0;
+    }
+  }
+  // pass 2: rank = 1 + distinct values strictly greater
+#pragma unroll
+  for (int bk = 0; bk < RB; ++bk) {
+    if (bk >= nb) break;
+    const int kend = min(64, c - bk * 64);
+    for (int k = 0; k < kend; ++k) {
+      if (!__builtin_amdgcn_readlane(first[bk], k)) continue;  // uniform
+      const float sk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[bk]), k));
+#pragma unroll
+      for (int bi = 0; bi < RB; ++bi) r[bi] += (bi < nb && sk > v[bi]) ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < RB; ++b)
+    if (b < nb && b * 64 + lane < c) ranks[c0 + b * 64 + lane] = r[b];
+}
+
+// The rest (RANK_REG_BLOCKS x 64 < c <= RANK_MAXC) through LDS.  A grid-stride
+// loop over groups of 4 impressions (uniform trip count per workgroup, so the
+// barriers line up): its LDS footprint holds few workgroups per CU and it
+// skips the impressions the register kernel took.
 __global__ __launch_bounds__(256) void dense_rank_kernel(const float* __restrict__ scores,
                                                          const int64_t* __restrict__ coff,
                                                          int64_t n_imp, int32_t* __restrict__ ranks,
@@ -22,7 +80,9 @@ __global__ __launch_bounds__(256) void dense_rank_kernel(const float* __restrict
   __shared__ float s_val[4][RANK_MAXC];
   __shared__ unsigned char s_first[4][RANK_MAXC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t imp = (int64_t)blockIdx.x * 4 + w;
+  const int64_t n_groups = (n_imp + 3) / 4;
+  for (int64_t g = blockIdx.x; g < n_groups; g += gridDim.x) {
+  const int64_t imp = g * 4 + w;
   int64_t c0 = 0;
   int c = 0;
   if (imp < n_imp) {
@@ -32,11 +92,12 @@ __global__ __launch_bounds__(256) void dense_rank_kernel(const float* __restrict
       if (lane == 0) atomicExch(status, NR_ERR_UNSUPPORTED);
       c = 0;
     } else {
-      c = (int)cc;
+      c = cc > 64 * RANK_REG_BLOCKS ? (int)cc : 0;  // smaller ones: dense_rank_reg_kernel
     }
   }
   float* sv = s_val[w];
   unsigned char* sf = s_first[w];
+  __syncthreads();  // the previous group's reads of this wave's slots are done
   for (int i = lane; i < c; i += 64) sv[i] = scores[c0 + i];
   __syncthreads();
   for (int i0 = 0; i0 < c; i0 += 64) {
@@ -58,6 +119,7 @@ __global__ __launch_bounds__(256) void dense_rank_kernel(const float* __restrict
     for (int k = 0; k < c; ++k) r += (sf[k] && sv[k] > si) ? 1 : 0;
     if (i < c) ranks[c0 + i] = r;
   }
+  }  // group loop
 }
 
 }  // namespace nr
@@ -68,7 +130,10 @@ extern "C" int nr_dense_rank(const float* scores, const int64_t* cand_off, int64
   NR_CHECK_ARG(n_imp >= 0, "nr_dense_rank: n_imp < 0");
   if (n_imp == 0) return NR_OK;
   NR_CHECK_ARG(scores && cand_off && ranks && status, "nr_dense_rank: null pointer");
-  hipLaunchKernelGGL(nr::dense_rank_kernel, dim3((unsigned)((n_imp + 3) / 4)), dim3(256), 0,
+  const int64_t groups = (n_imp + 3) / 4;
+  hipLaunchKernelGGL(nr::dense_rank_reg_kernel, dim3((unsigned)groups), dim3(256), 0, (hipStream_t)stream, scores,
+                     cand_off, n_imp, ranks);
+  hipLaunchKernelGGL(nr::dense_rank_kernel, dim3((unsigned)(groups < 1024 ? groups : 1024)), dim3(256), 0,
                      (hipStream_t)stream, scores, cand_off, n_imp, ranks, status);
   NR_CHECK_LAUNCH("nr_dense_rank");
   return NR_OK;

@@ -226,6 +226,24 @@ def test_dense_rank_golden_bit_exact(gpu_device):
     np.testing.assert_array_equal(ranks, g["ranks_flat"])
 
 
+def test_dense_rank_sizes_and_ties_bit_exact(gpu_device):
+    """Dense ranks vs scipy rankdata(-x, 'dense') across the register path
+    (<= 320 candidates, 1..5 blocks of 64) and the LDS path (321..2048), with
+    heavy ties (values drawn from a few levels), empty impressions, and the
+    > 2048 status."""
+    rng = np.random.default_rng(4)
+    counts = np.array([0, 1, 2, 63, 64, 65, 127, 128, 129, 300, 319, 320, 321, 500, 1000, 2048, 37, 0, 5], np.int64)
+    parts = [rng.integers(0, max(2, n // 3), n).astype(np.float32) / 7 if i % 2 else rng.random(n).astype(np.float32)
+             for i, n in enumerate(counts)]
+    scores = np.concatenate(parts)
+    off = torch.tensor(np.concatenate([[0], np.cumsum(counts)]), dtype=torch.int64, device=gpu_device)
+    ranks = ops.dense_rank(torch.tensor(scores, device=gpu_device), off).cpu().numpy()
+    want = np.concatenate([scipy.stats.rankdata(-p, method="dense") for p in parts if len(p)]).astype(np.int64)
+    np.testing.assert_array_equal(ranks, want)
+    with pytest.raises(ops._lib.NewsRecHIPError):
+        ops.dense_rank(torch.zeros(2049, device=gpu_device), torch.tensor([0, 2049], device=gpu_device))
+
+
 # ---------------------------------------------------------------- hot path vs golden
 @pytest.mark.parametrize("pooler", ["final", "latent"])
 def test_pool_score_matches_reference_golden(gpu_device, pooler):
