@@ -21,52 +21,62 @@ constexpr int RANK_MAXC = 2048;
 // the kernel runs at full occupancy).  Larger ones are left to the LDS kernel.
 constexpr int RANK_REG_BLOCKS = 5;
 
-__global__ __launch_bounds__(256) void dense_rank_reg_kernel(const float* __restrict__ scores,
-                                                             const int64_t* __restrict__ coff, int64_t n_imp,
-                                                             int32_t* __restrict__ ranks) {
-  constexpr int RB = RANK_REG_BLOCKS;
-  const int lane = threadIdx.x & 63;
-  const int64_t imp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (imp >= n_imp) return;  // wave-uniform
-  const int64_t c0 = coff[imp];
-  const int64_t cc = coff[imp + 1] - c0;
-  if (cc > 64 * RB || cc <= 0) return;
-  const int c = (int)cc, nb = (c + 63) / 64;
-  float v[RB];
-  int first[RB], r[RB];
+// NB = number of 64-candidate register blocks (compile time: no guarded work
+// for the blocks an impression does not have; most have one).
+template <int NB>
+__device__ __forceinline__ void dense_rank_reg(const float* __restrict__ sc, int c, int lane, int32_t* __restrict__ rk) {
+  float v[NB];
+  int first[NB], r[NB];
 #pragma unroll
-  for (int b = 0; b < RB; ++b) {
-    v[b] = b < nb && b * 64 + lane < c ? scores[c0 + b * 64 + lane] : 0.f;
+  for (int b = 0; b < NB; ++b) {
+    v[b] = b * 64 + lane < c ? sc[b * 64 + lane] : 0.f;
     first[b] = 1;
     r[b] = 1;
   }
   // pass 1: candidate i is the first occurrence of its value
 #pragma unroll
-  for (int bk = 0; bk < RB; ++bk) {
-    if (bk >= nb) break;
+  for (int bk = 0; bk < NB; ++bk) {
     const int kend = min(64, c - bk * 64);
     for (int k = 0; k < kend; ++k) {
       const float sk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[bk]), k));
 #pragma unroll
-      for (int bi = 0; bi < RB; ++bi)
-        if (bi < nb && bk * 64 + k < bi * 64 + lane && sk == v[bi]) first[bi] = 0;
+      for (int bi = bk; bi < NB; ++bi)
+        if (bk * 64 + k < bi * 64 + lane && sk == v[bi]) first[bi] = 0;
     }
   }
   // pass 2: rank = 1 + distinct values strictly greater
 #pragma unroll
-  for (int bk = 0; bk < RB; ++bk) {
-    if (bk >= nb) break;
+  for (int bk = 0; bk < NB; ++bk) {
     const int kend = min(64, c - bk * 64);
     for (int k = 0; k < kend; ++k) {
       if (!__builtin_amdgcn_readlane(first[bk], k)) continue;  // uniform
       const float sk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[bk]), k));
 #pragma unroll
-      for (int bi = 0; bi < RB; ++bi) r[bi] += (bi < nb && sk > v[bi]) ? 1 : 0;
+      for (int bi = 0; bi < NB; ++bi) r[bi] += sk > v[bi] ? 1 : 0;
     }
   }
 #pragma unroll
-  for (int b = 0; b < RB; ++b)
-    if (b < nb && b * 64 + lane < c) ranks[c0 + b * 64 + lane] = r[b];
+  for (int b = 0; b < NB; ++b)
+    if (b * 64 + lane < c) rk[b * 64 + lane] = r[b];
+}
+
+__global__ __launch_bounds__(256) void dense_rank_reg_kernel(const float* __restrict__ scores,
+                                                             const int64_t* __restrict__ coff, int64_t n_imp,
+                                                             int32_t* __restrict__ ranks) {
+  const int lane = threadIdx.x & 63;
+  const int64_t imp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (imp >= n_imp) return;  // wave-uniform
+  const int64_t c0 = coff[imp];
+  const int64_t cc = coff[imp + 1] - c0;
+  if (cc > 64 * RANK_REG_BLOCKS || cc <= 0) return;
+  const int c = (int)cc;
+  switch ((c + 63) / 64) {
+    case 1: dense_rank_reg<1>(scores + c0, c, lane, ranks + c0); break;
+    case 2: dense_rank_reg<2>(scores + c0, c, lane, ranks + c0); break;
+    case 3: dense_rank_reg<3>(scores + c0, c, lane, ranks + c0); break;
+    case 4: dense_rank_reg<4>(scores + c0, c, lane, ranks + c0); break;
+    default: dense_rank_reg<5>(scores + c0, c, lane, ranks + c0); break;
+  }
 }
 
 // The rest (RANK_REG_BLOCKS x 64 < c <= RANK_MAXC) through LDS.  A grid-stride
