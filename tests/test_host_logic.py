@@ -195,3 +195,35 @@ def test_eval_collate_fn_pads_and_truncates():
 
     assert eval_collate_fn(("a", "b"), tok, 7) == "batch"
     assert seen == {"texts": ["a", "b"], "max_length": 7, "padding": True, "truncation": True, "return_tensors": "pt"}
+
+
+def test_distinct_segments_exact_grouping():
+    """data_utils.distinct_segments (the engine's repeated-history grouping)
+    against a brute-force dict of the segments: identical groups numbered by
+    first occurrence, empty segments grouped together; the engine's cheap
+    (length, first, last) bound never rules out a real repeat share."""
+    from news_recommendation_project_v2_amd.data_utils import distinct_segments, lengths_to_offsets
+    from news_recommendation_project_v2_amd.engine import DEDUPE_MIN_SHARE, _may_repeat
+    from news_recommendation_project_v2_amd import synthetic
+    rng = np.random.default_rng(0)
+    for users, n in ((None, 800), (300, 900), (50, 400)):
+        im = synthetic.mind_impressions(60, n, seed=users or 1, users=users, mean_hist=4.0)
+        hl = im.hist_len.astype(np.int64).copy()
+        ho = lengths_to_offsets(hl)
+        keep = rng.random(n) < 0.05  # some empty histories
+        hl[keep] = 0
+        idx = np.concatenate([im.hist_idx[ho[i]:ho[i] + hl[i]] for i in range(n)])
+        group, first = distinct_segments(idx, hl)
+        off = lengths_to_offsets(hl)
+        seen, bg, bf = {}, [], []
+        for i in range(n):
+            key = tuple(idx[off[i]:off[i + 1]])
+            if key not in seen:
+                seen[key] = len(seen)
+                bf.append(i)
+            bg.append(seen[key])
+        np.testing.assert_array_equal(group, bg)
+        np.testing.assert_array_equal(first, bf)
+        share = 1.0 - len(first) / n
+        if share >= DEDUPE_MIN_SHARE:
+            assert _may_repeat(idx, hl)
