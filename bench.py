@@ -508,6 +508,8 @@ def main():
              "history_slots_rank0": imps.n_hist, "candidates_total": total_cand}
     if bounds is not None and world > 1:
         extra["partition"] = [int(x) for x in bounds]
+    if world > 1:  # shard transform cut in chunks whose all-gathers overlap the next chunk
+        extra["transform_chunks"] = head.tab.chunks
 
     if world > 1 and not args.no_extra and args.scaling == "strong":
         # weak scaling as an extra: every rank its own full MIND-large-dev-sized set
