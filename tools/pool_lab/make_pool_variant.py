@@ -63,6 +63,11 @@ VARIANTS = {
 #pragma unroll
       for (int q = 0; q < G; ++q) {
         const float t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b[q / 4]), 16 * (q % 4)));""")],
+    # non-temporal (streaming) loads for the gathered table rows
+    "nt": [("  for (int j = 0; j < RowFmt<T, DIM>::NL; ++j) r[j] = p[j * 64];",
+            "  for (int j = 0; j < RowFmt<T, DIM>::NL; ++j) {\n"
+            "    auto t = __builtin_nontemporal_load(reinterpret_cast<const __attribute__((ext_vector_type(4))) unsigned int*>(p + j * 64));\n"
+            "    r[j] = make_uint4(t.x, t.y, t.z, t.w);\n  }")],
     "lds4": lds_cap(40),
     "lds5": lds_cap(32),
     "lds6": lds_cap(26),
