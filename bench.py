@@ -132,13 +132,13 @@ def tx_flops(n: int, pooler: str) -> float:
 class Run:
     """One pooler/dtype on one rank: engine + its impression range + sharded table."""
 
-    def __init__(self, pooler, dtype, imps, table, dev, rank, world):
+    def __init__(self, pooler, dtype, imps, table, dev, rank, world, chunks=1):
         from news_recommendation_project_v2_amd.engine import PoolScoreEngine
         self.pooler, self.dtype = pooler, dtype
         self.model = make_model(pooler, dev)
         self.eng = PoolScoreEngine(self.model, dtype=DTYPES[dtype], device=dev).load_news(table)
         self.eng.load_impressions(imps.hist_idx, imps.hist_len, imps.cand_idx, imps.cand_len)
-        self.tab = ShardedTable(self.eng, rank, world)
+        self.tab = ShardedTable(self.eng, rank, world, chunks=chunks)
         self.scores = torch.empty(imps.n_cand, dtype=torch.float32, device=dev)
         self.imps = imps
 
@@ -150,6 +150,8 @@ class Run:
         s = torch.cuda.current_stream()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         acc = np.zeros(3)
+        split = np.zeros(2)
+        self.tab.timing = True
         for _ in range(reps):
             ev[0].record(s)
             self.tab.build()
@@ -160,6 +162,10 @@ class Run:
             ev[3].record(s)
             torch.cuda.synchronize()
             acc += [ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]), ev[2].elapsed_time(ev[3])]
+            t, g = self.tab.last_ms()
+            split += [t, g if g is not None else float("nan")]
+        self.tab.timing = False
+        self.split_ms = split / reps  # (transform, all-gather) of the table build
         return acc / reps
 
 
@@ -380,6 +386,50 @@ def cpu_leg(args, dev) -> tuple:
     return base, parity
 
 
+AUC_4DP = 5e-5  # "AUC equal to the CPU reference to 4 decimal places": |diff| < half a unit in the 4th
+
+
+def auc_gate_full(dev, poolers=("latent", "final"), dtype: str = "bf16") -> dict:
+    """The north star's AUC gate at BASELINE configs[2] size: all 376,471
+    MIND-large-dev-shaped impressions of the headline workload (same seed,
+    labels and N(0,1) table), GPU `dtype` path (device scores -> device dense
+    ranks -> device metrics) against the CPU reference in f32 (the oracle's
+    per-news restatement of get_cos_sim_scores, pinned to the reference golden;
+    per-impression AUC as score_row computes it).  CPU time is on this host's
+    cores (torch.set_num_threads as the cpu_baseline leg)."""
+    from news_recommendation_project_v2_amd import evaluation
+    from news_recommendation_project_v2_amd.engine import PoolScoreEngine
+    from oracle import data_ref, pool_ref
+    n_news, n_imp = synthetic.SHAPES["mind_large_dev"]
+    imps = synthetic.mind_impressions(n_news, n_imp, seed=1234)
+    table_d = news_table(n_news, dev)
+    table_c = table_d.cpu()
+    out = {}
+    for pooler in poolers:
+        t0 = time.perf_counter()
+        ref = pool_ref.cos_sim_scores_large(pooler, state_dict(pooler), imps.hist_idx, imps.hist_len, imps.cand_idx,
+                                            imps.cand_len, table_c)
+        auc_ref = float(np.nanmean(data_ref.impression_aucs(ref, imps.labels, imps.cand_len)))
+        t_cpu = time.perf_counter() - t0
+        eng = PoolScoreEngine(make_model(pooler, dev), dtype=DTYPES[dtype], device=dev).load_news(table_d)
+        eng.load_impressions(imps.hist_idx, imps.hist_len, imps.cand_idx, imps.cand_len)
+        s, _ = eng.step()
+        g = evaluation.score_device(eng.rank(s), imps.labels, imps.cand_off())
+        diff = abs(g["auc"] - auc_ref)
+        out[pooler] = {"cpu_ref_f32_auc": auc_ref, f"gpu_{dtype}_auc": g["auc"], "auc_abs_diff": diff,
+                       "auc_equal_4dp": bool(diff < AUC_4DP),
+                       "auc_rounded_4dp_equal": round(g["auc"], 4) == round(auc_ref, 4),
+                       "max_abs_score_diff": float(np.abs(s.cpu().numpy() - ref).max()),
+                       "cpu_ref_seconds": round(t_cpu, 1)}
+        log(f"[bench] AUC gate {pooler}: cpu f32 {auc_ref:.7f} gpu {dtype} {g['auc']:.7f} |d| {diff:.2e} "
+            f"(CPU reference {t_cpu:.1f}s)")
+        del eng, s, ref
+        torch.cuda.empty_cache()
+    return {"impressions": imps.n_imp, "candidates": imps.n_cand, "by_pooler": out,
+            "auc_equal_4dp": all(v["auc_equal_4dp"] for v in out.values()),
+            "criterion": f"|AUC_gpu - AUC_cpu_ref| < {AUC_4DP}"}
+
+
 def load_traffic(pooler: str, dtype: str):
     p = REPO / "profiles" / "pmc_pool_score.json"
     if p.is_file():
@@ -433,6 +483,8 @@ def main():
     ap.add_argument("--cpu-10k", action="store_true", help="also time the CPU reference on 10,000 impressions")
     ap.add_argument("--cpu-seconds", type=float, default=60.0, help="CPU-time cap per pooler and sample")
     ap.add_argument("--no-extra", action="store_true", help="headline config only")
+    ap.add_argument("--no-auc-gate", action="store_true",
+                    help="skip the full-size (376,471-impression) AUC parity gate vs the CPU reference")
     ap.add_argument("--dry-run", action="store_true", help="CPU-only check of the multi-rank plumbing")
     args = ap.parse_args()
 
@@ -500,18 +552,41 @@ def main():
     tx_rank = tx_flops(head.tab.rows, args.pooler)  # this rank's shard of the transform
     extra = {"stage_ms": {"transform_allgather": round(stages[0], 3), "inv_norm": round(stages[1], 4),
                           "pool_score": round(stages[2], 3)},
-             "transform_tflops": round(tx_rank / (stages[0] * 1e-3) / 1e12, 1),
-             "transform_peak_frac": round(tx_rank / (stages[0] * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS[args.dtype], 3),
+             # the transform's own interval (without the all-gather at N > 1)
+             "transform_tflops": round(tx_rank / (head.split_ms[0] * 1e-3) / 1e12, 1),
+             "transform_peak_frac": round(tx_rank / (head.split_ms[0] * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS[args.dtype],
+                                          3),
              "step_roofline_frac": round((bytes_ps / (HBM_PEAK_GBS * 1e9)
                                           + tx_rank / (MFMA_PEAK_TFLOPS[args.dtype] * 1e12)) / (ms * 1e-3), 4),
              "n_news": n_news, "impressions_rank0": imps.n_imp, "candidates_rank0": imps.n_cand,
              "history_slots_rank0": imps.n_hist, "candidates_total": total_cand}
     if bounds is not None and world > 1:
         extra["partition"] = [int(x) for x in bounds]
-    if world > 1:  # shard transform cut in chunks whose all-gathers overlap the next chunk
+    if world > 1:
+        # phase A / phase B separately: the shard's transform, then the RCCL all-gather
+        # (events on the current stream, which waits for RCCL's stream at the end of the call)
+        t_ms, g_ms = head.split_ms
+        gb_in = head.tab.gather_bytes_in
+        extra["transform_ms"] = round(float(t_ms), 3)
+        extra["allgather_ms"] = round(float(g_ms), 3)
+        extra["allgather_bytes_in_per_gpu"] = int(gb_in)
+        extra["allgather_GBs_in_per_gpu"] = round(gb_in / (g_ms * 1e-3) / 1e9, 1) if g_ms > 0 else None
         extra["transform_chunks"] = head.tab.chunks
 
     if world > 1 and not args.no_extra and args.scaling == "strong":
+        # the opt-in overlapped build (2 chunks, each chunk's all-gather beside the next
+        # chunk's transform): its step time, and its table against the default's bit for bit
+        ref_table = head.tab.full.clone()
+        r = Run(args.pooler, args.dtype, imps, table, dev, rank, world, chunks="auto")
+        if r.tab.chunks > 1:
+            d = timed(r.step, max(3, args.steps // 2), 2, world, dev, host_reduce) / max(3, args.steps // 2)
+            same = torch.tensor([int(torch.equal(r.tab.full, ref_table))], device="cpu" if host_reduce else dev)
+            dist.all_reduce(same, op=dist.ReduceOp.MIN)
+            extra["overlapped_build"] = {"chunks": r.tab.chunks, "ms_per_step": round(d * 1e3, 3),
+                                         "value": round(total_cand / d, 1),
+                                         "table_bit_identical": bool(same.item())}
+        del r, ref_table
+        torch.cuda.empty_cache()
         # weak scaling as an extra: every rank its own full MIND-large-dev-sized set
         own = synthetic.mind_impressions(n_news, n_imp, seed=1234 + rank)
         r = Run(args.pooler, args.dtype, own, table, dev, rank, world)
@@ -591,6 +666,10 @@ def main():
         log("[bench] timing the CPU reference restatement ...")
         cpu, extra["auc_vs_cpu_ref"] = cpu_leg(args, dev)
         log(f"[bench] AUC vs CPU reference: {json.dumps(extra['auc_vs_cpu_ref'])}")
+    gate = None
+    if rank == 0 and world == 1 and not args.no_auc_gate and args.cpu_seconds > 0:
+        log("[bench] full-size AUC gate (all MIND-large-dev impressions, both poolers) ...")
+        gate = auc_gate_full(dev, dtype=args.dtype)
 
     if rank == 0:
         out = {
@@ -623,6 +702,8 @@ def main():
                          "traffic": load_traffic(args.pooler, args.dtype) if world == 1 else None,
                          "algorithmic_bytes_per_launch": bytes_ps, "avg_launch_ms": round(stages[2], 4)},
             "cpu_baseline": cpu,
+            # the north star's AUC clause on the headline workload itself (configs[2] size)
+            "auc_parity": gate,
             "extra": extra,
         }
         print(json.dumps(out), flush=True)

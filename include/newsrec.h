@@ -67,6 +67,12 @@ extern "C" {
 /* Library version (major*100 + minor). */
 int nr_version(void);
 
+/* Hash of the sources the library was built from (16 hex digits: sha256 of
+ * csrc/{capi,gemm,pool_score,rowops,rank,encoder,train,metrics}.hip,
+ * csrc/nr_common.h and this header, concatenated in that order); the Python
+ * loader refuses a library whose hash differs from the tree it sits in. */
+const char* nr_build_hash(void);
+
 /* Select the HIP device for subsequent calls on this host thread and load the
  * code object once per device.  Replaces the implicit `.to(DEVICE)` of
  * config.py:19 for the library's own state. */
@@ -79,6 +85,10 @@ int nr_init(int device);
  * (the kernel maps blockIdx % 8 to an XCD).  Process-wide, not thread-safe
  * against concurrent launches. */
 int nr_set_persistent_workgroups(int n);
+
+/* The current budget (0 = the default, one workgroup per CU), so a caller can
+ * restore what it found. */
+int nr_persistent_workgroups(void);
 
 /* Thread-local message of the last failed call ("" if none). */
 const char* nr_last_error(void);

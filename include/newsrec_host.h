@@ -28,6 +28,10 @@ extern "C" {
 
 typedef struct nrh_split nrh_split;
 
+/* Hash of the sources the library was built from (16 hex digits: sha256 of
+ * csrc/host/behaviors.cpp + this header); native.py refuses a stale library. */
+const char* nrh_build_hash(void);
+
 /*
  * Parse n_rows behaviours rows.  imps / hist are the concatenated ASCII bytes
  * of the Impressions / History columns with row offsets imp_off / hist_off

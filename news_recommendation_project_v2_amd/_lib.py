@@ -8,10 +8,43 @@ PyTorch fallback: if the library is missing or a call fails, a
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 from pathlib import Path
+from typing import Optional, Sequence
 
 LIB_PATH = Path(__file__).resolve().with_name("libnewsrec_hip.so")
+CSRC = Path(__file__).resolve().with_name("csrc")
+INCLUDE = Path(__file__).resolve().parent.parent / "include"
+# translation units of libnewsrec_hip.so, in link order (also the hash order)
+HIP_SOURCES = ("capi.hip", "gemm.hip", "pool_score.hip", "rowops.hip", "rank.hip", "encoder.hip", "train.hip",
+               "metrics.hip")
+
+
+def hip_source_files() -> list:
+    return [CSRC / s for s in HIP_SOURCES] + [CSRC / "nr_common.h", INCLUDE / "newsrec.h"]
+
+
+def source_hash(files: Sequence[Path]) -> Optional[str]:
+    """First 16 hex digits of sha256 over the files' bytes, concatenated in
+    order (the Makefile computes the same with `cat ... | sha256sum`); None
+    when a source is absent (a library shipped without its sources)."""
+    h = hashlib.sha256()
+    for f in files:
+        if not Path(f).is_file():
+            return None
+        h.update(Path(f).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def embedded_hash(lib_path: Path, tag: bytes = b"nr-build-hash:") -> Optional[str]:
+    """The build hash a library carries (read from its bytes, without loading it)."""
+    try:
+        data = Path(lib_path).read_bytes()
+    except OSError:
+        return None
+    i = data.find(tag)
+    return data[i + len(tag):i + len(tag) + 16].decode("ascii", "replace") if i >= 0 else None
 
 NR_OK = 0
 NR_F32 = 0
@@ -39,9 +72,11 @@ _f = ctypes.c_float
 # name -> (restype, argtypes); must match include/newsrec.h
 SIGNATURES = {
     "nr_version": (_i, []),
+    "nr_build_hash": (ctypes.c_char_p, []),
     "nr_init": (_i, [_i]),
     "nr_last_error": (ctypes.c_char_p, []),
     "nr_set_persistent_workgroups": (_i, [_i]),
+    "nr_persistent_workgroups": (_i, []),
     "nr_gemm": (_i, [_i, _i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p]),
     "nr_gemm_relu_dropout": (_i, [_i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, ctypes.c_uint64, _f, _p]),
     "nr_gemm_drelu": (_i, [_i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _l, _p, _l, _f, _p]),
@@ -106,6 +141,12 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    want = source_hash(hip_source_files())
+    got = lib.nr_build_hash().decode("ascii", "replace")
+    if want is not None and got != want:
+        raise NewsRecHIPError(
+            f"{LIB_PATH} was built from other sources (build hash {got}, tree {want}): rebuild it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'`")
     _LIB = lib
     return lib
 

@@ -17,6 +17,65 @@ void set_error(const char* fmt, ...) {
 }
 void clear_error() { g_err[0] = 0; }
 
+// ---------------------------------------------------------------- residency
+// Every pointer a public entry hands to a kernel must be device (or managed)
+// memory: a host pointer reaching an async launch faults the GPU instead of
+// failing the call.  hipPointerGetAttributes costs ~µs, so
+// verified allocations are remembered as [base, base + size) ranges in a small
+// per-thread table (torch's caching allocator hands out sub-ranges of a few
+// large segments, so the table hits on almost every call).
+namespace {
+struct Range {
+  uintptr_t lo, hi;
+};
+constexpr int kRanges = 64;
+thread_local Range t_ranges[kRanges];
+thread_local int t_next = 0;
+}  // namespace
+
+bool device_accessible(const void* p) {
+  const uintptr_t a = (uintptr_t)p;
+  for (int i = 0; i < kRanges; ++i)
+    if (a >= t_ranges[i].lo && a < t_ranges[i].hi) return true;
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();  // unregistered host memory: do not leave the error for torch's launch checks
+    return false;
+  }
+  if (at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeManaged) return false;
+  void* base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, (void*)p) == hipSuccess && size) {
+    t_ranges[t_next] = Range{(uintptr_t)base, (uintptr_t)base + size};
+    t_next = (t_next + 1) % kRanges;
+  } else {
+    (void)hipGetLastError();
+  }
+  return true;
+}
+
+int check_device_ptrs(const char* fn, const char* names, std::initializer_list<const void*> ptrs) {
+  int i = 0;
+  for (const void* p : ptrs) {
+    if (p && !device_accessible(p)) {
+      // the i-th name of the stringified argument list
+      const char* s = names;
+      for (int k = 0; k < i && s; ++k) {
+        s = strchr(s, ',');
+        if (s) ++s;
+      }
+      while (s && *s == ' ') ++s;
+      const char* e = s ? strchr(s, ',') : nullptr;
+      const int len = s ? (e ? (int)(e - s) : (int)strlen(s)) : 1;
+      set_error("%s: `%.*s` (%p) is not device memory (host pointer? pass tensors on the GPU)", fn, len,
+                s ? s : "?", p);
+      return NR_ERR_INVALID;
+    }
+    ++i;
+  }
+  return NR_OK;
+}
+
 static int esize(int dtype) { return dtype == NR_F32 ? 4 : 2; }
 
 // Rows per chunk of the transforms: one chunk covers every MIND split's news
@@ -27,6 +86,17 @@ constexpr int64_t kChunk = 262144;
 }  // namespace nr
 
 extern "C" int nr_version(void) { return 100; }
+
+// Hash of the sources this library was compiled from (_lib.source_hash over
+// csrc/*.hip + nr_common.h + include/newsrec.h, passed by the build as
+// -DNR_BUILD_HASH).  The tag is kept in the binary so the build can read it
+// without loading the library; _lib.load() refuses a mismatching library.
+#ifndef NR_BUILD_HASH
+#define NR_BUILD_HASH "unknown"
+#endif
+static const char kBuildTag[] __attribute__((used)) = "nr-build-hash:" NR_BUILD_HASH;
+
+extern "C" const char* nr_build_hash(void) { return kBuildTag + 14; }
 
 extern "C" const char* nr_last_error(void) { return nr::g_err; }
 
@@ -60,6 +130,7 @@ extern "C" int nr_final_attn_transform(int dtype, int64_t n, const void* emb, in
   if (n == 0) return NR_OK;
   NR_CHECK_ARG(emb && W1 && b1 && W2 && b2 && W3 && b3 && W4 && b4 && W5 && table && ws,
                "nr_final_attn_transform: null pointer");
+  NR_CHECK_DEVICE("nr_final_attn_transform", emb, W1, b1, W2, b2, W3, b3, W4, b4, W5, table, ws);
   NR_CHECK_ARG(ws_bytes >= nr_final_attn_workspace_bytes(dtype, n),
                "nr_final_attn_transform: workspace too small (%lld < %lld)", (long long)ws_bytes,
                (long long)nr_final_attn_workspace_bytes(dtype, n));
@@ -106,6 +177,7 @@ extern "C" int nr_latent_transform(int dtype, int64_t n, const void* emb, int64_
   if (n == 0) return NR_OK;
   NR_CHECK_ARG(emb && A && Bt && W1i && b1i && W2 && b2 && table && ws,
                "nr_latent_transform: null pointer");
+  NR_CHECK_DEVICE("nr_latent_transform", emb, lnq_g, lnq_b, A, Bt, lnf_g, lnf_b, W1i, b1i, W2, b2, table, ws);
   NR_CHECK_ARG(ws_bytes >= nr_latent_workspace_bytes(dtype, n),
                "nr_latent_transform: workspace too small");
   const int es = nr::esize(dtype);
@@ -149,6 +221,7 @@ extern "C" int nr_latent_transform_lnfold(int dtype, int64_t n, const void* emb,
   if (n == 0) return NR_OK;
   NR_CHECK_ARG(emb && Aq && ucq && Bt && W1f && ucf && W2 && b2 && table && ws,
                "nr_latent_transform_lnfold: null pointer");
+  NR_CHECK_DEVICE("nr_latent_transform_lnfold", emb, Aq, ucq, Bt, W1f, ucf, W2, b2, table, ws);
   NR_CHECK_ARG(ws_bytes >= nr_latent_workspace_bytes(dtype, n), "nr_latent_transform_lnfold: workspace too small");
   NR_CHECK_ARG(((uintptr_t)ws & 15) == 0, "nr_latent_transform_lnfold: workspace must be 16-byte aligned");
   const int es = 2;

@@ -430,7 +430,11 @@ extern "C" int nr_encoder_forward(int dtype, int n_layers, const nr_encoder_laye
     const nr_encoder_layer& L = layers[l];
     NR_CHECK_ARG(L.wqkv && L.bqkv && L.wo && L.bo && L.ln1_g && L.ln1_b && L.w1 && L.b1 && L.w2 && L.b2 &&
                      L.ln2_g && L.ln2_b, "nr_encoder_forward: layer %d has a null pointer", l);
+    NR_CHECK_DEVICE("nr_encoder_forward(layer)", L.wqkv, L.bqkv, L.wo, L.bo, L.ln1_g, L.ln1_b, L.w1, L.b1, L.w2,
+                    L.b2, L.ln2_g, L.ln2_b);
   }
+  NR_CHECK_DEVICE("nr_encoder_forward", word_emb, pos_emb, type_emb, emb_ln_g, emb_ln_b, seq_lens, ids, pooled,
+                  hidden, status, ws);
   const nr::EncWs w = nr::enc_ws(dtype, n_tokens, n_seq, hidden == nullptr);
   NR_CHECK_ARG(ws_bytes >= w.total, "nr_encoder_forward: workspace too small (%lld < %lld)", (long long)ws_bytes,
                (long long)w.total);
@@ -486,6 +490,7 @@ extern "C" int nr_embed_ln(int dtype, int64_t n_tokens, const int32_t* ids, cons
   NR_CHECK_ARG(dtype == NR_F32 || dtype == NR_BF16, "nr_embed_ln: bad dtype");
   if (n_tokens <= 0) return NR_OK;
   NR_CHECK_ARG(ids && pos && word && pos_emb && type_emb && gamma && beta && out, "nr_embed_ln: null pointer");
+  NR_CHECK_DEVICE("nr_embed_ln", ids, pos, word, pos_emb, type_emb, gamma, beta, out);
   const dim3 grid((unsigned)((n_tokens + 3) / 4));
   hipStream_t s = (hipStream_t)stream;
   if (dtype == NR_F32)
@@ -504,6 +509,7 @@ extern "C" int nr_attention_varlen(int dtype, int32_t n_seq, int64_t n_qblocks, 
   NR_CHECK_ARG(dtype == NR_F32 || dtype == NR_BF16, "nr_attention_varlen: bad dtype");
   if (n_seq <= 0 || n_qblocks <= 0) return NR_OK;
   NR_CHECK_ARG(qkv && cu_seqlens && qblock_off && ctx, "nr_attention_varlen: null pointer");
+  NR_CHECK_DEVICE("nr_attention_varlen", qkv, cu_seqlens, qblock_off, ctx);
   NR_CHECK_ARG(n_qblocks <= 0x7fffffff, "nr_attention_varlen: too many query blocks");
   const dim3 grid((unsigned)n_qblocks, 4);  // 4 blocks x 4 waves = 16 heads
   hipStream_t s = (hipStream_t)stream;

@@ -1143,6 +1143,8 @@ extern "C" int nr_set_persistent_workgroups(int n) {
   return NR_OK;
 }
 
+extern "C" int nr_persistent_workgroups(void) { return g_persist_wgs; }
+
 static int num_cus() {
   if (g_persist_wgs) return g_persist_wgs;
   static int n_cu = 0;
@@ -1390,6 +1392,7 @@ extern "C" int nr_gemm_relu_dropout(int dtype_in, int dtype_out, int64_t M, int6
                                     void* C, int64_t ldc, uint64_t seed, float p, void* stream) {
   nr::clear_error();
   NR_CHECK_ARG(p >= 0.f && p < 1.f, "nr_gemm_relu_dropout: p must be in [0, 1)");
+  if (M > 0) NR_CHECK_DEVICE("nr_gemm_relu_dropout", A, W, bias, C);
   const double t = (double)p * 4294967296.0;
   const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
   return nr::gemm_dispatch_ex(dtype_in, dtype_out, NR_EPI_RELU_DROPOUT, M, N, K, A, lda, W, ldw, bias, nullptr, 0,
@@ -1400,6 +1403,7 @@ extern "C" int nr_gemm_drelu(int dtype_in, int dtype_out, int64_t M, int64_t N, 
                              int64_t lda, const void* W, int64_t ldw, const void* Y, int64_t ldy, void* C,
                              int64_t ldc, float scale, void* stream) {
   nr::clear_error();
+  if (M > 0) NR_CHECK_DEVICE("nr_gemm_drelu", A, W, Y, C);
   return nr::gemm_dispatch_ex(dtype_in, dtype_out, NR_EPI_DRELU, M, N, K, A, lda, W, ldw, nullptr, Y, ldy, C, ldc,
                               nr::EpiArgs{0, 0, scale}, (hipStream_t)stream);
 }
@@ -1408,6 +1412,7 @@ extern "C" int nr_gemm(int dtype_in, int dtype_out, int epilogue, int64_t M, int
                        const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
                        const void* R, int64_t ldr, void* C, int64_t ldc, void* stream) {
   nr::clear_error();
+  if (M > 0) NR_CHECK_DEVICE("nr_gemm", A, W, bias, R, C);
   return nr::gemm_dispatch(dtype_in, dtype_out, epilogue, M, N, K, A, lda, W, ldw, bias, R, ldr, C,
                            ldc, (hipStream_t)stream);
 }
@@ -1431,6 +1436,7 @@ extern "C" int nr_gemm_grouped(int dtype_in, int dtype_out, int n, const int64_t
                  (long long)M[i], (long long)N[i], (long long)K[i]);
     if (M[i] == 0) continue;  // empty problem: no operand is read (torch gives a null data pointer)
     NR_CHECK_ARG(A[i] && W[i] && C[i], "nr_gemm_grouped: problem %d null operand", i);
+    NR_CHECK_DEVICE("nr_gemm_grouped", A[i], W[i], C[i]);
     NR_CHECK_ARG(lda[i] >= K[i] && ldw[i] >= K[i] && lda[i] % e16 == 0 && ldw[i] % e16 == 0 && ldc[i] >= N[i] &&
                      ldc[i] % vo == 0 && ((uintptr_t)A[i] & 15) == 0 && ((uintptr_t)W[i] & 15) == 0 &&
                      ((uintptr_t)C[i] & 15) == 0,

@@ -257,6 +257,14 @@ struct nrh_split {
 
 extern "C" const char* nrh_last_error(void) { return g_err; }
 
+// sha256 of behaviors.cpp + include/newsrec_host.h (native.source_hash), set by the build
+#ifndef NRH_BUILD_HASH
+#define NRH_BUILD_HASH "unknown"
+#endif
+static const char kBuildTag[] __attribute__((used)) = "nrh-build-hash:" NRH_BUILD_HASH;
+
+extern "C" const char* nrh_build_hash(void) { return kBuildTag + 15; }
+
 extern "C" int nrh_split_behaviors(const char* imps, const int64_t* imp_off, const char* hist, const int64_t* hist_off,
                                    const uint8_t* hist_skip, int64_t n_rows, int label_present, nrh_split** out) {
   g_err[0] = 0;

@@ -229,6 +229,7 @@ extern "C" int nr_impression_metrics(const int32_t* ranks, const float* labels, 
   NR_CHECK_ARG(n_imp >= 0, "nr_impression_metrics: n_imp < 0");
   if (n_imp == 0) return NR_OK;
   NR_CHECK_ARG(ranks && labels && cand_off && metrics && tie_flag && status, "nr_impression_metrics: null pointer");
+  NR_CHECK_DEVICE("nr_impression_metrics", ranks, labels, cand_off, metrics, tie_flag, status);
   const dim3 grid((unsigned)((n_imp + 3) / 4));
   hipLaunchKernelGGL(nr::metrics_reg_kernel, grid, dim3(256), 0, (hipStream_t)stream, ranks, labels, cand_off, n_imp,
                      metrics, tie_flag, status);

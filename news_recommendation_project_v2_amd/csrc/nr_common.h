@@ -11,12 +11,20 @@
 #include <stdio.h>
 #include <stdarg.h>
 
+#include <initializer_list>
+
 #include "../../include/newsrec.h"
 
 namespace nr {
 
 void set_error(const char* fmt, ...);
 void clear_error();
+
+// Device residency of caller pointers (capi.hip): true for device / managed
+// memory.  check_device_ptrs names the first offending argument of the
+// stringified list `names`; null pointers are skipped (nullable arguments).
+bool device_accessible(const void* p);
+int check_device_ptrs(const char* fn, const char* names, std::initializer_list<const void*> ptrs);
 
 // internal dispatchers (validate + launch, no error reset)
 int gemm_dispatch(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, int64_t K,
@@ -82,7 +90,15 @@ __device__ __forceinline__ float wave_max(float v) {
     }                                           \
   } while (0)
 
-#define NR_CHECK_LAUNCH(name)                                                 \
+// Every public entry validates the pointers it hands to a kernel:
+//   NR_CHECK_DEVICE("nr_pool_score", hist_table, cand_table, ...);
+#define NR_CHECK_DEVICE(fn, ...)                                                 \
+  do {                                                                           \
+    const int _rc = nr::check_device_ptrs(fn, #__VA_ARGS__, {__VA_ARGS__});      \
+    if (_rc) return _rc;                                                         \
+  } while (0)
+
+#define NR_CHECK_LAUNCH(name)                                               \
   do {                                                                        \
     hipError_t _e = hipGetLastError();                                        \
     if (_e != hipSuccess) {                                                   \

@@ -303,6 +303,8 @@ extern "C" int nr_pool_score(int pooler, int dtype, int64_t dim, const void* his
   const bool score = cand_off != nullptr;
   NR_CHECK_ARG(hist_table && hist_off && (score || users), "nr_pool_score: null pointer");
   NR_CHECK_ARG(!score || (cand_table && cand_inv_norm && cand_idx && scores), "nr_pool_score: null candidate pointer");
+  NR_CHECK_DEVICE("nr_pool_score", hist_table, cand_table, cand_inv_norm, hist_idx, hist_off, cand_idx, cand_off,
+                  scores, users);
   if (!score) {
     cand_table = hist_table;
     cand_ld = hist_ld;
@@ -343,6 +345,7 @@ extern "C" int nr_score_users(int dtype, int64_t dim, const float* users, const 
   if (n_imp == 0) return NR_OK;
   NR_CHECK_ARG(users && user_idx && cand_table && cand_inv_norm && cand_idx && cand_off && scores,
                "nr_score_users: null pointer");
+  NR_CHECK_DEVICE("nr_score_users", users, user_idx, cand_table, cand_inv_norm, cand_idx, cand_off, scores);
   NR_CHECK_ARG(cand_ld >= dim && cand_ld % (dtype == NR_F32 ? 4 : 8) == 0 && ((uintptr_t)cand_table & 15) == 0,
                "nr_score_users: cand_table must be 16-byte aligned with 16-byte row strides");
   hipStream_t s = (hipStream_t)stream;

@@ -140,6 +140,7 @@ extern "C" int nr_dense_rank(const float* scores, const int64_t* cand_off, int64
   NR_CHECK_ARG(n_imp >= 0, "nr_dense_rank: n_imp < 0");
   if (n_imp == 0) return NR_OK;
   NR_CHECK_ARG(scores && cand_off && ranks && status, "nr_dense_rank: null pointer");
+  NR_CHECK_DEVICE("nr_dense_rank", scores, cand_off, ranks, status);
   const int64_t groups = (n_imp + 3) / 4;
   hipLaunchKernelGGL(nr::dense_rank_reg_kernel, dim3((unsigned)groups), dim3(256), 0, (hipStream_t)stream, scores,
                      cand_off, n_imp, ranks);

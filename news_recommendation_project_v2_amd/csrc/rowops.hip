@@ -383,6 +383,7 @@ extern "C" int nr_gather_layernorm(int dtype_in, int64_t n, int64_t dim, const v
                                    const int64_t* row_idx, int n_ln, const float* gammas, const float* betas,
                                    float eps, float* out, int64_t ldo, void* stream) {
   nr::clear_error();
+  if (n > 0) NR_CHECK_DEVICE("nr_gather_layernorm", x, row_idx, gammas, betas, out);
   return nr::gather_ln_dispatch(dtype_in, n, dim, x, ldx, row_idx, n_ln, gammas, betas, eps, out, ldo,
                                 (hipStream_t)stream);
 }
@@ -391,6 +392,7 @@ extern "C" int nr_layernorm(int dtype_in, int dtype_out, int64_t rows, int64_t d
                             int64_t ldx, const float* gamma, const float* beta, float eps, void* y,
                             int64_t ldy, void* stream) {
   nr::clear_error();
+  if (rows > 0) NR_CHECK_DEVICE("nr_layernorm", x, gamma, beta, y);
   return nr::layernorm_dispatch(dtype_in, dtype_out, rows, dim, x, ldx, gamma, beta, eps, y, ldy,
                                 (hipStream_t)stream);
 }
@@ -398,17 +400,20 @@ extern "C" int nr_layernorm(int dtype_in, int dtype_out, int64_t rows, int64_t d
 extern "C" int nr_softmax64(int64_t rows, int64_t groups, const float* x, int64_t ldx,
                             int dtype_out, void* y, int64_t ldy, void* stream) {
   nr::clear_error();
+  if (rows > 0) NR_CHECK_DEVICE("nr_softmax64", x, y);
   return nr::softmax64_dispatch(rows, groups, x, ldx, dtype_out, y, ldy, (hipStream_t)stream);
 }
 
 extern "C" int nr_row_inv_norm(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx,
                                float eps, float* out, void* stream) {
   nr::clear_error();
+  if (rows > 0) NR_CHECK_DEVICE("nr_row_inv_norm", x, out);
   return nr::inv_norm_dispatch(dtype, rows, dim, x, ldx, eps, out, (hipStream_t)stream);
 }
 
 extern "C" int nr_row_stats(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps, float* out,
                             void* stream) {
   nr::clear_error();
+  if (rows > 0) NR_CHECK_DEVICE("nr_row_stats", x, out);
   return nr::row_stats_dispatch(dtype, rows, dim, x, ldx, eps, out, (hipStream_t)stream);
 }

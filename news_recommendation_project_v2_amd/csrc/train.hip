@@ -484,6 +484,7 @@ extern "C" int nr_gather_rows(int dtype_in, int dtype_out, int64_t n, int64_t di
   NR_CHECK_ARG(n >= 0 && dim > 0 && lds >= dim && ldd >= dim, "nr_gather_rows: bad shape");
   if (n == 0) return NR_OK;
   NR_CHECK_ARG(src && dst, "nr_gather_rows: null pointer");
+  NR_CHECK_DEVICE("nr_gather_rows", src, idx, dst);
   NR_DT2(dtype_in, dtype_out,
          hipLaunchKernelGGL((gather_rows_kernel<TI, TO>), dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream, n,
                             dim, (const TI*)src, lds, idx, (TO*)dst, ldd));
@@ -498,6 +499,7 @@ extern "C" int nr_transpose(int dtype_in, int dtype_out, int64_t rows, int64_t c
   NR_CHECK_ARG(rows >= 0 && cols >= 0 && lds >= cols && ldd >= rows, "nr_transpose: bad shape");
   if (rows == 0 || cols == 0) return NR_OK;
   NR_CHECK_ARG(src && dst, "nr_transpose: null pointer");
+  NR_CHECK_DEVICE("nr_transpose", src, dst);
   NR_CHECK_ARG((rows + 63) / 64 <= 65535, "nr_transpose: too many rows");
   const dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
   const bool b16 = dtype_in == dtype_out && dtype_in != NR_F32;
@@ -521,6 +523,7 @@ extern "C" int nr_final_pool_fwd(int dtype, int64_t n_seg, const int64_t* off, c
   NR_CHECK_ARG(NR_OKDT(dtype) && n_seg >= 0 && ld >= 2048, "nr_final_pool_fwd: bad args");
   if (n_seg == 0) return NR_OK;
   NR_CHECK_ARG(off && xp && users && z, "nr_final_pool_fwd: null pointer");
+  NR_CHECK_DEVICE("nr_final_pool_fwd", off, xp, users, z);
   NR_DT1(dtype, hipLaunchKernelGGL((final_pool_fwd_kernel<T>), dim3((unsigned)n_seg, 4), dim3(256), 0,
                                    (hipStream_t)stream, n_seg, off, (const T*)xp, ld, users, z));
   NR_CHECK_LAUNCH("nr_final_pool_fwd");
@@ -535,6 +538,7 @@ extern "C" int nr_final_pool_bwd(int dtype, int64_t n_seg, const int64_t* off, i
                "nr_final_pool_bwd: bad args");
   if (n_seg == 0 && n_rows == 0) return NR_OK;
   NR_CHECK_ARG(off && xp && users && z && du && dx && dl, "nr_final_pool_bwd: null pointer");
+  NR_CHECK_DEVICE("nr_final_pool_bwd", off, xp, users, z, du, dx, dl);
   const unsigned grid = (unsigned)(n_seg + 64);  // 64 trailing blocks zero the padding rows
   NR_DT1(dtype, hipLaunchKernelGGL((final_pool_bwd_kernel<T>), dim3(grid, 4), dim3(256), 0, (hipStream_t)stream,
                                    n_seg, off, n_rows, (const T*)xp, ld, users, z, du, (T*)dx, lddx, (T*)dl, lddl));
@@ -549,6 +553,7 @@ extern "C" int nr_cosine_margin(int64_t B, const float* users, const float* E, i
   NR_CHECK_ARG(B >= 0 && lde >= 1024 && lde % 4 == 0, "nr_cosine_margin: bad args");
   if (B == 0) return NR_OK;
   NR_CHECK_ARG(users && E && pos && neg && loss && du && dE, "nr_cosine_margin: null pointer");
+  NR_CHECK_DEVICE("nr_cosine_margin", users, E, pos, neg, s_out, loss, du, dE);
   hipLaunchKernelGGL(cosine_margin_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, (hipStream_t)stream, B,
                      users, E, lde, pos, neg, margin, s_out, loss, du, dE);
   NR_CHECK_LAUNCH("nr_cosine_margin");
@@ -561,6 +566,7 @@ extern "C" int nr_scatter_add_rows(int dtype, int64_t n, int64_t dim, const void
   NR_CHECK_ARG(NR_OKDT(dtype) && n >= 0 && dim > 0 && lds >= dim && ldd >= dim, "nr_scatter_add_rows: bad args");
   if (n == 0) return NR_OK;
   NR_CHECK_ARG(src && idx && dst, "nr_scatter_add_rows: null pointer");
+  NR_CHECK_DEVICE("nr_scatter_add_rows", src, idx, dst);
   NR_DT1(dtype, hipLaunchKernelGGL((scatter_add_rows_kernel<T>), dim3((unsigned)n), dim3(256), 0,
                                    (hipStream_t)stream, n, dim, (const T*)src, lds, idx, dst, ldd));
   NR_CHECK_LAUNCH("nr_scatter_add_rows");
@@ -573,6 +579,7 @@ extern "C" int nr_col_sum(int dtype, int64_t rows, int64_t cols, const void* src
   NR_CHECK_ARG(NR_OKDT(dtype) && rows >= 0 && cols > 0 && lds >= cols, "nr_col_sum: bad args");
   if (rows == 0) return NR_OK;
   NR_CHECK_ARG(src && out, "nr_col_sum: null pointer");
+  NR_CHECK_DEVICE("nr_col_sum", src, out);
   // ~1024 blocks: column groups of 512 x row ranges (multiple of 4 rows, >= 32)
   const int64_t cgroups = (cols + 511) / 512;
   int64_t rpb = (rows * cgroups + 1023) / 1024;
@@ -594,6 +601,7 @@ extern "C" int nr_ln_param_grad(int dtype_in, int64_t n, int64_t dim, const void
   NR_CHECK_ARG(dtype_in == NR_F32 || dtype_in == NR_BF16 || dtype_in == NR_F16, "nr_ln_param_grad: bad dtype");
   if (n == 0) return NR_OK;
   NR_CHECK_ARG(x && dy && dgamma && dbeta, "nr_ln_param_grad: null pointer");
+  NR_CHECK_DEVICE("nr_ln_param_grad", x, row_idx, dy, dgamma, dbeta);
   NR_CHECK_ARG(lddy % 4 == 0 && ((uintptr_t)dy & 15) == 0, "nr_ln_param_grad: dy rows must be 16-byte aligned");
   const int64_t g16 = (n + 15) / 16;  // ~16 rows per block: few enough blocks that the final atomics stay cheap
   const unsigned grid = (unsigned)(g16 < 256 ? g16 : 256);
@@ -616,6 +624,7 @@ extern "C" int nr_sumsq(int64_t n, const float* x, float* out, void* stream) {
   NR_CHECK_ARG(n >= 0, "nr_sumsq: bad n");
   if (n == 0) return NR_OK;
   NR_CHECK_ARG(x && out, "nr_sumsq: null pointer");
+  NR_CHECK_DEVICE("nr_sumsq", x, out);
   const int64_t g = (n / 4 + 255) / 256;
   hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)(g < 1 ? 1 : g < 1024 ? g : 1024)), dim3(256), 0,
                      (hipStream_t)stream, n, x, out);
@@ -630,6 +639,7 @@ extern "C" int nr_adamw(int64_t n, float* p, const float* g, float* m, float* v,
   NR_CHECK_ARG(n >= 0 && step >= 1, "nr_adamw: bad args");
   if (n == 0) return NR_OK;
   NR_CHECK_ARG(p && g && m && v, "nr_adamw: null pointer");
+  NR_CHECK_DEVICE("nr_adamw", p, g, m, v, p_bf16, sumsq);
   const float bc1 = (float)(1.0 - pow((double)beta1, (double)step));
   const float bc2s = (float)sqrt(1.0 - pow((double)beta2, (double)step));
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v,
@@ -650,6 +660,7 @@ extern "C" int nr_splitk_fixup(int dtype_out, int epilogue, int64_t rows, int64_
   if (rows == 0) return NR_OK;
   NR_CHECK_ARG(partials && C && (epilogue != NR_EPI_DRELU || (R && ldr >= N)), "nr_splitk_fixup: null pointer");
   NR_CHECK_ARG(((uintptr_t)partials & 15) == 0, "nr_splitk_fixup: partials must be 16-byte aligned");
+  NR_CHECK_DEVICE("nr_splitk_fixup", partials, bias, R, C);
   // dropout threshold and scale exactly as nr_gemm_relu_dropout forms them
   const double t = (double)p * 4294967296.0;
   const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;

@@ -5,8 +5,9 @@ parallel strategy the hot path needs:
   phase A  each rank runs the per-news pooler transform on a contiguous
            1/world slice of the news table (MFMA GEMMs, no communication);
   phase B  the all-gather of the [N/world, k*1024] slices (RCCL ncclAllGather
-           over xGMI) gives every GPU the full table; the shard is transformed
-           in two chunks and chunk 0's all-gather overlaps chunk 1's transform;
+           over xGMI) gives every GPU the full table (opt-in: the shard is
+           transformed in chunks and chunk c's all-gather overlaps chunk c+1's
+           transform);
   phase C  impressions are split into contiguous, cost-balanced ranges and
            pooled + scored with no further communication.
 Scores stay on their rank; ``gather_scores`` concatenates them in impression
@@ -55,7 +56,11 @@ def partition_by_cost(hist_len: np.ndarray, cand_len: np.ndarray, world: int, ta
 # (N = 2), +0.05 at 18 k (N = 4), +0.19 at 9 k (N = 8, where the chain's
 # K = 4096 GEMM is one tile round either way) -- against half of the
 # all-gather (74 / 110 / 129 MB inbound per GPU at N = 2 / 4 / 8 over 1 / 3 /
-# 7 xGMI links).  So: two chunks for shards of >= 2 x CHUNK_MIN_ROWS rows.
+# 7 xGMI links).  Whether RCCL's kernels actually run beside the persistent GEMMs
+# at world > 1 (and whether RCCL_CUS is enough) has not been measured on a
+# multi-GPU node yet, so the overlap is opt-in (``chunks="auto"`` or an int); the
+# default is one transform + one in-place all_gather_into_tensor.  The bench at
+# N > 1 measures both and checks the tables agree bit for bit.
 CHUNK_MIN_ROWS = 8192
 # CUs left to RCCL's kernels while the persistent GEMMs of an overlapped chunk
 # run (a persistent GEMM workgroup holds a whole CU)
@@ -65,13 +70,20 @@ RCCL_CUS = 16
 class ShardedTable:
     """Phase A + B: sharded per-news transform and the one-time all-gather.
 
-    With ``chunks`` > 1 (default 2 at world > 1 when each half has at least
-    CHUNK_MIN_ROWS rows) the shard's rows are transformed chunk by chunk and
-    each chunk is all-gathered asynchronously (``dist.all_gather`` into the
-    rank-major table's row ranges) while the next chunk is transformed; the
-    persistent GEMMs of the chunks then run on all but RCCL_CUS CUs."""
+    Default (``chunks=1``): the shard is transformed, then one in-place
+    all_gather_into_tensor.  With ``chunks`` > 1 (or "auto": 2 at world > 1
+    when each half has at least CHUNK_MIN_ROWS rows) the shard's rows are
+    transformed chunk by chunk and each chunk is all-gathered asynchronously
+    (``dist.all_gather`` into the rank-major table's row ranges) while the next
+    chunk is transformed; the persistent GEMMs of the chunks then run on all but
+    RCCL_CUS CUs.
 
-    def __init__(self, engine: PoolScoreEngine, rank: int, world: int, group=None, chunks: Optional[int] = None):
+    ``timing=True`` records HIP events on the current stream around the
+    transform and around the collective (chunks == 1: the current stream waits
+    for RCCL's stream at the end of the call, so the second interval is the
+    all-gather); ``last_ms()`` reads them after a sync."""
+
+    def __init__(self, engine: PoolScoreEngine, rank: int, world: int, group=None, chunks=1, timing: bool = False):
         self.eng, self.rank, self.world, self.group = engine, rank, world, group
         n = engine.hist_src.shape[0]
         self.rows = shard_rows(n, world)
@@ -94,10 +106,33 @@ class ShardedTable:
         in_place = world == 1 or not _host_staged(group)
         self.local = self.full[rank * self.rows:(rank + 1) * self.rows] if in_place else \
             torch.empty((self.rows, width), dtype=engine.dtype, device=engine.device)
-        if chunks is None:
+        if chunks is None or chunks == "auto":
             chunks = 2 if world > 1 and self.rows >= 2 * CHUNK_MIN_ROWS else 1
         self.chunks = max(1, min(int(chunks), self.rows))
         self.bounds = [round(c * self.rows / self.chunks) for c in range(self.chunks + 1)]
+        self.timing = bool(timing) and self.full.is_cuda
+        self._ev = None
+
+    def _mark(self, i: int) -> None:
+        if self.timing:
+            if self._ev is None:
+                self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            self._ev[i].record()
+
+    def last_ms(self):
+        """(transform_ms, allgather_ms) of the last build() with timing on (the
+        all-gather interval includes any wait for the collective); None for the
+        overlapped path's gather, which has no separate interval."""
+        if not self._ev:
+            return None
+        t = self._ev[0].elapsed_time(self._ev[1])
+        g = self._ev[1].elapsed_time(self._ev[2]) if self.chunks == 1 else None
+        return t, g
+
+    @property
+    def gather_bytes_in(self) -> int:
+        """Bytes each rank receives from its peers in the all-gather."""
+        return (self.world - 1) * self.rows * self.full.shape[1] * self.full.element_size()
 
     def _overlapped(self) -> None:
         """Transform chunk c, then all-gather it asynchronously (byte views: any
@@ -105,14 +140,19 @@ class ShardedTable:
         in-place all_gather_into_tensor (no staging buffer, no copies)."""
         from . import ops
         if self.chunks == 1:
+            self._mark(0)
             self.eng.transform(rows=slice(self.lo, self.lo + self.rows), out=self.local, src=self.src)
+            self._mark(1)
             dist.all_gather_into_tensor(self.full.view(torch.uint8), self.local.view(torch.uint8), group=self.group)
+            self._mark(2)
             return
         reserve = self.full.is_cuda and self.chunks > 1
+        prev = ops.persistent_workgroups() if reserve else 0
         if reserve:
             ncu = torch.cuda.get_device_properties(self.full.device).multi_processor_count
             ops.set_persistent_workgroups(max(8, (ncu - RCCL_CUS) // 8 * 8))
         works = []
+        self._mark(0)
         try:
             for a, b in zip(self.bounds[:-1], self.bounds[1:]):
                 self.eng.transform(rows=slice(self.lo + a, self.lo + b), out=self.local[a:b], src=self.src)
@@ -120,16 +160,22 @@ class ShardedTable:
                 works.append(dist.all_gather(outs, self.local[a:b].view(torch.uint8), group=self.group, async_op=True))
         finally:
             if reserve:
-                ops.set_persistent_workgroups(0)
-        for w in works:
-            w.wait()
+                ops.set_persistent_workgroups(prev)
+            # every collective already issued completes before this rank leaves (on an
+            # exception too: peers are inside the same collectives and would hang)
+            for w in works:
+                w.wait()
+        self._mark(1)
+        self._mark(2)
 
     def build(self) -> torch.Tensor:
         if self.world > 1 and not (_host_staged(self.group) and self.local.is_cuda):
             self._overlapped()
             self.eng.hist_table = self.full
             return self.full
+        self._mark(0)
         self.eng.transform(rows=slice(self.lo, self.lo + self.rows), out=self.local, src=self.src)
+        self._mark(1)
         if self.world > 1:
             if _host_staged(self.group) and self.local.is_cuda:
                 # gloo moves host memory: stage the slices through the host as raw bytes
@@ -137,6 +183,7 @@ class ShardedTable:
                 dist.all_gather_into_tensor(host.view(torch.uint8), self.local.cpu().view(torch.uint8),
                                             group=self.group)
                 self.full.copy_(host)
+        self._mark(2)
         self.eng.hist_table = self.full
         return self.full
 

@@ -54,6 +54,7 @@ class PoolScoreEngine:
         self.cand_inv = None
         self.hist_table = None
         self._ws = None
+        self._users = None  # f32 [distinct histories, D], reused across steps
 
     # ------------------------------------------------------------ inputs
     def load_news(self, news_embeddings: torch.Tensor, query_news_embeddings: Optional[torch.Tensor] = None):
@@ -123,7 +124,10 @@ class PoolScoreEngine:
 
     def pool_score(self, want_users: bool = False, scores: Optional[torch.Tensor] = None):
         if self.user_idx is not None:  # distinct histories pooled once, then scored per impression
-            users = ops.pool_users(self.pooler, self.hist_table, self.uhist_idx, self.uhist_off)
+            n_u = self.uhist_off.numel() - 1
+            if self._users is None or self._users.shape[0] != n_u:
+                self._users = torch.empty((n_u, 1024), dtype=torch.float32, device=self.device)
+            users = ops.pool_users(self.pooler, self.hist_table, self.uhist_idx, self.uhist_off, out=self._users)
             s = ops.score_users(users, self.user_idx, self.cand_table, self.cand_inv, self.cand_idx, self.cand_off,
                                 self.n_cand, scores=scores)
             return s, (users[self.user_idx.long()] if want_users else None)

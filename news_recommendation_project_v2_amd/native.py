@@ -18,6 +18,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 LIB_PATH = Path(__file__).resolve().with_name("libnewsrec_host.so")
+SOURCES = (Path(__file__).resolve().with_name("csrc") / "host" / "behaviors.cpp",
+           Path(__file__).resolve().parent.parent / "include" / "newsrec_host.h")
 _LIB = None
 _p = ctypes.c_void_p
 
@@ -27,7 +29,13 @@ def load():
     if _LIB is None:
         if not LIB_PATH.is_file():
             return None
+        from ._lib import source_hash
         lib = ctypes.CDLL(os.fspath(LIB_PATH))
+        lib.nrh_build_hash.restype = ctypes.c_char_p
+        want, got = source_hash(SOURCES), lib.nrh_build_hash().decode("ascii", "replace")
+        if want is not None and got != want:
+            raise RuntimeError(f"{LIB_PATH} was built from other sources (build hash {got}, tree {want}): "
+                               "rebuild it with `python -c 'import __graft_entry__ as g; g.build()'`")
         lib.nrh_split_behaviors.restype = ctypes.c_int
         lib.nrh_split_behaviors.argtypes = [_p, _p, _p, _p, _p, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(_p)]
         lib.nrh_split_sizes.restype = ctypes.c_int

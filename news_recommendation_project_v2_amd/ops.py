@@ -67,6 +67,11 @@ def set_persistent_workgroups(n: int = 0) -> None:
     _lib.call("nr_set_persistent_workgroups", int(n))
 
 
+def persistent_workgroups() -> int:
+    """The current persistent-GEMM workgroup budget (0 = one per CU)."""
+    return int(_lib.load().nr_persistent_workgroups())
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
          epilogue: str = "none", residual: Optional[torch.Tensor] = None,
          out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
@@ -224,13 +229,16 @@ def pool_score(pooler: str, hist_table: torch.Tensor, cand_table: torch.Tensor, 
     return scores, users
 
 
-def pool_users(pooler: str, hist_table: torch.Tensor, hist_idx: torch.Tensor, hist_off: torch.Tensor) -> torch.Tensor:
+def pool_users(pooler: str, hist_table: torch.Tensor, hist_idx: torch.Tensor, hist_off: torch.Tensor,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Pooling only (nr_pool_score with no candidates): users [n, D] f32, one
-    row per history segment."""
-    dev = _dev(hist_table, hist_idx, hist_off)
+    row per history segment (into ``out`` when given)."""
+    dev = _dev(hist_table, hist_idx, hist_off, out)
     _check_csr(hist_idx, hist_off, "hist")
     n, dim = hist_off.numel() - 1, hist_table.shape[1] if pooler != "final" else hist_table.shape[1] // 2
-    users = torch.empty((n, dim), dtype=torch.float32, device=dev)
+    if out is not None and (out.dtype != torch.float32 or out.shape != (n, dim) or not out.is_contiguous()):
+        raise _lib.NewsRecHIPError(f"pool_users: out must be contiguous f32 {(n, dim)}")
+    users = torch.empty((n, dim), dtype=torch.float32, device=dev) if out is None else out
     if n == 0:
         return users
     hidx = hist_idx if hist_idx.numel() else torch.zeros(1, dtype=torch.int32, device=dev)

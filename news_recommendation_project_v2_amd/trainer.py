@@ -43,7 +43,12 @@ class AttentionAttentionTrainer:
                  final_attn_ckpt_dir: Optional[Path] = None, exp_name: str = "",
                  max_neg_ratio: Optional[float] = None, max_pos_ratio: Optional[float] = None,
                  rng: Optional[np.random.Generator] = None, batch_size: int = DEFAULT_TRAIN_BATCH,
-                 dtype: torch.dtype = torch.float32, lr: float = 1e-6, dropout: float = 0.1, seed: int = 1234):
+                 dtype: torch.dtype = torch.float32, lr: float = 1e-6, dropout: float = 0.1, seed: int = 1234,
+                 nan_check_every: Optional[int] = None):
+        if nan_check_every is not None:
+            if int(nan_check_every) < 1:
+                raise ValueError("nan_check_every must be >= 1")
+            self.NAN_CHECK_EVERY = int(nan_check_every)
         self.rng = rng if rng is not None else np.random.default_rng(1234)
         self.log_dir = log_dir
         self.exp_name = exp_name
@@ -69,17 +74,21 @@ class AttentionAttentionTrainer:
                           hist_off=torch.as_tensor(hoff).to(d), pos=torch.as_tensor(pos).to(d),
                           neg=torch.as_tensor(neg).to(d))
 
-    NAN_CHECK_EVERY = 64  # batches between host checks of the device-side losses
+    # batches between host checks of the device-side losses; 1 = the reference's
+    # behaviour exactly (sync on every loss, stop right after the first NaN batch)
+    NAN_CHECK_EVERY = 64
 
     def train_one_epoch(self) -> float:
         """trainer.py:1030-1117.  The reference syncs on every loss and stops the
         epoch after the first NaN batch (whose optimizer step it has already
         applied, :1069-1072).  Here losses stay on the device and are checked
         every NAN_CHECK_EVERY batches, so up to that many further steps may run
-        after a NaN.  The results are the same: a NaN loss means NaN gradients,
-        the clipped AdamW step of that batch already makes every parameter NaN in
-        both implementations, and the epoch loss sums exactly the batches before
-        the first NaN, like the reference's running_loss."""
+        after a NaN (``nan_check_every=1`` checks every batch, as the reference
+        does, at the cost of one host sync per step).  The parameters end NaN in
+        both cases (a NaN loss means NaN gradients, and the clipped AdamW step of
+        that batch already makes every parameter NaN), and the epoch loss sums
+        exactly the batches before the first NaN, like the reference's
+        running_loss; only the optimizer / RNG step counts can differ."""
         self.token_attention_model.train()
         self.final_attention_model.train()
         running_loss, running_count = 0.0, 0

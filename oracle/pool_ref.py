@@ -175,3 +175,114 @@ def final_second_attention_score(pooler: str, sd: dict, hist_idx, hist_len, cand
     scores = cos_sim_scores(pooler, sd, hist_idx, hist_len, np.asarray(cand_idx)[np.repeat(hb, cl)], cl[hb],
                             table, batch_size).numpy()
     return {"scores": scores, "grouped_scores": dense_ranks(scores, cl)}
+
+
+# ---------------------------------------------------------------- full-size checker
+# The reference's per-slot algorithm above takes ~5,700 s on MIND-large dev
+# (BASELINE.md §2).  The functions below compute the same scores per unique news
+# (exact up to f32 summation order) in chunks of impressions, so the
+# CPU checker covers all 376,471 impressions in about a minute of host time.
+
+def latent_hiddens_kv_once(sd: dict, emb: torch.Tensor, heads: int = 8) -> torch.Tensor:
+    """latent_hiddens for single-slot rows emb [n, D], with K, V =
+    to_kv(LN_c(latents)) computed once: latent_attention.py:161-162 rebuilds
+    them for every batch row from the same latents, so every row sees the same
+    K, V.  SDPA (:72, no mask, scale 1/sqrt(512)) written out as softmax(q kᵀ) v."""
+    p = "cross_attend_blocks.0."
+    q_ = "cross_attend_blocks.1."
+    d = emb.shape[-1]
+    ctx = F.layer_norm(sd["latents"], (d,), sd[p + "norm_context.weight"], sd[p + "norm_context.bias"], 1e-5)
+    k, v = F.linear(ctx, sd[p + "fn.to_kv.weight"]).chunk(2, dim=-1)          # [64, h*dh] each
+    nl, hd = k.shape
+    dh = hd // heads
+    k = k.reshape(nl, heads, dh).permute(1, 0, 2)                             # [h, 64, dh]
+    v = v.reshape(nl, heads, dh).permute(1, 0, 2)
+    xq = F.layer_norm(emb, (d,), sd[p + "norm.weight"], sd[p + "norm.bias"], 1e-5)
+    q = F.linear(xq, sd[p + "fn.to_q.weight"]).reshape(-1, heads, dh)         # [n, h, dh]
+    a = torch.softmax(torch.einsum("nhd,hjd->nhj", q, k) / math.sqrt(dh), dim=-1)
+    o = torch.einsum("nhj,hjd->nhd", a, v).reshape(-1, heads * dh)
+    h = F.linear(o, sd[p + "fn.to_out.weight"]) + emb
+    z = F.layer_norm(h, (d,), sd[q_ + "norm.weight"], sd[q_ + "norm.bias"], 1e-5)
+    z = F.linear(z, sd[q_ + "fn.net.0.weight"], sd[q_ + "fn.net.0.bias"])
+    a_, g = z.chunk(2, dim=-1)
+    return F.linear(a_ * F.gelu(g), sd[q_ + "fn.net.2.weight"], sd[q_ + "fn.net.2.bias"]) + h
+
+
+def per_news_tables_large(pooler: str, sd: dict, table: torch.Tensor, chunk: int = 4096) -> torch.Tensor:
+    """per_news_tables over a whole news table (latent: K/V once per model)."""
+    outs = []
+    with torch.no_grad():
+        for s in range(0, table.shape[0], chunk):
+            e = table[s:s + chunk]
+            if pooler == "final":
+                outs.append(per_news_tables("final", sd, e, chunk=chunk))
+            else:
+                outs.append(latent_hiddens_kv_once(sd, e))
+    return torch.cat(outs)
+
+
+_FASTPOOL = []
+
+
+def _fastpool():
+    """oracle/libfastpool.so (built by __graft_entry__.build()), or None."""
+    if not _FASTPOOL:
+        import ctypes
+        from pathlib import Path
+        so = Path(__file__).resolve().with_name("libfastpool.so")
+        lib = None
+        if so.is_file():
+            lib = ctypes.CDLL(str(so))
+            v, i64 = ctypes.c_void_p, ctypes.c_int64
+            lib.fp_pool.argtypes = [ctypes.c_int, v, i64, v, v, i64, v]
+            lib.fp_pool.restype = None
+            lib.fp_cosine.argtypes = [v, v, v, v, i64, v]
+            lib.fp_cosine.restype = None
+        _FASTPOOL.append(lib)
+    return _FASTPOOL[0]
+
+
+def cos_sim_scores_large(pooler: str, sd: dict, hist_idx, hist_len, cand_idx, cand_len, table: torch.Tensor,
+                         chunk_imps: int = 16384) -> np.ndarray:
+    """get_cos_sim_scores (data_model_helper.py:174-239) over any number of
+    impressions: per-news tables once, then impression chunks of the masked
+    reductions (FinalAttention Σx·p/(Σp+1e-10), modeling_utils.py:224-228;
+    Latent normalize(mean), latent_attention.py:165-170) and the per-vector-
+    clamped cosine (F.cosine_similarity, data_model_helper.py:223-227).
+    Host memory stays bounded by the chunk.  Returns f32 scores [C]."""
+    hist_idx = np.asarray(hist_idx, dtype=np.int64)
+    hist_len = np.asarray(hist_len, dtype=np.int64)
+    cand_idx = np.asarray(cand_idx, dtype=np.int64)
+    cand_len = np.asarray(cand_len, dtype=np.int64)
+    ho = np.concatenate([[0], np.cumsum(hist_len)])
+    co = np.concatenate([[0], np.cumsum(cand_len)])
+    n = len(hist_len)
+    out = np.empty(int(co[-1]), dtype=np.float32)
+    with torch.no_grad():
+        tab = per_news_tables_large(pooler, sd, table)
+        if pooler == "final":
+            x, p = tab[:, :1024], tab[:, 1024:]
+            tab = torch.cat([x * p, p], dim=1)  # per-news x*p: the same product every slot of the news forms
+        lib = _fastpool()
+        if lib is not None:  # the same reductions in C / OpenMP (oracle/fastpool.c)
+            tab = tab.contiguous()
+            users = np.empty((n, 1024), dtype=np.float32)
+            t = np.ascontiguousarray(table.numpy(), dtype=np.float32)
+            P = lambda arr: arr.ctypes.data  # noqa: E731
+            lib.fp_pool(0 if pooler == "final" else 1, tab.data_ptr(), tab.shape[1], P(hist_idx), P(ho), n, P(users))
+            lib.fp_cosine(P(users), P(t), P(cand_idx), P(co), n, P(out))
+            return out
+        for a in range(0, n, chunk_imps):
+            b = min(a + chunk_imps, n)
+            hl = torch.as_tensor(hist_len[a:b])
+            seg = torch.repeat_interleave(torch.arange(b - a), hl)
+            rows = tab[torch.as_tensor(hist_idx[ho[a]:ho[b]])]
+            acc = torch.zeros(b - a, rows.shape[1]).index_add_(0, seg, rows)
+            if pooler == "final":
+                users = acc[:, :1024] / (acc[:, 1024:] + 1e-10)
+            else:
+                users = F.normalize(acc / hl.unsqueeze(1).float(), p=2, dim=-1)
+            cseg = torch.repeat_interleave(torch.arange(b - a), torch.as_tensor(cand_len[a:b]))
+            out[co[a]:co[b]] = F.cosine_similarity(users[cseg], table[torch.as_tensor(cand_idx[co[a]:co[b]])],
+                                                   dim=-1).numpy()
+    return out

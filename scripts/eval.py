@@ -79,6 +79,8 @@ def main():
     ap.add_argument("--log-dir", type=Path, default=Path("logs"))
     ap.add_argument("--exp-name", default="attn_attn_epoch_5")
     ap.add_argument("--host-metrics", action="store_true", help="MIND metrics on the host (numpy) instead of the GPU")
+    ap.add_argument("--dump-scores", type=Path, default=None,
+                    help="write each split's per-candidate scores and dense ranks to {dir}/{split}.npz (rank 0)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -129,6 +131,10 @@ def main():
                 comp.dtype, rank, world))
         if rank != 0:
             continue
+        if args.dump_scores:
+            args.dump_scores.mkdir(parents=True, exist_ok=True)
+            np.savez(args.dump_scores / f"{name}.npz", scores=np.asarray(out["scores"], dtype=np.float32),
+                     ranks=np.concatenate([np.asarray(r, dtype=np.int64) for r in out["grouped_scores"]]))
         if args.host_metrics:
             results[name] = score(out["grouped_scores"], out["labels"])
         else:  # same metrics, one wave per impression on the MI355X (evaluation.score_device)

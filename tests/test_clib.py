@@ -58,3 +58,44 @@ def test_encoder_forward_validates_on_the_host():
     rc = lib.nr_pool_score(_lib.NR_POOL_MEAN, 0, 1024, None, 1024, None, 0, None, None, None, None, None, 1, None, None,
                            None)
     assert rc == -1 and b"null" in lib.nr_last_error()
+
+
+def test_library_hash_matches_the_tree():
+    """The loaded library was built from the sources beside it:
+    its embedded nr_build_hash equals the sha256 of csrc/*.hip + headers."""
+    if not _lib.LIB_PATH.is_file():
+        pytest.skip("libnewsrec_hip.so not built (run __graft_entry__.build())")
+    want = _lib.source_hash(_lib.hip_source_files())
+    assert _lib.embedded_hash(_lib.LIB_PATH) == want
+    assert _lib.load().nr_build_hash().decode() == want
+
+
+def test_loader_refuses_a_stale_library(monkeypatch):
+    if not _lib.LIB_PATH.is_file():
+        pytest.skip("libnewsrec_hip.so not built (run __graft_entry__.build())")
+    monkeypatch.setattr(_lib, "_LIB", None)
+    monkeypatch.setattr(_lib, "source_hash", lambda files: "0" * 16)
+    with pytest.raises(_lib.NewsRecHIPError, match="other sources"):
+        _lib.load()
+
+
+def test_host_pointers_are_refused_not_launched():
+    """Every entry validates pointer residency (hipPointerGetAttributes) before
+    launching: host memory gives NR_ERR_INVALID naming the argument, never a
+    kernel that faults (on this GPU-less host the runtime knows
+    no device memory at all, so every non-null pointer is refused)."""
+    if not _lib.LIB_PATH.is_file():
+        pytest.skip("libnewsrec_hip.so not built (run __graft_entry__.build())")
+    import numpy as np
+    lib = _lib.load()
+    t = np.zeros((4, 1024), np.float32)
+    off = np.array([0, 1, 2], np.int64)
+    idx = np.zeros(2, np.int32)
+    sc = np.zeros(2, np.float32)
+    inv = np.ones(4, np.float32)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    rc = lib.nr_pool_score(_lib.NR_POOL_LATENT, _lib.NR_F32, 1024, P(t), 1024, P(t), 1024, P(inv), P(idx), P(off),
+                           P(idx), P(off), 2, P(sc), None, None)
+    assert rc == -1 and b"`hist_table`" in lib.nr_last_error() and b"not device memory" in lib.nr_last_error()
+    rc = lib.nr_gemm(_lib.NR_F32, _lib.NR_F32, 0, 4, 128, 32, P(t), 1024, P(t), 1024, None, None, 0, P(t), 1024, None)
+    assert rc == -1 and b"`A`" in lib.nr_last_error()

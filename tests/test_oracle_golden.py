@@ -96,3 +96,45 @@ def test_token_attn_oracle_matches_reference():
     states = torch.split(torch.from_numpy(g["db_states"]), list(g["db_lens"]))
     got = token_ref.apply_token_attn(sd, states)
     np.testing.assert_allclose(got.numpy(), g["db_out"], rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("pooler", ["final", "latent"])
+@pytest.mark.parametrize("fast", [True, False])
+def test_large_oracle_matches_reference(pooler, fast, monkeypatch):
+    """The full-size checker (per-news tables with K/V once, then the C / OpenMP
+    reductions of oracle/fastpool.c, or their chunked PyTorch restatement)
+    against the reference's own golden scores."""
+    g = golden(f"pool_{pooler}")
+    sd = (W.final_attention_state_dict(int(g["weight_seed"])) if pooler == "final"
+          else W.latent_attention_state_dict(int(g["weight_seed"]), ln_random=True))
+    table = W.news_table(1234, int(g["n_news"]), 1024, name=str(g["table_name"]))
+    if fast:
+        if pool_ref._fastpool() is None:
+            pytest.skip("oracle/libfastpool.so not built (run __graft_entry__.build())")
+    else:
+        monkeypatch.setattr(pool_ref, "_fastpool", lambda: None)
+    s = pool_ref.cos_sim_scores_large(pooler, sd, g["hist_idx"], g["hist_len"], g["cand_idx"], g["cand_len"], table,
+                                      chunk_imps=7)
+    np.testing.assert_allclose(s, g["scores"], rtol=0, atol=2e-6)
+    if pooler == "latent":
+        rows = torch.tensor(g["unpooled_in_rows"])
+        with torch.no_grad():
+            out = pool_ref.latent_hiddens_kv_once(sd, table[rows].reshape(-1, 1024))
+        np.testing.assert_allclose(out.numpy(), g["unpooled_out"].reshape(-1, 1024), rtol=0, atol=1e-5)
+
+
+def test_vectorised_auc_matches_sklearn_score():
+    """data_ref.impression_aucs (Mann-Whitney on raw scores, used for the
+    376 k-impression gate) equals score_row's sklearn AUC on 1/dense-rank for
+    every impression, including ties and single-class rows."""
+    rng = np.random.default_rng(7)
+    lens = rng.integers(2, 60, 400)
+    scores = np.round(rng.standard_normal(int(lens.sum())), 1).astype(np.float32)  # many ties
+    labels = (rng.random(int(lens.sum())) < 0.2).astype(np.int64)
+    off = np.concatenate([[0], np.cumsum(lens)])
+    labels[off[5]:off[6]] = 0  # a single-class impression -> nan
+    got = data_ref.impression_aucs(scores, labels, lens)
+    ranks = pool_ref.dense_ranks(scores, lens)
+    want = data_ref.score_per_row(ranks, unflat(labels, lens))[:, 0]
+    np.testing.assert_allclose(got, want, rtol=0, atol=1e-12, equal_nan=True)
+    assert np.isnan(got[5])
