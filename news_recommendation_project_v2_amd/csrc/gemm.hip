@@ -720,6 +720,27 @@ __device__ __forceinline__ uint4 swap_pair16(uint2 a, uint2 b) {
   return uint4{sx[0], sy[0], sx[1], sy[1]};
 }
 
+// The 32x32 counterpart (guide T21): a swapped-operand 32x32 accumulator
+// leaves lane l with row l & 31, columns 8 g + 4 (l >> 5) .. +3 of group g;
+// for groups (2p, 2p + 1) packed as (a, b), one v_permlane32_swap per dword
+// gives lanes 0-31 columns 16 p .. +7 ([own a | upper's a]) and lanes 32-63
+// columns 16 p + 8 .. +15 ([lower's b | own b]).  Applied to a 16-B row segment
+// (a = its first 8 bytes, b = the last 8) it maps back to (group 2p, 2p + 1).
+__device__ __forceinline__ uint4 swap_pair32(uint2 a, uint2 b) {
+  const auto sx = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+  const auto sy = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+  return uint4{sx[0], sy[0], sx[1], sy[1]};
+}
+
+template <bool MF32>
+struct AccT {  // a wave's 128x64 accumulators: 8x4 tiles of 16x16, or 4x2 tiles of 32x32
+  typedef f32x4 type[8][4];
+};
+template <>
+struct AccT<true> {
+  typedef f32x16 type[4][2];
+};
+
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
@@ -743,7 +764,7 @@ constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78, kVmcnt11 = 0x0F7B;
 // its first K step while tile t's epilogue still reads slot t.
 constexpr int kLnSlot = 8 * 512 + 256 * 8;
 
-template <int EPI, bool LNF = false>
+template <int EPI, bool LNF = false, bool MF32 = false>
 __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, int64_t K,
                                                           const __bf16* __restrict__ A, int64_t lda,
                                                           const __bf16* __restrict__ W, int64_t ldw,
@@ -862,35 +883,66 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   const int bbase = G2BM * 128 + (wn * 64 + c16) * 128;
   const int cf0 = ((0 + q4) ^ sw) << 4, cf1 = ((4 + q4) ^ sw) << 4;
   typedef f32x4 frag_t;
-  frag_t fa[4][2], fb0[2][2], fb1[2][2];
-  f32x4 acc[8][4];
+  // MF32 (v_mfma_f32_32x32x16_bf16): operand map row lane & 31, 16-B k chunk
+  // 2 s + lane / 32 of the 16-deep k slice s; a quadrant is 2 row tiles x 1 col tile
+  const int r32 = lane & 31, h32 = lane >> 5;
+  const int sw32 = (r32 >> 1) & 7;
+  const int abase32 = (wm * 128 + r32) * 128, bbase32 = G2BM * 128 + (wn * 64 + r32) * 128;
+  frag_t fa[4][2], fb0[2][2], fb1[2][2];  // 16x16x32: [row tile][k half]; 32x32x16: fa[i][s] = [2 x 4], fb[s >> 1][s & 1]
+  typename AccT<MF32>::type acc;
   auto readA = [&](int stage, int qm) {
-    const unsigned char* sp = smem + stage * G2_STAGE + abase + qm * 4 * 2048;
+    if constexpr (MF32) {
+      const unsigned char* sp = smem + stage * G2_STAGE + abase32 + qm * 64 * 128;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      fa[i][0] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf0);
-      fa[i][1] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf1);
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          fa[2 * i + (s4 >> 1)][s4 & 1] =
+              *reinterpret_cast<const frag_t*>(sp + i * 32 * 128 + (((2 * s4 + h32) ^ sw32) << 4));
+    } else {
+      const unsigned char* sp = smem + stage * G2_STAGE + abase + qm * 4 * 2048;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fa[i][0] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf0);
+        fa[i][1] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf1);
+      }
     }
   };
   auto readB = [&](int stage, int qn, frag_t (&fb)[2][2]) {
-    const unsigned char* sp = smem + stage * G2_STAGE + bbase + qn * 2 * 2048;
+    if constexpr (MF32) {
+      const unsigned char* sp = smem + stage * G2_STAGE + bbase32 + qn * 32 * 128;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      fb[j][0] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf0);
-      fb[j][1] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf1);
+      for (int s4 = 0; s4 < 4; ++s4) fb[s4 >> 1][s4 & 1] = *reinterpret_cast<const frag_t*>(sp + (((2 * s4 + h32) ^ sw32) << 4));
+    } else {
+      const unsigned char* sp = smem + stage * G2_STAGE + bbase + qn * 2 * 2048;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        fb[j][0] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf0);
+        fb[j][1] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf1);
+      }
     }
   };
   // swapped operands: D[n][m] = sum_k W[n][k] A[m][k] = C[m][n]
   auto mma = [&](int qm, int qn, const frag_t (&fb)[2][2]) {
+    if constexpr (MF32) {
 #pragma unroll
-    for (int f = 0; f < 2; ++f)
+      for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 2; ++i)
+          acc[2 * qm + i][qn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              __builtin_bit_cast(bf16x8, fb[s4 >> 1][s4 & 1]), __builtin_bit_cast(bf16x8, fa[2 * i + (s4 >> 1)][s4 & 1]),
+              acc[2 * qm + i][qn], 0, 0, 0);
+    } else {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 * qm + i][2 * qn + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8, fb[j][f]), __builtin_bit_cast(bf16x8, fa[i][f]), acc[4 * qm + i][2 * qn + j],
-              0, 0, 0);
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[4 * qm + i][2 * qn + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, fb[j][f]), __builtin_bit_cast(bf16x8, fa[i][f]), acc[4 * qm + i][2 * qn + j],
+                0, 0, 0);
+    }
   };
 #define NR_PHASE_SYNC_MMA(QM, NI, FB)                   \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
@@ -973,7 +1025,23 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     if (more) tile_base(tn, nm0, nn0);
     // the accumulators start at the bias (acc = bias + A.W^T); this wave's
     // columns wn*64 + 16 ni + 4 q4 .. +3
-    {
+    if constexpr (MF32) {
+      // lane's columns of tile ni: 32 ni + 8 g + 4 h32 + (reg & 3), g = reg >> 2
+      f32x16 b16[2];
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 b4 = bias ? *reinterpret_cast<const f32x4*>(bias_lds + (32 * ni + 8 * g + 4 * h32) * 4)
+                                : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) b16[ni][4 * g + r] = b4[r];
+        }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = b16[ni];
+    } else {
       f32x4 b4[4];
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni)
@@ -996,6 +1064,142 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     // not store: with an in-place residual (R == C, the latent ff2) another
     // wave group's duplicate store of row M - 1 could land before this
     // group's residual load of it and add the residual twice.
+    if constexpr (MF32) {
+    // 32x32 accumulators: lane l holds row r32 of row tile mi, columns
+    // 32 ni + 8 g + 4 h32 + r (g = reg >> 2, r = reg & 3); after swap_pair32 of
+    // groups (2p, 2p + 1) the lane stores columns 32 ni + 16 p + 8 h32 .. +7
+    const int64_t row0 = (int64_t)m0 + wm * 128 + r32;  // + 32 mi
+    const int64_t col0 = (int64_t)n0 + wn * 64;
+    const int so = 8 * h32;  // lane's 8 store columns within a 16-column pair
+    f32x16 lu[2], lc[2];
+    const unsigned char* ln_st = ln_lds + lslot * kLnSlot + 8 * 512;
+    if constexpr (LNF) {
+      const unsigned char* uc = ln_lds + lslot * kLnSlot + wave * 512;
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 u4 = *reinterpret_cast<const f32x4*>(uc + (32 * ni + 8 * g + 4 * h32) * 4);
+          const f32x4 c4 = *reinterpret_cast<const f32x4*>(uc + 256 + (32 * ni + 8 * g + 4 * h32) * 4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            lu[ni][4 * g + r] = u4[r];
+            lc[ni][4 * g + r] = c4[r];
+          }
+        }
+    }
+    uint4 rq[4][2][2];
+    if constexpr (EPI == NR_EPI_RESADD) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int64_t row = min(row0 + 32 * mi, M - 1);
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp)
+            rq[mi][ni][pp] = *reinterpret_cast<const uint4*>(R + row * ldr + col0 + 32 * ni + 16 * pp + so);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int64_t row = min(row0 + 32 * mi, M - 1);
+      const bool live = row0 + 32 * mi < M;
+      if constexpr (LNF) {
+        const float2 ms = *reinterpret_cast<const float2*>(ln_st + (wm * 128 + r32 + 32 * mi) * 8);
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[mi][ni][r] = fmaf(ms.y, fmaf(-ms.x, lu[ni][r], acc[mi][ni][r]), lc[ni][r]);
+      }
+      if constexpr (EPI == NR_EPI_GEGLU) {
+        // W rows interleaved in 32-row (a, g) blocks: tile 0 = a, tile 1 = g
+        uint2 pk[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = acc[mi][0][4 * g + r] * gelu_erf(acc[mi][1][4 * g + r]);
+          pk[g] = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+        }
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          const uint4 v = swap_pair32(pk[2 * pp], pk[2 * pp + 1]);
+          if (live) *reinterpret_cast<uint4*>(C + row * ldc + col0 / 2 + 16 * pp + so) = v;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        if constexpr (EPI == NR_EPI_RESADD) {
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+              const uint4 q = swap_pair32(uint2{rq[mi][ni][pp].x, rq[mi][ni][pp].y}, uint2{rq[mi][ni][pp].z, rq[mi][ni][pp].w});
+              const uint32_t w[2][2] = {{q.x, q.y}, {q.z, q.w}};  // groups 2pp, 2pp + 1
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const uint32_t u = w[h][r >> 1];
+                  acc[mi][ni][4 * (2 * pp + h) + r] += (r & 1) ? bf16_hi(u) : bf16_lo(u);
+                }
+            }
+        }
+        float v[2][16];
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float x = acc[mi][ni][r];
+            if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
+              const uint64_t gi = (uint64_t)(row * N + col0 + 32 * ni + 8 * (r >> 2) + 4 * h32 + (r & 3));
+              x = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(x, 0.f) * ea.scale;
+            }
+            if constexpr (EPI == NR_EPI_EXP) x = expf(x);
+            if constexpr (EPI == NR_EPI_GELU) x = gelu_erf(x);
+            v[ni][r] = x;
+          }
+        if constexpr (EPI == NR_EPI_SOFTMAX64) {
+          // the wave's 64 columns are one softmax group: row r32's values sit in lanes l and l ^ 32
+          float mx = v[0][0];
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, v[ni][r]);
+          mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+          float sum = 0.f;
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              v[ni][r] = expf(v[ni][r] - mx);
+              sum += v[ni][r];
+            }
+          sum += __shfl_xor(sum, 32, 64);
+          const float inv = 1.0f / sum;
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[ni][r] *= inv;
+        }
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          uint2 pk[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            pk[g] = uint2{pack_bf16x2(v[ni][4 * g], v[ni][4 * g + 1]), pack_bf16x2(v[ni][4 * g + 2], v[ni][4 * g + 3])};
+            if constexpr (EPI == NR_EPI_RELU) pk[g] = uint2{relu_bf16x2(pk[g].x), relu_bf16x2(pk[g].y)};
+          }
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp) {
+            const uint4 q = swap_pair32(pk[2 * pp], pk[2 * pp + 1]);
+            if (live) *reinterpret_cast<uint4*>(C + row * ldc + col0 + 32 * ni + 16 * pp + so) = q;
+          }
+        }
+        if constexpr (EPI == NR_EPI_RESADD) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    } else {
     const int64_t row0 = (int64_t)m0 + wm * 128 + c16;  // + 16 mi
     const int64_t col0 = (int64_t)n0 + wn * 64;          // this wave's 64 columns
     const int qo = 16 * (q4 & 1) + 8 * (q4 >> 1);        // lane's 8 columns after swap_pair16
@@ -1118,6 +1322,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
         }
         if constexpr (EPI == NR_EPI_RESADD) __builtin_amdgcn_sched_barrier(0);  // row groups in load order
       }
+    }
     }
     if (!more) break;
     if (wmu == 1) __builtin_amdgcn_s_barrier();  // re-skew

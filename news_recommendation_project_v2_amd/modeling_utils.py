@@ -74,13 +74,85 @@ def pool_rows(pooler: str, table: torch.Tensor, hist_off: torch.Tensor) -> torch
     return ops.pool_rows(pooler, table, hist_off)
 
 
+def _pad64(n: int) -> int:
+    return max(64, (n + 63) // 64 * 64)
+
+
+class _FinalAttentionFn(torch.autograd.Function):
+    """FinalAttention forward + backward on the HIP kernels, over the packed valid
+    history rows (CSR ``off``), so the reference module trains through autograd
+    (trainer.py:1046-1063: ``model.train()``, forward, ``loss.backward()``).
+
+    Forward (modeling_utils.py:218-228, f32, exact-f32 MFMA): rows padded with
+    zeros to a multiple of 64 (the weight-grad GEMMs' K), then
+      X1 = drop1(relu(S W1ᵀ + b1)); X2 = drop2(relu(X1 W2ᵀ + b2)); X = X2 W3ᵀ + b3
+      Y = drop3(relu(X W4ᵀ + b4)); P = exp(Y W5ᵀ); users = Σ x p / (Σ p + 1e-10)
+    with dropout fused into the ReLU epilogues (nr_gemm_relu_dropout: the
+    counter-hash stream keyed by (seed, packed row, column), the same draw
+    oracle/train_ref.py restates; p = 0 in eval).  Backward: nr_final_pool_bwd,
+    data-grad GEMMs through transposed weights with the relu/dropout backward
+    fused (nr_gemm_drelu), weight grads dOutᵀ · X as one grouped launch, bias
+    grads by column sums; the padding rows carry zero gradient."""
+
+    @staticmethod
+    def forward(ctx, rows, off, ps, seeds, W1, b1, W2, b2, W3, b3, W4, b4, W5):
+        Hs, D = rows.shape
+        H = W1.shape[0]
+        Hp = _pad64(Hs)
+        dev = rows.device
+        S = torch.zeros((Hp, D), dtype=torch.float32, device=dev)
+        S[:Hs] = rows
+        X1 = ops.gemm_relu_dropout(S, W1.contiguous(), b1.contiguous(), seeds[0], ps[0])
+        X2 = ops.gemm_relu_dropout(X1, W2.contiguous(), b2.contiguous(), seeds[1], ps[1])
+        XP = torch.empty((Hp, 2 * D), dtype=torch.float32, device=dev)
+        X = XP[:, :D]
+        ops.gemm(X2, W3.contiguous(), b3.contiguous(), out=X)
+        Y = ops.gemm_relu_dropout(X, W4.contiguous(), b4.contiguous(), seeds[2], ps[2])
+        ops.gemm(Y, W5.contiguous(), None, epilogue="exp", out=XP[:, D:])
+        users, z = ops.final_pool_fwd(XP, off)
+        ctx.save_for_backward(S, X1, X2, XP, Y, users, z, off, W1, W2, W3, W4, W5)
+        ctx.ps, ctx.Hs = ps, Hs
+        return users
+
+    @staticmethod
+    def backward(ctx, du):
+        S, X1, X2, XP, Y, users, z, off, W1, W2, W3, W4, W5 = ctx.saved_tensors
+        ps, Hs = ctx.ps, ctx.Hs
+        Hp, D = S.shape
+        du = du.float().contiguous()
+        dXp = torch.empty((Hp, D), dtype=torch.float32, device=S.device)
+        dL = torch.empty_like(dXp)
+        ops.final_pool_bwd(XP, off, users, z, du, dXp, dL)
+        X = XP[:, :D]
+        T = ops.transpose
+        dY = ops.gemm_drelu(dL, T(W5.contiguous()), Y, 1.0 / (1.0 - ps[2]))
+        dX = ops.gemm(dY, T(W4.contiguous()), None, epilogue="resadd", residual=dXp)
+        dZ2 = ops.gemm_drelu(dX, T(W3.contiguous()), X2, 1.0 / (1.0 - ps[1]))
+        dZ1 = ops.gemm_drelu(dZ2, T(W2.contiguous()), X1, 1.0 / (1.0 - ps[0]))
+        dS = ops.gemm(dZ1, T(W1.contiguous()), None)
+        gW = [torch.empty_like(w, dtype=torch.float32) for w in (W1, W2, W3, W4, W5)]
+        ops.gemm_grouped([(T(g_out), T(x_in), gw) for g_out, x_in, gw in
+                          ((dZ1, S, gW[0]), (dZ2, X1, gW[1]), (dX, X2, gW[2]), (dY, X, gW[3]), (dL, Y, gW[4]))])
+        gb = []
+        for g_out in (dZ1, dZ2, dX, dY):
+            b = torch.zeros(g_out.shape[1], dtype=torch.float32, device=S.device)
+            ops.col_sum(g_out, b)
+            gb.append(b)
+        return (dS[:Hs], None, None, None, gW[0], gb[0], gW[1], gb[1], gW[2], gb[2], gW[3], gb[3], gW[4])
+
+
 class FinalAttention(torch.nn.Module):
     """Additive per-dimension attention pooler (modeling_utils.py:175-228).
 
     forward(emb [B, L, D], mask [B, L]) -> [B, D]:
       x = W3 relu(W2 relu(W1 e + b1) + b2) + b3 ;  w = W5 relu(W4 x + b4)
       out = sum_L x * exp(w) * m / (sum_L exp(w) * m + 1e-10)
-    Dropouts (p=0.1) exist for state/API parity and are inactive in eval.
+    In eval under no_grad: the per-item table once per valid row + the pooling
+    kernel.  When autograd is recording (train mode, or any input / parameter
+    requiring grad), ``_FinalAttentionFn``: the same math with the backward
+    wired to the HIP kernels; in train mode the dropouts (p = 0.1, their
+    modules' ``p``) are active, drawn from the counter-hash stream with seeds
+    taken from torch's default generator (torch.manual_seed reproduces them).
     """
 
     def __init__(self, reduced_dim: int, hidden_dim: int):
@@ -124,9 +196,16 @@ class FinalAttention(torch.nn.Module):
     def forward(self, embeddings: torch.Tensor, attention_mask: torch.Tensor) -> torch.Tensor:
         if embeddings.device.type != "cuda":
             raise NewsRecHIPError("FinalAttention.forward runs on the MI355X HIP path only (got a CPU tensor)")
-        if self.training:
-            raise NewsRecHIPError("FinalAttention HIP forward is inference-only (dropout inactive); call .eval()")
         rows, off = flatten_valid(embeddings, attention_mask)
+        params = [self.linear1.weight, self.linear1.bias, self.linear2.weight, self.linear2.bias, self.linear3.weight,
+                  self.linear3.bias, self.linear4.weight, self.linear4.bias, self.linear5.weight]
+        if self.training or (torch.is_grad_enabled() and (rows.requires_grad or any(p.requires_grad for p in params))):
+            if any(p.dtype != torch.float32 for p in params):
+                raise NewsRecHIPError("FinalAttention autograd path trains f32 parameters (as the reference does)")
+            drops = (self.dropout1, self.dropout2, self.dropout3)
+            ps = tuple(float(d.p) if self.training else 0.0 for d in drops)
+            seeds = tuple(int(s) for s in torch.randint(0, 2**62, (3,)).tolist()) if self.training else (0, 0, 0)
+            return _FinalAttentionFn.apply(rows.float(), off, ps, seeds, *params)
         table = self.item_table(rows.float())
         return pool_rows("final", table, off)
 

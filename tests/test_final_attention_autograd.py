@@ -1,0 +1,120 @@
+"""FinalAttention trains through the reference's own module API:
+``model.train()``, forward on padded embeddings + mask, ``loss.backward()``,
+a torch optimizer step -- the calls trainer.py:1046-1069 makes -- with the
+forward and backward on the HIP kernels (modeling_utils._FinalAttentionFn).
+Gradients are checked against torch autograd of the oracle's restatement of
+modeling_utils.py:195-228 (oracle/train_ref.final_attention_train: train mode,
+dropout drawn from the same counter-hash stream), with the tolerances of
+tests/test_train.py (each gradient within 1e-3 of its tensor's max)."""
+import numpy as np
+import pytest
+import torch
+
+from news_recommendation_project_v2_amd import weights as W
+from news_recommendation_project_v2_amd.modeling_utils import FinalAttention
+from oracle import train_ref
+
+
+def _batch(seed=0, B=6, L=11, D=1024):
+    rng = np.random.default_rng(seed)
+    lens = np.array([11, 3, 1, 7, 0, 5])[:B]
+    mask = np.zeros((B, L), dtype=np.int64)
+    for b, n in enumerate(lens):
+        mask[b, :n] = 1
+    emb = rng.standard_normal((B, L, D)).astype(np.float32) * mask[..., None]
+    slot_rows = -np.ones((B, L), dtype=np.int64)
+    r = 0
+    for b, n in enumerate(lens):
+        slot_rows[b, :n] = np.arange(r, r + n)
+        r += n
+    return torch.from_numpy(emb), torch.from_numpy(mask), slot_rows
+
+
+def _rel_close(got, want, name, tol=1e-3):
+    got, want = got.detach().cpu().float(), want.detach().cpu().float()
+    scale = float(want.abs().max()) or 1.0
+    err = float((got - want).abs().max())
+    assert err <= tol * scale, f"{name}: max |d| {err:.3e} vs max |ref| {scale:.3e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_final_attention_backward_matches_oracle(gpu_device, p):
+    sd = W.final_attention_state_dict(1234)
+    m = FinalAttention(1024, 4096)
+    m.load_state_dict(sd)
+    for d in (m.dropout1, m.dropout2, m.dropout3):
+        d.p = p
+    m = m.to(gpu_device).train()
+    emb, mask, slot_rows = _batch()
+    R = torch.randn(emb.shape[0], 1024, generator=torch.Generator().manual_seed(3))
+    e_d = emb.to(gpu_device).requires_grad_(True)
+    torch.manual_seed(77)
+    out = m(e_d, mask.to(gpu_device))
+    (out * R.to(gpu_device)).sum().backward()
+    torch.manual_seed(77)  # the module draws its three dropout seeds from torch's default generator
+    seeds = [int(s) for s in torch.randint(0, 2**62, (3,)).tolist()]
+
+    ref_sd = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    e_c = emb.clone().requires_grad_(True)
+    want = train_ref.final_attention_train(ref_sd, e_c, mask, seeds, p, slot_rows)
+    (want * R).sum().backward()
+
+    _rel_close(out, want, "users", tol=1e-4)
+    _rel_close(e_d.grad, e_c.grad, "d embeddings")
+    for name, prm in m.named_parameters():
+        _rel_close(prm.grad, ref_sd[name].grad, f"d {name}")
+    if p > 0:  # the dropout is live: a different draw changes the output
+        torch.manual_seed(78)
+        again = m(e_d, mask.to(gpu_device))
+        assert float((again - out).abs().max()) > 1e-3
+
+
+@pytest.mark.gpu
+def test_reference_training_loop_through_the_module(gpu_device):
+    """trainer.py:1046-1069 as written against the module: train(), forward,
+    cosine + MarginRankingLoss(2), backward, clip_grad_norm_(0.5), AdamW(lr 1e-6,
+    wd 0.01) step -- parameters after the step equal the oracle's (dropout p = 0)."""
+    import torch.nn.functional as F
+    sd = W.final_attention_state_dict(1234)
+    m = FinalAttention(1024, 4096)
+    m.load_state_dict(sd)
+    for d in (m.dropout1, m.dropout2, m.dropout3):
+        d.p = 0.0
+    m = m.to(gpu_device).train()
+    emb, mask, slot_rows = _batch(1)
+    g = torch.Generator().manual_seed(5)
+    pos, neg = torch.randn(6, 1024, generator=g), torch.randn(6, 1024, generator=g)
+
+    def step(model, e, msk, P, N, params):
+        before = [q.detach().clone() for q in params]
+        out = model(e, msk)
+        res = F.cosine_similarity(out.repeat(2, 1), torch.cat([P, N]))
+        loss = torch.nn.MarginRankingLoss(2)(res[:6], res[6:], torch.ones(6, device=res.device))
+        opt = torch.optim.AdamW(params, lr=1e-6, weight_decay=0.01)
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, 0.5)
+        opt.step()
+        upd = [(q.detach() - b).cpu() for q, b in zip(params, before)]
+        return float(loss), [q.grad.detach().cpu() for q in params], upd
+
+    names = [n for n, _ in m.named_parameters()]
+    loss_gpu, g_gpu, u_gpu = step(m, emb.to(gpu_device), mask.to(gpu_device), pos.to(gpu_device),
+                                  neg.to(gpu_device), list(m.parameters()))
+    ref_sd = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+
+    def ref_model(e, msk):
+        return train_ref.final_attention_train(ref_sd, e, msk, (0, 0, 0), 0.0, slot_rows)
+
+    loss_ref, g_ref, u_ref = step(ref_model, emb, mask, pos, neg, [ref_sd[n] for n in names])
+    assert abs(loss_gpu - loss_ref) <= 1e-5 * max(1.0, abs(loss_ref))
+    for name, a, b, ua, ub in zip(names, g_gpu, g_ref, u_gpu, u_ref):
+        _rel_close(a, b, f"clipped d {name}")
+        # AdamW's first step moves each element by lr * g / (|g| + eps) (+ decay): +-lr
+        # wherever |g| >> eps, so the updates agree to ~1e-8 wherever the gradient's
+        # sign is settled (|g| well above the 1e-3 * max gradient tolerance)
+        thr = max(1e-2 * float(b.abs().max()), 1e-6)
+        sure = (a.abs() > thr) & (b.abs() > thr)
+        assert int(sure.sum()) > 0, name
+        np.testing.assert_allclose(ua[sure].numpy(), ub[sure].numpy(), rtol=0, atol=2e-8, err_msg=name)

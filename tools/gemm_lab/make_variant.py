@@ -95,6 +95,14 @@ VARIANTS = {
     "gm2": [("constexpr int kGemmGroupM = 4;", "constexpr int kGemmGroupM = 2;")],
     "gm8": [("constexpr int kGemmGroupM = 4;", "constexpr int kGemmGroupM = 8;")],
     "gm16": [("constexpr int kGemmGroupM = 4;", "constexpr int kGemmGroupM = 16;")],
+    # the persistent kernel's main loop and epilogue on v_mfma_f32_32x32x16_bf16 (MF32)
+    "mf32": [
+        ("hipLaunchKernelGGL((gemm256t_kernel<E>), grid,", "hipLaunchKernelGGL((gemm256t_kernel<E, false, true>), grid,"),
+        ("hipLaunchKernelGGL((gemm256t_kernel<NR_EPI_GEGLU, true>), grid,",
+         "hipLaunchKernelGGL((gemm256t_kernel<NR_EPI_GEGLU, true, true>), grid,"),
+        ("hipLaunchKernelGGL((gemm256t_kernel<NR_EPI_SOFTMAX64, true>), grid,",
+         "hipLaunchKernelGGL((gemm256t_kernel<NR_EPI_SOFTMAX64, true, true>), grid,"),
+    ],
     # no s_setprio around the MFMA phases
     "noprio": [
         ("  __builtin_amdgcn_s_setprio(1);                       \\\n  mma(QM, NI, FB);                                     \\\n"
