@@ -1334,6 +1334,418 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
 #undef NR_PHASE_SYNC_MMA
 }
 
+// ---------------------------------------------------------------------------
+// 4-wave persistent variant: the same 256x256 block tile, LDS stage images,
+// swizzled LDS-DMA and cross-tile operand stream as gemm256t_kernel, but 4
+// waves (one per SIMD) of 128x128 each on v_mfma_f32_32x32x16_bf16 (4 x 4
+// accumulators of 32x32 = 256 accumulator registers, AGPR-resident).  Per K
+// step a wave reads 32 KiB of fragments (the whole workgroup 128 KiB instead of
+// the 8-wave layout's 192 KiB) and issues 64 MFMAs of 32 cycles, whose 24
+// free issue cycles each hold the ds_reads and DMAs of a single wave.  Phases
+// (row tile i of the wave's 128 rows, all four column tiles, K = 64):
+//   P0: read B (16 frags) + A tiles 0, 1; barrier; DMA B of step k+2; MMA tile 0
+//   P1: read A tile 2;                     DMA A rows of tiles 0, 1; MMA tile 1
+//   P2: read A tile 3;                                               MMA tile 2
+//   P3: barrier; DMA A rows of tiles 2, 3; MMA tile 3; vmcnt (step k+1 landed); barrier
+// Stage st is refilled for step k + 2 once every wave has read the region (the
+// barriers in P0 / P3 follow lgkmcnt(0)), and read again only after the vmcnt
+// + barrier that ends step k + 1.
+template <int EPI, bool LNF = false>
+__global__ __launch_bounds__(256, 1) void gemm256w4_kernel(int64_t M, int64_t N, int64_t K,
+                                                           const __bf16* __restrict__ A, int64_t lda,
+                                                           const __bf16* __restrict__ W, int64_t ldw,
+                                                           const float* __restrict__ bias, const __bf16* R,
+                                                           int64_t ldr, __bf16* C, int64_t ldc, EpiArgs ea, int ntn,
+                                                           int ntm, int n_tiles) {
+  constexpr int BK = 64;
+  // stages + 2 bias slots (tile parity; 4 waves x 128 floats) + LNF slots (u, c: 4 x 2 x 512 B; stats 256 x 8 B)
+  constexpr int kLn4 = 4 * 1024 + 256 * 8;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE + 2 * 4 * 512 + (LNF ? 2 * kLn4 : 0)];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nk = (int)(K / BK);  // >= 2 (host)
+
+  const int G = (int)gridDim.x;
+  int t, t_end, t_step;
+  if (G % 8 == 0) {
+    const int x = (int)blockIdx.x & 7, li = (int)blockIdx.x >> 3;
+    const int qq = n_tiles >> 3, rr = n_tiles & 7;
+    const int lo = x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq;
+    t = lo + li;
+    t_end = lo + qq + (x < rr ? 1 : 0);
+    t_step = G >> 3;
+  } else {
+    t = (int)blockIdx.x;
+    t_end = n_tiles;
+    t_step = G;
+  }
+  if (t >= t_end) return;
+  auto tile_base = [&](int tile, uint32_t& mb, uint32_t& nb) {
+    int mt, nt;
+    tile_of(tile, ntn, ntm, ea.group_m, mt, nt);
+    mb = (uint32_t)mt * G2BM;
+    nb = (uint32_t)nt * G2BN;
+  };
+  auto rsrc = [](const void* p, int64_t bytes) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    const int n = __builtin_amdgcn_readfirstlane((int)(bytes > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)bytes));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rA = rsrc(A, M * lda * 2), rW = rsrc(W, N * ldw * 2);
+  // output / residual through buffer descriptors (host: < 4 GiB each): one 32-bit
+  // offset per row tile, the column steps in the instruction's immediate offset
+  const int64_t ccols = EPI == NR_EPI_GEGLU ? N / 2 : N;
+  const __amdgpu_buffer_rsrc_t rC = rsrc(C, ((M - 1) * ldc + ccols) * 2);
+  const __amdgpu_buffer_rsrc_t rR = rsrc(R, EPI == NR_EPI_RESADD ? ((M - 1) * ldr + N) * 2 : 0);
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  // DMA units.  A unit i = rows 32 i .. +31 of both 128-row halves: wave w owns
+  // rows 128 (w >> 1) + 32 i + 16 (w & 1) + 8 j + l / 8 (j = 0, 1).  B: wave w
+  // owns rows 64 w + 8 j + l / 8 (j = 0..7).  16-B chunk (l & 7) ^ ((row >> 1) & 7).
+  const uint32_t ldab = (uint32_t)lda * 2, ldwb = (uint32_t)ldw * 2, mlast = (uint32_t)(M - 1);
+  auto chunk = [&](int j) { return (uint32_t)(((lane & 7) ^ ((4 * j + (lane >> 4)) & 7)) * 16); };
+  const int qa = (wave >> 1) * 128 + (wave & 1) * 16;
+  // Per-lane DMA offsets: one base per chunk parity, the row steps (8 j, 32 i)
+  // ride in the scalar offset with the K offset (4 VGPRs instead of 16).  B rows
+  // never pass N; A rows past M (last M-tile only) are clamped to M - 1 per lane.
+  uint32_t oA[2], oB[2], amb = 0;
+  bool afull = true;
+  auto set_offA = [&](uint32_t mb) {
+    amb = mb;
+    afull = mb + (uint32_t)G2BM <= (uint32_t)M;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) oA[j] = (mb + (uint32_t)(qa + (lane >> 3))) * ldab + chunk(j);
+  };
+  auto set_offB = [&](uint32_t nb) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) oB[j] = (nb + (uint32_t)(64 * wave + (lane >> 3))) * ldwb + chunk(j);
+  };
+  auto dmaA = [&](int i, int stage, int kt) {
+    unsigned char* sa = smem + stage * G2_STAGE + (qa + 32 * i) * 128;
+    if (afull) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sa + 8 * j * 128), 16, oA[j],
+                                                 kt * (BK * 2) + (32 * i + 8 * j) * ldab, 0, 0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t o = min(amb + (uint32_t)(qa + 32 * i + 8 * j + (lane >> 3)), mlast) * ldab + chunk(j);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sa + 8 * j * 128), 16, o, kt * (BK * 2), 0, 0);
+      }
+    }
+  };
+  auto dmaB = [&](int stage, int kt) {
+    unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128 + 64 * wave * 128;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(sb + 8 * j * 128), 16, oB[j & 1],
+                                               kt * (BK * 2) + 8 * j * ldwb, 0, 0);
+  };
+  // this wave's 128 bias floats, slot = tile parity (the next tile's bias lands
+  // while this tile's epilogue still reads its own; added in the epilogue, so the
+  // accumulators start at zero)
+  unsigned char* bias_lds = smem + 2 * G2_STAGE + wave * 512;
+  const __amdgpu_buffer_rsrc_t rBias = rsrc(bias, N * 4);
+  auto dma_bias = [&](int slot, uint32_t nb) {
+    if (bias)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rBias, (lds_void*)(bias_lds + slot * 2048 + 256 * h), 4,
+                                                 (nb + (uint32_t)(wn * 128 + 64 * h + lane)) * 4, 0, 0, 0);
+  };
+  unsigned char* ln_lds = smem + 2 * G2_STAGE + 2 * 4 * 512;
+  const __amdgpu_buffer_rsrc_t rUC = rsrc(ea.ln_uc, LNF ? 2 * N * 4 : 0);
+  const __amdgpu_buffer_rsrc_t rST = rsrc(ea.ln_stats, LNF ? M * 8 : 0);
+  constexpr int kLnDma = 6;
+  auto dma_ln = [&](int slot, uint32_t mb, uint32_t nb) {
+    if constexpr (LNF) {
+      unsigned char* base = ln_lds + slot * kLn4;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t cu = (nb + (uint32_t)(wn * 128 + 64 * h + lane)) * 4;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rUC, (lds_void*)(base + wave * 1024 + 256 * h), 4, cu, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rUC, (lds_void*)(base + wave * 1024 + 512 + 256 * h), 4,
+                                                 cu + (uint32_t)N * 4, 0, 0, 0);
+        const uint32_t row = min(mb + (uint32_t)(64 * wave + 32 * h + (lane >> 1)), mlast);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rST, (lds_void*)(base + 4 * 1024 + wave * 512 + 256 * h), 4,
+                                                 row * 8 + (uint32_t)(lane & 1) * 4, 0, 0, 0);
+      }
+    }
+  };
+  int lslot = 0;
+
+  // 32x32x16 fragments: row lane & 31, 16-B chunk 2 s + lane / 32 of k slice s
+  const int r32 = lane & 31, h32 = lane >> 5;
+  const int sw32 = (r32 >> 1) & 7;
+  int cs[4];
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) cs[s4] = ((2 * s4 + h32) ^ sw32) << 4;
+  const int abase = (wm * 128 + r32) * 128, bbase = G2BM * 128 + (wn * 128 + r32) * 128;
+  typedef f32x4 frag_t;
+  frag_t fa0[4], fa1[4], fb[4][4];
+  f32x16 acc[4][4];
+  auto readA = [&](int stage, int i, frag_t (&fa)[4]) {
+    const unsigned char* sp = smem + stage * G2_STAGE + abase + i * 32 * 128;
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) fa[s4] = *reinterpret_cast<const frag_t*>(sp + cs[s4]);
+  };
+  auto readB = [&](int stage) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned char* sp = smem + stage * G2_STAGE + bbase + j * 32 * 128;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) fb[j][s4] = *reinterpret_cast<const frag_t*>(sp + cs[s4]);
+    }
+  };
+  auto mma = [&](int i, const frag_t (&fa)[4]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fb[j][s4]),
+                                                            __builtin_bit_cast(bf16x8, fa[s4]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {
+    const bool pf = kt + 2 < nk || more;
+    const bool edge = kt + 2 >= nk;  // this step's DMAs fetch the next tile's step kt + 2 - nk
+    const int kf = edge ? kt + 2 - nk : kt + 2;
+    readB(st);
+    readA(st, 0, fa0);
+    readA(st, 1, fa1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    if (pf) {
+      if (kt + 2 == nk) {
+        set_offA(nm0);
+        set_offB(nn0);
+        dma_bias(lslot ^ 1, nn0);
+      }
+      dmaB(st, kf);
+    }
+    mma(0, fa0);
+    readA(st, 2, fa0);
+    if (pf) {
+      dmaA(0, st, kf);
+      dmaA(1, st, kf);
+    }
+    mma(1, fa1);
+    readA(st, 3, fa1);
+    mma(2, fa0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    if (pf) {
+      dmaA(2, st, kf);
+      dmaA(3, st, kf);
+      if (LNF && kt + 2 == nk) dma_ln(lslot ^ 1, nm0, nn0);
+    }
+    mma(3, fa1);
+    // step kt + 1 (issued during step kt - 1, or the prologue) has landed; this step's DMAs may fly
+    if (!pf) {
+      __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    } else if (kt + 2 == nk) {
+      // 16 operand DMAs + the bias (and LN) DMAs of the next tile are this step's
+      if (LNF) {
+        if (bias) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+      } else {
+        if (bias) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      }
+    } else {
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  uint32_t m0, n0;
+  tile_base(t, m0, n0);
+  set_offA(m0);
+  set_offB(n0);
+  dma_ln(0, m0, n0);
+  dma_bias(0, n0);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    dmaB(k, k);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dmaA(i, k, k);
+  }
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // step 0 (+ bias, LN) landed
+  __builtin_amdgcn_s_barrier();
+  int st = 0;
+  while (true) {
+    const int tn = t + t_step;
+    const bool more = tn < t_end;
+    uint32_t nm0 = 0, nn0 = 0;
+    if (more) tile_base(tn, nm0, nn0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    for (int kt = 0; kt < nk; ++kt) {
+      kstep(kt, st, more, nm0, nn0);
+      st ^= 1;
+    }
+    // pin the accumulators to AGPRs at the loop exit: the epilogue then reads
+    // them out one row tile at a time instead of copying all 256 to VGPRs
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[i][j]));
+    // ---------------- epilogue of tile (m0, n0): rows wm*128 + 32 i + r32, cols wn*128 + 32 j
+    // (tile coordinates made opaque here: otherwise the epilogue's addresses are
+    // hoisted into the K loop, where they hold ~100 VGPRs and force spills)
+    uint32_t em0 = m0, en0 = n0;
+    asm volatile("" : "+s"(em0), "+s"(en0));
+    const uint32_t row0 = em0 + (uint32_t)(wm * 128 + r32);
+    const uint32_t col0 = en0 + (uint32_t)(wn * 128);
+    const int so = 8 * h32;
+    const unsigned char* ln_base = ln_lds + lslot * kLn4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t row = min(row0 + (uint32_t)(32 * i), mlast);
+      const bool live = row0 + (uint32_t)(32 * i) < (uint32_t)M;
+      const uint32_t cof = (row * (uint32_t)ldc + (EPI == NR_EPI_GEGLU ? col0 / 2 : col0) + so) * 2;
+      // one row tile at a time (the scheduler would otherwise read all 256
+      // accumulators out up front and spill): a fence between row tiles
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 v[4];  // this row tile's values (the accumulators are only read)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = acc[i][j];
+      if (bias) {  // tile j's lane columns 32 j + 8 g + 4 h32 + (reg & 3)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias_lds + lslot * 2048 + (32 * j + 8 * g + 4 * h32) * 4);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[j][4 * g + r] += b4[r];
+          }
+      }
+      if constexpr (LNF) {
+        const float2 ms = *reinterpret_cast<const float2*>(ln_base + 4 * 1024 + (wm * 128 + r32 + 32 * i) * 8);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 u4 = *reinterpret_cast<const f32x4*>(ln_base + wave * 1024 + (32 * j + 8 * g + 4 * h32) * 4);
+            const f32x4 c4 = *reinterpret_cast<const f32x4*>(ln_base + wave * 1024 + 512 + (32 * j + 8 * g + 4 * h32) * 4);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              v[j][4 * g + r] = fmaf(ms.y, fmaf(-ms.x, u4[r], v[j][4 * g + r]), c4[r]);
+          }
+      }
+      if constexpr (EPI == NR_EPI_GEGLU) {
+        // W rows interleaved in 32-row (a, g) blocks: tiles (0, 1) and (2, 3) are (a, g) pairs
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          uint2 pk[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = v[2 * hh][4 * g + r] * gelu_erf(v[2 * hh + 1][4 * g + r]);
+            pk[g] = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
+          }
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp) {
+            const uint4 v = swap_pair32(pk[2 * pp], pk[2 * pp + 1]);
+            if (live)
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rC, cof + (32 * hh + 16 * pp) * 2, 0, 0);
+          }
+        }
+      } else {
+        if constexpr (EPI == NR_EPI_RESADD) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp) {
+              const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(
+                  rR, (row * (uint32_t)ldr + col0 + so) * 2 + (32 * j + 16 * pp) * 2, 0, 0);
+              const uint4 q = swap_pair32(uint2{rv.x, rv.y}, uint2{rv.z, rv.w});
+              const uint32_t w[2][2] = {{q.x, q.y}, {q.z, q.w}};
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const uint32_t u = w[h][r >> 1];
+                  v[j][4 * (2 * pp + h) + r] += (r & 1) ? bf16_hi(u) : bf16_lo(u);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            float x = v[j][r];
+            if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
+              const uint64_t gi = (uint64_t)row * N + col0 + 32 * j + 8 * (r >> 2) + 4 * h32 + (r & 3);
+              x = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(x, 0.f) * ea.scale;
+            }
+            if constexpr (EPI == NR_EPI_EXP) x = expf(x);
+            if constexpr (EPI == NR_EPI_GELU) x = gelu_erf(x);
+            v[j][r] = x;
+          }
+        if constexpr (EPI == NR_EPI_SOFTMAX64) {
+          // 64-column softmax groups = tile pairs (0, 1) and (2, 3); a row sits in lanes l and l ^ 32
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            float mx = v[2 * hh][0];
+#pragma unroll
+            for (int j = 2 * hh; j < 2 * hh + 2; ++j)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) mx = fmaxf(mx, v[j][r]);
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            float sum = 0.f;
+#pragma unroll
+            for (int j = 2 * hh; j < 2 * hh + 2; ++j)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                v[j][r] = expf(v[j][r] - mx);
+                sum += v[j][r];
+              }
+            sum += __shfl_xor(sum, 32, 64);
+            const float inv = 1.0f / sum;
+#pragma unroll
+            for (int j = 2 * hh; j < 2 * hh + 2; ++j)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) v[j][r] *= inv;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint2 pk[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            pk[g] = uint2{pack_bf16x2(v[j][4 * g], v[j][4 * g + 1]),
+                          pack_bf16x2(v[j][4 * g + 2], v[j][4 * g + 3])};
+            if constexpr (EPI == NR_EPI_RELU) pk[g] = uint2{relu_bf16x2(pk[g].x), relu_bf16x2(pk[g].y)};
+          }
+#pragma unroll
+          for (int pp = 0; pp < 2; ++pp) {
+            const uint4 q = swap_pair32(pk[2 * pp], pk[2 * pp + 1]);
+            if (live)
+              __builtin_amdgcn_raw_buffer_store_b128(u32x4{q.x, q.y, q.z, q.w}, rC, cof + (32 * j + 16 * pp) * 2, 0, 0);
+          }
+        }
+      }
+    }
+    if (!more) break;
+    lslot ^= 1;
+    t = tn;
+    m0 = nm0;
+    n0 = nn0;
+  }
+}
+
 // Workgroups of a persistent GEMM launch: the device's CU count rounded down
 // to a multiple of the 8 XCDs, unless the caller has set a budget for a
 // CU-masked stream (nr_set_persistent_workgroups).

@@ -103,6 +103,14 @@ VARIANTS = {
         ("hipLaunchKernelGGL((gemm256t_kernel<NR_EPI_SOFTMAX64, true>), grid,",
          "hipLaunchKernelGGL((gemm256t_kernel<NR_EPI_SOFTMAX64, true, true>), grid,"),
     ],
+    # 4 waves of 128x128 per 256x256 tile on 32x32x16 MFMAs (gemm256w4_kernel)
+    "w4": [
+        ("hipLaunchKernelGGL((gemm256t_kernel<E>), grid, dim3(512),", "hipLaunchKernelGGL((gemm256w4_kernel<E>), grid, dim3(256),"),
+        ("hipLaunchKernelGGL((gemm256t_kernel<NR_EPI_GEGLU, true>), grid, dim3(512),",
+         "hipLaunchKernelGGL((gemm256w4_kernel<NR_EPI_GEGLU, true>), grid, dim3(256),"),
+        ("hipLaunchKernelGGL((gemm256t_kernel<NR_EPI_SOFTMAX64, true>), grid, dim3(512),",
+         "hipLaunchKernelGGL((gemm256w4_kernel<NR_EPI_SOFTMAX64, true>), grid, dim3(256),"),
+    ],
     # no s_setprio around the MFMA phases
     "noprio": [
         ("  __builtin_amdgcn_s_setprio(1);                       \\\n  mma(QM, NI, FB);                                     \\\n"
