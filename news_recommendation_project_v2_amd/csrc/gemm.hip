@@ -1491,12 +1491,15 @@ __global__ __launch_bounds__(256, 1) void gemm256w4_kernel(int64_t M, int64_t N,
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) fa[s4] = *reinterpret_cast<const frag_t*>(sp + cs[s4]);
   };
-  auto readB = [&](int stage) {
+  // P0's reads in MFMA order (k slice s: B of all four column tiles, then A of
+  // row tile 0), so the first MFMAs wait only for their own fragments
+  auto readP0 = [&](int stage) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const unsigned char* sp = smem + stage * G2_STAGE + bbase + j * 32 * 128;
+    for (int s4 = 0; s4 < 4; ++s4) {
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) fb[j][s4] = *reinterpret_cast<const frag_t*>(sp + cs[s4]);
+      for (int j = 0; j < 4; ++j)
+        fb[j][s4] = *reinterpret_cast<const frag_t*>(smem + stage * G2_STAGE + bbase + j * 32 * 128 + cs[s4]);
+      fa0[s4] = *reinterpret_cast<const frag_t*>(smem + stage * G2_STAGE + abase + cs[s4]);
     }
   };
   auto mma = [&](int i, const frag_t (&fa)[4]) {
@@ -1513,9 +1516,11 @@ __global__ __launch_bounds__(256, 1) void gemm256w4_kernel(int64_t M, int64_t N,
     const bool pf = kt + 2 < nk || more;
     const bool edge = kt + 2 >= nk;  // this step's DMAs fetch the next tile's step kt + 2 - nk
     const int kf = edge ? kt + 2 - nk : kt + 2;
-    readB(st);
-    readA(st, 0, fa0);
+    // P0: fragments of row tile 0 and all of B; MFMAs start as their operands land
+    readP0(st);
     readA(st, 1, fa1);
+    mma(0, fa0);
+    // P1: every wave has read B and A tiles 0, 1 of this stage -> refill them for step kt + 2
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -1526,16 +1531,15 @@ __global__ __launch_bounds__(256, 1) void gemm256w4_kernel(int64_t M, int64_t N,
         dma_bias(lslot ^ 1, nn0);
       }
       dmaB(st, kf);
-    }
-    mma(0, fa0);
-    readA(st, 2, fa0);
-    if (pf) {
       dmaA(0, st, kf);
       dmaA(1, st, kf);
     }
+    readA(st, 2, fa0);
     mma(1, fa1);
+    // P2
     readA(st, 3, fa1);
     mma(2, fa0);
+    // P3: A tiles 2, 3 read by every wave -> refill them
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();

@@ -1,0 +1,91 @@
+"""Every public C-ABI entry refuses host memory before launching.
+
+On this GPU-less host the HIP runtime knows no device allocation, so any
+non-null pointer is "not device memory": each entry below is called with
+otherwise valid arguments pointing at a host buffer and must return
+NR_ERR_INVALID (-1) with a residency message, never reach a kernel launch.
+The GPU-side counterpart (device tensors accepted, CPU tensors refused, no
+fault) is tests/test_residency.py."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from news_recommendation_project_v2_amd import _lib
+
+F32, BF16 = _lib.NR_F32, _lib.NR_BF16
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not _lib.LIB_PATH.is_file():
+        pytest.skip("libnewsrec_hip.so not built (run __graft_entry__.build())")
+    return _lib.load()
+
+
+@pytest.fixture(scope="module")
+def H():
+    """One 256-B aligned host buffer; every pointer argument points into it."""
+    raw = np.zeros(64 << 20, dtype=np.uint8)
+    base = raw.ctypes.data
+    off = (-base) % 256
+    return raw, ctypes.c_void_p(base + off)
+
+
+def _calls(P):
+    f = ctypes.c_float
+    L = ctypes.c_int64
+    grp = (L * 1)(4096)
+    ptrs = (ctypes.c_void_p * 1)(P.value)
+    layer = _lib.EncoderLayer(*([P.value] * 12))
+    return {
+        "nr_gemm": (F32, F32, 0, 4, 128, 32, P, 32, P, 32, None, None, 0, P, 128, None),
+        "nr_gemm_relu_dropout": (BF16, BF16, 4, 256, 64, P, 64, P, 64, P, P, 256, 7, f(0.1), None),
+        "nr_gemm_drelu": (BF16, BF16, 4, 256, 64, P, 64, P, 64, P, 256, P, 256, f(1.0), None),
+        "nr_gemm_grouped": (BF16, F32, 1, (L * 1)(256), (L * 1)(256), (L * 1)(64), ptrs, (L * 1)(64), ptrs,
+                            (L * 1)(64), ptrs, (L * 1)(256), None),
+        "nr_layernorm": (F32, F32, 2, 1024, P, 1024, P, P, f(1e-5), P, 1024, None),
+        "nr_gather_layernorm": (F32, 2, 1024, P, 1024, P, 1, P, P, f(1e-12), P, 1024, None),
+        "nr_softmax64": (2, 2, P, 128, F32, P, 128, None),
+        "nr_row_inv_norm": (F32, 2, 1024, P, 1024, f(1e-8), P, None),
+        "nr_row_stats": (F32, 2, 1024, P, 1024, f(1e-5), P, None),
+        "nr_pool_score": (_lib.NR_POOL_LATENT, F32, 1024, P, 1024, P, 1024, P, P, P, P, P, 2, P, None, None),
+        "nr_score_users": (F32, 1024, P, P, P, 1024, P, P, P, 2, P, None),
+        "nr_dense_rank": (P, P, 2, P, P, None),
+        "nr_impression_metrics": (P, P, P, 2, P, P, P, None),
+        "nr_final_attn_transform": (F32, 2, P, 1024, P, P, P, P, P, P, P, P, P, P, P, 1 << 24, None),
+        "nr_latent_transform": (F32, 2, P, 1024, P, P, P, P, P, P, P, P, P, P, P, P, 1 << 24, None),
+        "nr_latent_transform_lnfold": (BF16, 2, P, 1024, P, P, P, P, P, P, P, P, P, 1 << 24, None),
+        "nr_embed_ln": (F32, 4, P, P, P, P, P, P, P, f(1e-5), P, None),
+        "nr_attention_varlen": (F32, 1, 1, P, P, P, P, None),
+        "nr_encoder_forward": (F32, 1, ctypes.byref(layer), P, 100, P, 514, P, P, P, f(1e-5), 1, 4, P, P,
+                               _lib.NR_POOL_MEAN, P, None, None, P, 1 << 24, None),
+        "nr_gather_rows": (F32, F32, 2, 1024, P, 1024, P, P, 1024, None),
+        "nr_transpose": (F32, F32, 64, 64, P, 64, P, 64, None),
+        "nr_final_pool_fwd": (F32, 2, P, P, 2048, P, P, None),
+        "nr_final_pool_bwd": (F32, 2, P, 64, P, 2048, P, P, P, P, 1024, P, 1024, None),
+        "nr_cosine_margin": (2, P, P, 1024, P, P, f(2.0), P, P, P, P, None),
+        "nr_scatter_add_rows": (F32, 2, 1024, P, 1024, P, P, 1024, None),
+        "nr_col_sum": (F32, 4, 128, P, 128, P, None),
+        "nr_ln_param_grad": (F32, 2, 1024, P, 1024, P, f(1e-12), P, 1024, P, P, None),
+        "nr_sumsq": (16, P, P, None),
+        "nr_adamw": (16, P, P, P, P, None, 1, f(1e-6), f(0.9), f(0.999), f(1e-8), f(0.01), f(0.5), P, None),
+        "nr_splitk_fixup": (F32, _lib.NR_EPI_NONE, 2, 256, 2, P, P, None, 0, P, 256, 0, 0, f(0.0), f(1.0), None),
+    }
+
+
+def test_every_entry_with_pointers_is_covered():
+    """The table below names every header entry that takes a device pointer."""
+    no_ptr = {"nr_version", "nr_build_hash", "nr_init", "nr_last_error", "nr_set_persistent_workgroups",
+              "nr_persistent_workgroups", "nr_final_attn_workspace_bytes", "nr_latent_workspace_bytes",
+              "nr_encoder_workspace_bytes"}
+    assert set(_calls(ctypes.c_void_p(256))) == set(_lib.SIGNATURES) - no_ptr
+
+
+def test_host_pointers_refused_by_every_entry(lib, H):
+    _, P = H
+    for name, args in _calls(P).items():
+        rc = getattr(lib, name)(*args)
+        msg = lib.nr_last_error().decode()
+        assert rc == -1, f"{name}: rc {rc} ({msg})"
+        assert "not device memory" in msg, f"{name}: {msg}"
