@@ -21,7 +21,7 @@ def _batch(seed=0, B=6, L=11, D=1024):
     mask = np.zeros((B, L), dtype=np.int64)
     for b, n in enumerate(lens):
         mask[b, :n] = 1
-    emb = rng.standard_normal((B, L, D)).astype(np.float32) * mask[..., None]
+    emb = (rng.standard_normal((B, L, D)) * mask[..., None]).astype(np.float32)
     slot_rows = -np.ones((B, L), dtype=np.int64)
     r = 0
     for b, n in enumerate(lens):
