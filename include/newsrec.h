@@ -90,6 +90,13 @@ int nr_set_persistent_workgroups(int n);
  * restore what it found. */
 int nr_persistent_workgroups(void);
 
+/* Split-K tail of the bf16 per-news transforms (default on): the rows past the
+ * last full round of 256x256 tiles of a K >= 1024 GEMM run as K-slices that
+ * fill the CUs (f32 partials) + a fixup applying the same epilogue, instead of
+ * a partly filled last round.  Results agree with on = 0 to bf16 rounding.
+ * Process-wide; for A/B measurements and tests. */
+int nr_set_split_tail(int on);
+
 /* Thread-local message of the last failed call ("" if none). */
 const char* nr_last_error(void);
 

@@ -1458,7 +1458,6 @@ __global__ __launch_bounds__(256, 1) void gemm256w4_kernel(int64_t M, int64_t N,
   unsigned char* ln_lds = smem + 2 * G2_STAGE + 2 * 4 * 512;
   const __amdgpu_buffer_rsrc_t rUC = rsrc(ea.ln_uc, LNF ? 2 * N * 4 : 0);
   const __amdgpu_buffer_rsrc_t rST = rsrc(ea.ln_stats, LNF ? M * 8 : 0);
-  constexpr int kLnDma = 6;
   auto dma_ln = [&](int slot, uint32_t mb, uint32_t nb) {
     if constexpr (LNF) {
       unsigned char* base = ln_lds + slot * kLn4;
@@ -2006,7 +2005,179 @@ int gemm_dispatch_ex(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N,
   return launch_gemm_t<__bf16, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
 }
 
+// ---------------------------------------------------------------------------
+// Split-K tail of the bf16 transform GEMMs.  A persistent launch over M rows
+// runs ceil(tiles / CUs) rounds of 256x256 tiles; when the last round is only
+// partly filled (M = 72,023: ff2 / final.l3 / l5 4.4 rounds, S 2.2, ff1 35.25)
+// its CUs idle for a whole tile time.  Here the rows of the full rounds run as
+// usual and the rows past them run as `s` K-slices in one grouped launch
+// (f32 partials, gemm256p_group_kernel) that fills the CUs, followed by a
+// row-wise fixup that sums the slices and applies the same epilogue (bias,
+// LayerNorm fold, ReLU / exp / GEGLU / softmax64 / residual).  The sum runs
+// in f32 in a different order than one tile's K loop, so results agree with
+// the unsplit launch to bf16 rounding (tests/test_gpu_parity.py
+// `test_split_tail_matches_unsplit`).
+
+// One thread per 4 output columns; softmax64 groups are 16 consecutive threads.
+template <int EPI, bool LNF>
+__global__ __launch_bounds__(256) void tail_fixup_kernel(int64_t rows, int64_t N, int parts, const float* __restrict__ P,
+                                                         const float* __restrict__ bias,
+                                                         const float* __restrict__ stats,  // [rows] (mean, rstd)
+                                                         const float* __restrict__ uc,     // u [N] | c [N]
+                                                         const __bf16* R, int64_t ldr, __bf16* C, int64_t ldc) {
+  const int64_t ncols = EPI == NR_EPI_GEGLU ? N / 2 : N;
+  const int64_t quads = ncols / 4;
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = (int64_t)blockIdx.y;
+  if (r >= rows) return;
+  const bool act = q < quads;
+  const int64_t o = act ? 4 * q : 0;  // first output column
+  float2 ms = make_float2(0.f, 1.f);
+  if constexpr (LNF) ms = *reinterpret_cast<const float2*>(stats + 2 * r);
+  auto col_val = [&](int64_t c) {  // the epilogue's pre-activation value of input column c (4 of them)
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < parts; ++p) acc += *reinterpret_cast<const f32x4*>(P + ((int64_t)p * rows + r) * N + c);
+    if (bias) acc += *reinterpret_cast<const f32x4*>(bias + c);
+    if constexpr (LNF) {
+      const f32x4 u = *reinterpret_cast<const f32x4*>(uc + c), cc = *reinterpret_cast<const f32x4*>(uc + N + c);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] = fmaf(ms.y, fmaf(-ms.x, u[k], acc[k]), cc[k]);
+    }
+    return acc;
+  };
+  float v[4];
+  if constexpr (EPI == NR_EPI_GEGLU) {
+    // W rows interleaved in 32-row (a, g) blocks: output column o = 32 b + w -> a = 64 b + w, g = a + 32
+    const int64_t ca = 64 * (o / 32) + (o % 32);
+    const f32x4 a = col_val(ca), g = col_val(ca + 32);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = a[k] * gelu_erf(g[k]);
+  } else {
+    const f32x4 a = col_val(o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float x = a[k];
+      if constexpr (EPI == NR_EPI_RELU) x = fmaxf(x, 0.f);
+      if constexpr (EPI == NR_EPI_EXP) x = expf(x);
+      if constexpr (EPI == NR_EPI_GELU) x = gelu_erf(x);
+      v[k] = x;
+    }
+    if constexpr (EPI == NR_EPI_SOFTMAX64) {
+      float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+#pragma unroll
+      for (int m = 8; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[k] = expf(v[k] - mx);
+        sum += v[k];
+      }
+#pragma unroll
+      for (int m = 8; m >= 1; m >>= 1) sum += __shfl_xor(sum, m, 64);
+      const float inv = 1.0f / sum;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] *= inv;
+    }
+    if constexpr (EPI == NR_EPI_RESADD) {
+      const uint2 rr = *reinterpret_cast<const uint2*>(R + r * ldr + o);
+      v[0] += bf16_lo(rr.x);
+      v[1] += bf16_hi(rr.x);
+      v[2] += bf16_lo(rr.y);
+      v[3] += bf16_hi(rr.y);
+    }
+  }
+  if (act) *reinterpret_cast<uint2*>(C + r * ldc + o) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+}
+
+static int g_split_tail = 1;  // nr_set_split_tail
+
+// Scratch the split tail may need (f32 partials), for any M: at most #CUs tiles
+// of 256 x 256 f32 are in the tail's slices.
+int64_t split_tail_scratch_bytes() { return (int64_t)num_cus() * G2BM * G2BN * 4; }
+
+// bf16 -> bf16 GEMM over M rows with the split-K tail (see above); `lnf`:
+// LayerNorm folded (stats [M] pairs, uc [2N], no bias) as gemm_lnfold_dispatch.
+// Falls back to the single persistent launch when splitting does not pay
+// (K < 1024, no partial last round, fewer than 2 slices, or too little scratch).
+int gemm_split_tail_dispatch(int epi, bool lnf, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                             const void* W, int64_t ldw, const float* bias, const float* stats, const float* uc,
+                             const void* R, int64_t ldr, void* C, int64_t ldc, void* scratch, int64_t scratch_bytes,
+                             hipStream_t s) {
+  auto whole = [&](int64_t m, int64_t r0) -> int {
+    const char* a = (const char*)A + r0 * lda * 2;
+    char* c = (char*)C + r0 * ldc * 2;
+    const char* r = R ? (const char*)R + r0 * ldr * 2 : nullptr;
+    if (lnf) return gemm_lnfold_dispatch(epi, m, N, K, a, lda, W, ldw, stats + 2 * r0, uc, c, ldc, s);
+    return gemm_dispatch(NR_BF16, NR_BF16, epi, m, N, K, a, lda, W, ldw, bias, r, ldr, c, ldc, s);
+  };
+  const int ncu = num_cus();
+  const int64_t ntn = N / G2BN;
+  const int64_t ntm = (M + G2BM - 1) / G2BM;
+  if (!g_split_tail || N % G2BN || K < 1024 || ntn > ncu || ncu % ntn) return whole(M, 0);
+  const int64_t per_round = ncu / ntn;                 // M-tiles per full round
+  const int64_t ntm_main = ntm / per_round * per_round;
+  const int64_t tail_tiles = (ntm - ntm_main) * ntn;
+  if (tail_tiles == 0) return whole(M, 0);
+  int parts = (int)(ncu / tail_tiles);
+  if (parts > NR_GEMM_MAX_GROUP) parts = NR_GEMM_MAX_GROUP;
+  while (parts > 1 && (K % (64 * parts) || K / parts < 128)) --parts;
+  const int64_t row0 = ntm_main * G2BM, rows = M - row0;
+  if (parts < 2 || !scratch || scratch_bytes < (int64_t)parts * rows * N * 4 || ((uintptr_t)scratch & 15))
+    return whole(M, 0);
+  int rc;
+  if (row0 > 0 && (rc = whole(row0, 0))) return rc;
+  // the tail rows as `parts` K-slices: out_p = A[row0:, k_p] . W[:, k_p]^T (f32, no bias)
+  GemmGroup g{};
+  const int64_t ks = K / parts;
+  int64_t tiles = 0;
+  for (int p = 0; p < parts; ++p) {
+    g.M[p] = rows; g.N[p] = N; g.K[p] = ks;
+    g.A[p] = (const __bf16*)A + row0 * lda + p * ks;
+    g.W[p] = (const __bf16*)W + p * ks;
+    g.C[p] = (float*)scratch + (int64_t)p * rows * N;
+    g.lda[p] = lda; g.ldw[p] = ldw; g.ldc[p] = N;
+    g.ntn[p] = (int)ntn;
+    tiles += ((rows + G2BM - 1) / G2BM) * ntn;
+    g.tile_end[p] = (int)tiles;
+  }
+  g.n = parts;
+  hipLaunchKernelGGL((gemm256p_group_kernel<__bf16, float, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);
+  NR_CHECK_LAUNCH("nr_gemm(split tail)");
+  const int64_t ncols = epi == NR_EPI_GEGLU ? N / 2 : N;
+  const dim3 grid((unsigned)((ncols / 4 + 255) / 256), (unsigned)rows);
+  const float* st = lnf ? stats + 2 * row0 : nullptr;
+  const __bf16* r = R ? (const __bf16*)R + row0 * ldr : nullptr;
+  __bf16* c = (__bf16*)C + row0 * ldc;
+  const float* P = (const float*)scratch;
+#define NR_FIX(E)                                                                                                 \
+  do {                                                                                                            \
+    if (lnf)                                                                                                      \
+      hipLaunchKernelGGL((tail_fixup_kernel<E, true>), grid, dim3(256), 0, s, rows, N, parts, P, nullptr, st, uc, \
+                         r, ldr, c, ldc);                                                                         \
+    else                                                                                                          \
+      hipLaunchKernelGGL((tail_fixup_kernel<E, false>), grid, dim3(256), 0, s, rows, N, parts, P, bias, st, uc,   \
+                         r, ldr, c, ldc);                                                                         \
+  } while (0)
+  switch (epi) {
+    case NR_EPI_NONE: NR_FIX(NR_EPI_NONE); break;
+    case NR_EPI_RELU: NR_FIX(NR_EPI_RELU); break;
+    case NR_EPI_EXP: NR_FIX(NR_EPI_EXP); break;
+    case NR_EPI_GEGLU: NR_FIX(NR_EPI_GEGLU); break;
+    case NR_EPI_RESADD: NR_FIX(NR_EPI_RESADD); break;
+    case NR_EPI_SOFTMAX64: NR_FIX(NR_EPI_SOFTMAX64); break;
+    default: set_error("nr_gemm(split tail): epilogue %d unsupported", epi); return NR_ERR_UNSUPPORTED;
+  }
+#undef NR_FIX
+  NR_CHECK_LAUNCH("nr_gemm(split tail fixup)");
+  return NR_OK;
+}
+
 }  // namespace nr
+
+extern "C" int nr_set_split_tail(int on) {
+  nr::g_split_tail = on ? 1 : 0;
+  return NR_OK;
+}
 
 extern "C" int nr_gemm_relu_dropout(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K,
                                     const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
