@@ -2015,7 +2015,7 @@ int gemm_dispatch_ex(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N,
 // row-wise fixup that sums the slices and applies the same epilogue (bias,
 // LayerNorm fold, ReLU / exp / GEGLU / softmax64 / residual).  The sum runs
 // in f32 in a different order than one tile's K loop, so results agree with
-// the unsplit launch to bf16 rounding (tests/test_gpu_parity.py
+// the unsplit launch to bf16 rounding (tests/test_lnfold.py
 // `test_split_tail_matches_unsplit`).
 
 // One thread per 4 output columns; softmax64 groups are 16 consecutive threads.
@@ -2098,7 +2098,10 @@ int64_t split_tail_scratch_bytes() { return (int64_t)num_cus() * G2BM * G2BN * 4
 // bf16 -> bf16 GEMM over M rows with the split-K tail (see above); `lnf`:
 // LayerNorm folded (stats [M] pairs, uc [2N], no bias) as gemm_lnfold_dispatch.
 // Falls back to the single persistent launch when splitting does not pay
-// (K < 1024, no partial last round, fewer than 2 slices, or too little scratch).
+// (K < 4096, no partial last round, fewer than 2 slices, or too little scratch).
+// K >= 4096 only: at K = 1024 a tile takes ~20 us, the idle part of the last
+// round is worth less than the slice launch + fixup + f32 partial traffic
+// (measured in round 3: latent S + ff1 split 26 us slower per transform).
 int gemm_split_tail_dispatch(int epi, bool lnf, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                              const void* W, int64_t ldw, const float* bias, const float* stats, const float* uc,
                              const void* R, int64_t ldr, void* C, int64_t ldc, void* scratch, int64_t scratch_bytes,
@@ -2113,7 +2116,7 @@ int gemm_split_tail_dispatch(int epi, bool lnf, int64_t M, int64_t N, int64_t K,
   const int ncu = num_cus();
   const int64_t ntn = N / G2BN;
   const int64_t ntm = (M + G2BM - 1) / G2BM;
-  if (!g_split_tail || N % G2BN || K < 1024 || ntn > ncu || ncu % ntn) return whole(M, 0);
+  if (!g_split_tail || N % G2BN || K < 4096 || ntn > ncu || ncu % ntn) return whole(M, 0);
   const int64_t per_round = ncu / ntn;                 // M-tiles per full round
   const int64_t ntm_main = ntm / per_round * per_round;
   const int64_t tail_tiles = (ntm - ntm_main) * ntn;

@@ -89,10 +89,15 @@ def test_latent_lnfold_rejects_f32(gpu_device):
 @pytest.mark.parametrize("pooler", ["latent", "final"])
 def test_split_tail_matches_unsplit(gpu_device, pooler):
     """The bf16 transforms' split-K tail (rows past the last full round of
-    tiles run as K-slices + fixup: at M = 72,023 the S / ff1 / ff2 GEMMs of the
-    latent chain and final.l3 / l5) against the same transform with the split
-    off: rows before the tail are bit-identical; tail rows differ only by the
-    f32 summation order, i.e. at most one bf16 rounding step of the value."""
+    tiles run as K-slices + fixup: at M = 72,023 the K = 4096 GEMMs, latent ff2
+    and final.l3 / l5) against the same transform with the split off: rows
+    before the tail are bit-identical; in the tail rows a split GEMM's sums
+    differ from the unsplit one's only in f32 summation order, which moves a
+    bf16 output by at most one rounding step.  Latent: ff2 is the last GEMM, so
+    each tail value is within one bf16 ulp (2^-7 relative, + 2^-12 for the
+    residual's cancellation).  FinalAttention: x (l3) moves by an ulp, which
+    l4 and l5 carry into the exp logits, so those are held to 2^-5 of the row's
+    rms logit; every tail row's cosine with the unsplit row > 0.99999."""
     from news_recommendation_project_v2_amd import _lib, synthetic
     from news_recommendation_project_v2_amd.engine import PoolScoreEngine
     from news_recommendation_project_v2_amd.latent_attention import LatentAttentionModel
@@ -117,6 +122,10 @@ def test_split_tail_matches_unsplit(gpu_device, pooler):
     g, r = got[head:].float(), ref[head:].float()
     if pooler == "final":  # the exp(w) half: compare the logits
         g, r = torch.cat([g[:, :1024], g[:, 1024:].log()], 1), torch.cat([r[:, :1024], r[:, 1024:].log()], 1)
-    tol = r.abs() * 2.0 ** -7 + 1e-6
+    if pooler == "latent":
+        tol = r.abs() * 2.0 ** -7 + 2.0 ** -12
+    else:
+        tol = r.abs() * 2.0 ** -7 + r.pow(2).mean(1, keepdim=True).sqrt() * 2.0 ** -5
     assert ((g - r).abs() <= tol).all(), float(((g - r).abs() - tol).max())
+    assert torch.nn.functional.cosine_similarity(g, r, dim=1).min().item() > 0.99999
     assert not torch.equal(got, ref) or pooler == "final"  # the latent tail did take the split path

@@ -32,9 +32,11 @@ def main():
     import bench
     from news_recommendation_project_v2_amd import synthetic
     imps = synthetic.mind_shaped("mind_large_dev", seed=1234)
-    res = {}
+    res = json.loads(dst.read_text()) if dst.exists() else {}  # configs not in `src` keep their last values
     for cfg in ("latent_bf16", "final_bf16", "latent_fp32"):
         pooler, dt = cfg.split("_")
+        if not (src / f"pmc_{cfg}_FETCH_SIZE").is_dir():
+            continue
         f = counters(src / f"pmc_{cfg}_FETCH_SIZE")["FETCH_SIZE"]
         w = counters(src / f"pmc_{cfg}_WRITE_SIZE")["WRITE_SIZE"]
         hm = counters(src / f"pmc_{cfg}_TCC_HIT_sum_TCC_MISS_sum")
