@@ -90,10 +90,13 @@ int nr_set_persistent_workgroups(int n);
  * restore what it found. */
 int nr_persistent_workgroups(void);
 
-/* Split-K tail of the bf16 per-news transforms (default on): the rows past the
- * last full round of 256x256 tiles of a K >= 1024 GEMM run as K-slices that
+/* Split-K tail of the bf16 per-news transforms (default OFF): the rows past the
+ * last full round of 256x256 tiles of a K >= 4096 GEMM run as K-slices that
  * fill the CUs (f32 partials) + a fixup applying the same epilogue, instead of
- * a partly filled last round.  Results agree with on = 0 to bf16 rounding.
+ * a partly filled last round.  Results agree with on = 0 to bf16 rounding, but
+ * which rows are split depends on M, so with it on a row's output depends on
+ * how the table was cut (chunks, ranks); off, every row is computed the same
+ * way for any M (the sharded transform is bit-identical to one launch).
  * Process-wide; for A/B measurements and tests. */
 int nr_set_split_tail(int on);
 

@@ -2089,7 +2089,11 @@ __global__ __launch_bounds__(256) void tail_fixup_kernel(int64_t rows, int64_t N
   if (act) *reinterpret_cast<uint2*>(C + r * ldc + o) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
 }
 
-static int g_split_tail = 1;  // nr_set_split_tail
+// nr_set_split_tail; off by default: the split rows depend on M, so with it on a
+// row's bits depend on how the table is cut into chunks / rank shards (round-3
+// GPU run: the chunked one-rank RCCL transform differed from one launch), for
+// ~15 us per K = 4096 GEMM (profiles/round3/split_tail_ab.jsonl)
+static int g_split_tail = 0;
 
 // Scratch the split tail may need (f32 partials), for any M: at most #CUs tiles
 // of 256 x 256 f32 are in the tail's slices.

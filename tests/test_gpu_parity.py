@@ -546,6 +546,26 @@ def test_train_v3_and_save_emb_scripts_synthetic(gpu_device, tmp_path, monkeypat
     assert torch.allclose(t.norm(dim=1), torch.ones(t.shape[0]), atol=1e-4)
 
 
+@pytest.mark.parametrize("pooler", ["latent", "final"])
+def test_transform_rows_independent_of_the_cut(gpu_device, pooler):
+    """A news row's transformed bits do not depend on which rows share its
+    launch: the MIND-large-dev table (72,023 rows) transformed whole equals,
+    bit for bit, its rank shards at N = 8 (9,003 rows: the SCALE run's cut),
+    N = 3 and a ragged odd cut transformed one by one.  This is what lets the
+    sharded N-GPU table equal the 1-GPU table exactly (the split-K tail, which
+    splits rows depending on M, is off by default for this reason)."""
+    n = synthetic.SHAPES["mind_large_dev"][0]
+    table = W.news_table(1234, n, 1024, name="mind_large").to(gpu_device)
+    eng = PoolScoreEngine(_model(pooler, gpu_device), dtype=torch.bfloat16, device=gpu_device)
+    want = eng.load_news(table).transform().clone()
+    for cuts in ([(n + 7) // 8 * i for i in range(9)], [(n + 2) // 3 * i for i in range(4)], [0, 1, 257, 40001, n]):
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            b = min(b, n)
+            got = eng.load_news(table[a:b]).transform()
+            torch.cuda.synchronize()
+            assert torch.equal(got, want[a:b]), (pooler, a, b)
+
+
 @pytest.mark.parametrize("pooler,chunks", [("final", 3), ("latent", 3), ("latent", 1)])
 def test_sharded_table_overlapped_rccl_single_rank(gpu_device, pooler, chunks, tmp_path):
     """The overlapped transform / all-gather path RCCL ranks take (chunks

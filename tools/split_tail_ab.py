@@ -48,7 +48,7 @@ def main():
                     e1.record()
                     torch.cuda.synchronize()
                     t[on].append(e0.elapsed_time(e1) / 5)
-            lib.nr_set_split_tail(1)
+            lib.nr_set_split_tail(0)
             print(json.dumps({"pooler": pooler, "m": n, "split_ms": round(float(np.median(t[1])), 4),
                               "nosplit_ms": round(float(np.median(t[0])), 4)}), flush=True)
 
