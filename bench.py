@@ -289,6 +289,36 @@ def config2_leg(dev, n_news: int = 8192) -> dict:
     return out
 
 
+def encoder_bf16_leg(dev, n_news: int = 16384) -> dict:
+    """BASELINE configs[2]'s embedding step in bf16: the 24-layer XLM-R-large-
+    shaped title encoder (packed varlen, nr_encoder_forward) over n_news
+    synthetic titles, query (~46 tokens) + passage (~20) passes as save_emb.py
+    runs them; tokens/s, news/s and the GEMM+attention FLOP rate against the
+    2.5 PF dense bf16 peak (0.604 GFLOP per token + 4 L^2 1024 per sequence and
+    layer)."""
+    sys.path.insert(0, str(REPO / "scripts"))
+    from save_emb import synthetic_titles
+    from news_recommendation_project_v2_amd.encoder import XLMREncoder
+    enc = XLMREncoder(W.xlmr_state_dict(1234, 24, 50_000), dtype=torch.bfloat16, device=dev)
+    p_ids, p_lens = synthetic_titles(n_news, 1234, 50_000, 20)
+    q_ids, q_lens = synthetic_titles(n_news, 1234, 50_000, 20, prefix_len=26)
+    enc.encode_packed(q_ids, q_lens, normalize=True)  # warm-up at the full size
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    enc.encode_packed(q_ids, q_lens, normalize=True)
+    enc.encode_packed(p_ids, p_lens, normalize=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    tok = int(p_lens.sum() + q_lens.sum())
+    sq = float((np.asarray(p_lens, dtype=np.float64) ** 2).sum() + (np.asarray(q_lens, dtype=np.float64) ** 2).sum())
+    flops = tok * 603_979_776 + 24 * 4 * 1024 * sq
+    del enc
+    torch.cuda.empty_cache()
+    return {"news": n_news, "tokens": tok, "seconds": round(dt, 3), "tokens_per_s": round(tok / dt, 1),
+            "news_per_s": round(n_news / dt, 1), "tflops": round(flops / dt / 1e12, 1),
+            "peak_frac": round(flops / dt / 2.5e15, 3)}
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -660,6 +690,7 @@ def main():
                             "score_bytes": int(4 * imps.n_cand)}
         extra["train_bf16_config5"] = train_step_ms(dev)
         extra["config2_mind_small_f32"] = config2_leg(dev)
+        extra["encoder_bf16_config3"] = encoder_bf16_leg(dev)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

@@ -4,7 +4,7 @@
 set -o pipefail
 OUT=gpurun_out/${1:-r3s4b}
 mkdir -p "$OUT"
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests \
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu ${TESTS:-tests} \
   > "$OUT/pytest_gpu.log" 2>&1 && \
 ( cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/gemm_trace" -o gemm --output-format csv -- \
