@@ -77,6 +77,80 @@ VARIANTS = {
          '    if (pb) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");\n'
          '    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");'),
     ],
+    # operand refills spread 2 pieces per phase: P1 A1 (deferred from the previous step,
+    # into the other stage), P2 A0, P3 B0, P4 B1 (shipped: P2 A0+B0, P3 B1, P4 A1);
+    # P4 then leaves 6 pieces in flight (vmcnt(6), 9 with the LN slices)
+    "dma2": [
+        ("constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78, kVmcnt11 = 0x0F7B;",
+         "constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78, kVmcnt11 = 0x0F7B, kVmcnt6 = 0x0F76, kVmcnt9 = 0x0F79;"),
+        ("""  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {
+    const bool pf = kt + 2 < nk || more;
+    const int kf = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
+    readA(st, 0);
+    readB(st, 0, fb0);
+    NR_PHASE_SYNC_MMA(0, 0, fb0)
+    readB(st, 1, fb1);
+    if (pf) {
+      if (kt + 2 == nk) {
+        set_offA(nm0);
+        set_offB(nn0);
+        dma_bias(nn0);
+      }
+      dmaA(0, st, kf);
+      dmaB(0, st, kf);
+    }
+    NR_PHASE_SYNC_MMA(0, 1, fb1)
+    readA(st, 1);
+    if (pf) dmaB(1, st, kf);
+    NR_PHASE_SYNC_MMA(1, 1, fb1)
+    if (pf) {
+      dmaA(1, st, kf);
+      if (LNF && kt + 2 == nk) {
+        // the next tile's LN slices after its step-0 DMAs: they get a whole K step
+        dma_ln(lslot ^ 1, nm0, nn0);
+        __builtin_amdgcn_s_waitcnt(kVmcnt11);
+      } else {
+        __builtin_amdgcn_s_waitcnt(kVmcnt8);  // step kt + 1 landed; kt + 2 (8 DMAs) may fly
+      }
+    } else {
+      __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    }""",
+         """  bool a1p = false;  // the previous step's A1 refill (stage st ^ 1, step a1k), issued in this step's P1
+  int a1k = 0;
+  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {
+    const bool pf = kt + 2 < nk || more;
+    const int kf = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
+    readA(st, 0);
+    readB(st, 0, fb0);
+    if (a1p) dmaA(1, st ^ 1, a1k);
+    NR_PHASE_SYNC_MMA(0, 0, fb0)
+    readB(st, 1, fb1);
+    if (pf) {
+      if (kt + 2 == nk) {
+        set_offA(nm0);
+        set_offB(nn0);
+        dma_bias(nn0);
+      }
+      dmaA(0, st, kf);
+    }
+    NR_PHASE_SYNC_MMA(0, 1, fb1)
+    readA(st, 1);
+    if (pf) dmaB(0, st, kf);
+    NR_PHASE_SYNC_MMA(1, 1, fb1)
+    if (pf) {
+      dmaB(1, st, kf);
+      if (LNF && kt + 2 == nk) {
+        dma_ln(lslot ^ 1, nm0, nn0);
+        __builtin_amdgcn_s_waitcnt(kVmcnt9);
+      } else {
+        __builtin_amdgcn_s_waitcnt(kVmcnt6);  // step kt + 1 landed (incl. its A1 from P1); 6 of kt + 2 fly
+      }
+    } else {
+      __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    }
+    a1p = pf;
+    a1k = kf;"""),
+    ],
     # DIAGNOSTIC (wrong results): no operand DMAs inside the K loop
     "nodma": [
         ("  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {\n    const int ns = st ^ 1;\n"
