@@ -46,6 +46,10 @@ __device__ __forceinline__ float gelu_erf(float g) {
   return x >= 0.f ? g * fmaf(-0.5f, ans, 1.0f) : 0.5f * g * ans;
 }
 
+// exp of the persistent bf16 kernel's EXP and SOFTMAX64 epilogues (outputs are
+// rounded to bf16).
+__device__ __forceinline__ float epi_exp(float x) { return expf(x); }
+
 // Extra epilogue arguments (dropout of the training forward; unused otherwise).
 struct EpiArgs {
   uint64_t seed;  // dropout stream
@@ -1155,7 +1159,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
               const uint64_t gi = (uint64_t)(row * N + col0 + 32 * ni + 8 * (r >> 2) + 4 * h32 + (r & 3));
               x = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(x, 0.f) * ea.scale;
             }
-            if constexpr (EPI == NR_EPI_EXP) x = expf(x);
+            if constexpr (EPI == NR_EPI_EXP) x = epi_exp(x);
             if constexpr (EPI == NR_EPI_GELU) x = gelu_erf(x);
             v[ni][r] = x;
           }
@@ -1172,7 +1176,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              v[ni][r] = expf(v[ni][r] - mx);
+              v[ni][r] = epi_exp(v[ni][r] - mx);
               sum += v[ni][r];
             }
           sum += __shfl_xor(sum, 32, 64);
@@ -1276,7 +1280,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
               const uint64_t gi = (uint64_t)(row * N + col0 + 16 * ni + 4 * q4 + r);
               x = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(x, 0.f) * ea.scale;
             }
-            if constexpr (EPI == NR_EPI_EXP) x = expf(x);
+            if constexpr (EPI == NR_EPI_EXP) x = epi_exp(x);
             if constexpr (EPI == NR_EPI_GELU) x = gelu_erf(x);
             v[ni][r] = x;
           }
@@ -1295,7 +1299,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              v[ni][r] = expf(v[ni][r] - mx);
+              v[ni][r] = epi_exp(v[ni][r] - mx);
               sum += v[ni][r];
             }
           sum += __shfl_xor(sum, 16, 64);

@@ -151,6 +151,12 @@ VARIANTS = {
     a1p = pf;
     a1k = kf;"""),
     ],
+    # the persistent kernel's EXP / SOFTMAX64 epilogues on v_exp_f32 (x log2 e), not the
+    # accurate expf (stamps: the S epilogue 13.5 k cycles per tile vs 4.2 k plain)
+    "fastexp": [
+        ("__device__ __forceinline__ float epi_exp(float x) { return expf(x); }",
+         "__device__ __forceinline__ float epi_exp(float x) { return __expf(x); }"),
+    ],
     # DIAGNOSTIC (wrong results): no operand DMAs inside the K loop
     "nodma": [
         ("  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {\n    const int ns = st ^ 1;\n"
