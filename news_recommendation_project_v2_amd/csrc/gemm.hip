@@ -46,9 +46,13 @@ __device__ __forceinline__ float gelu_erf(float g) {
   return x >= 0.f ? g * fmaf(-0.5f, ans, 1.0f) : 0.5f * g * ans;
 }
 
-// exp of the persistent bf16 kernel's EXP and SOFTMAX64 epilogues (outputs are
-// rounded to bf16).
-__device__ __forceinline__ float epi_exp(float x) { return expf(x); }
+// exp of the persistent bf16 kernel's EXP and SOFTMAX64 epilogues: v_exp_f32 of
+// x log2(e) (relative error ~1e-6 here, against bf16 outputs' 2^-8), not the
+// range-reduced expf (13 instructions): the softmax64 epilogue was 13.5 k
+// cycles per tile against 4.2 k for a plain one; S GEMM 745 -> 874 TF/s,
+// FinalAttention transform -2.4 % (round 3, profiles/round3/s4/).  The f32
+// parity kernels keep expf.
+__device__ __forceinline__ float epi_exp(float x) { return __expf(x); }
 
 // Extra epilogue arguments (dropout of the training forward; unused otherwise).
 struct EpiArgs {
@@ -760,7 +764,7 @@ __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t v) {  // v_pk_max_i16 w
 // not inline asm, so the compiler's own wait insertion sees them: it then knows
 // the older stores have retired and keeps its waits for the epilogue's
 // residual loads counted instead of vmcnt(0).
-constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78, kVmcnt11 = 0x0F7B;
+constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78, kVmcnt11 = 0x0F7B, kVmcnt6 = 0x0F76, kVmcnt9 = 0x0F79;
 
 // LNF (LayerNorm folded into the epilogue): per tile, every wave's (u, c)
 // column slices (2 x 256 B) and the tile's 256 row stats (2 KiB), in two
@@ -956,20 +960,25 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   mma(QM, NI, FB);                                     \
   __builtin_amdgcn_s_setprio(0);                       \
   __builtin_amdgcn_s_barrier();
-  // K step kt of the current tile (stage st).  All of step kt + 2 is
-  // prefetched into this stage, each quarter one phase after its last read
-  // (both wave groups' reads of phase p retire before the barrier instance
-  // the leading group passes to enter phase p + 1): A0 + B0 in P2 (read in
-  // P1), B1 in P3 (read in P2), A1 in P4 (read in P3) -- this tile's step, or
+  // K step kt of the current tile (stage st).  Step kt + 2 is prefetched into
+  // this stage, each quarter at least one phase after its last read (both
+  // wave groups' reads of phase p retire before the barrier instance the
+  // leading group passes to enter phase p + 1), two 1-KiB pieces per wave in
+  // every phase: A0 in P2 (read in P1), B0 in P3 (read in P1), B1 in P4 (read
+  // in P2), and A1 (read in P3) in the NEXT step's P1 -- this tile's step, or
   // past its end the next tile's steps 0 and 1 (with the next tile's bias
-  // slice ahead of step 0).  P4 then waits for step kt + 1 with the whole of
-  // step kt + 2 still in flight (+0.4..2.4 % over issuing it in P3/P4 as
-  // halves, profiles/round2/gemm_quarters_ab.jsonl).
+  // slice ahead of step 0).  P4 then waits for step kt + 1 (its A1 issued in
+  // this step's P1) with 6 pieces of step kt + 2 in flight.  Round 3: the even
+  // spread (was P2: A0 + B0, P3: B1, P4: A1) is 1.5 % / 2.6 % faster on the
+  // latent / FinalAttention transforms at M = 72,023 (profiles/round3/s4/).
+  bool a1p = false;  // the previous step's A1 refill (stage st ^ 1, step a1k), issued in this step's P1
+  int a1k = 0;
   auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {
     const bool pf = kt + 2 < nk || more;
     const int kf = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
     readA(st, 0);
     readB(st, 0, fb0);
+    if (a1p) dmaA(1, st ^ 1, a1k);
     NR_PHASE_SYNC_MMA(0, 0, fb0)
     readB(st, 1, fb1);
     if (pf) {
@@ -979,24 +988,24 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
         dma_bias(nn0);
       }
       dmaA(0, st, kf);
-      dmaB(0, st, kf);
     }
     NR_PHASE_SYNC_MMA(0, 1, fb1)
     readA(st, 1);
-    if (pf) dmaB(1, st, kf);
+    if (pf) dmaB(0, st, kf);
     NR_PHASE_SYNC_MMA(1, 1, fb1)
     if (pf) {
-      dmaA(1, st, kf);
+      dmaB(1, st, kf);
       if (LNF && kt + 2 == nk) {
-        // the next tile's LN slices after its step-0 DMAs: they get a whole K step
         dma_ln(lslot ^ 1, nm0, nn0);
-        __builtin_amdgcn_s_waitcnt(kVmcnt11);
+        __builtin_amdgcn_s_waitcnt(kVmcnt9);
       } else {
-        __builtin_amdgcn_s_waitcnt(kVmcnt8);  // step kt + 1 landed; kt + 2 (8 DMAs) may fly
+        __builtin_amdgcn_s_waitcnt(kVmcnt6);  // step kt + 1 landed (incl. its A1 from P1); 6 of kt + 2 fly
       }
     } else {
       __builtin_amdgcn_s_waitcnt(kVmcnt0);
     }
+    a1p = pf;
+    a1k = kf;
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
     mma(1, 0, fb0);

@@ -226,6 +226,75 @@ VARIANTS = {
         ("  return K >= 128 && M * lda * 2 <= kMax && N * ldw * 2 <= kMax;",
          "  return K >= 128 && K % 128 == 0 && M * lda * 2 <= kMax && N * ldw * 2 <= kMax;"),
     ],
+    # rb with the next tile's step-0 B0 read at its tile top (no fragments live through the epilogue)
+    "rb2": [
+        ("constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78, kVmcnt11 = 0x0F7B;",
+         "constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78, kVmcnt11 = 0x0F7B, kVmcnt10 = 0x0F7A;"),
+        ("""  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {
+    const bool pf = kt + 2 < nk || more;
+    const int kf = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
+    readA(st, 0);
+    readB(st, 0, fb0);
+    NR_PHASE_SYNC_MMA(0, 0, fb0)
+    readB(st, 1, fb1);""",
+         """  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0, frag_t (&fx)[2][2], frag_t (&fy)[2][2]) {
+    const bool pf = kt + 2 < nk || more;
+    const bool nx = kt + 1 < nk || more;
+    const int kf = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
+    readA(st, 0);
+    NR_PHASE_SYNC_MMA(0, 0, fx)
+    readB(st, 1, fy);"""),
+        ("""    NR_PHASE_SYNC_MMA(0, 1, fb1)
+    readA(st, 1);
+    if (pf) dmaB(1, st, kf);
+    NR_PHASE_SYNC_MMA(1, 1, fb1)
+    if (pf) {""",
+         """    NR_PHASE_SYNC_MMA(0, 1, fy)
+    readA(st, 1);
+    if (pf) dmaB(1, st, kf);
+    if (nx) {
+      if (pf) __builtin_amdgcn_s_waitcnt(kVmcnt10);  // step kt + 1's B0 quarter landed (10+ younger pieces)
+      else __builtin_amdgcn_s_waitcnt(kVmcnt0);
+    }
+    NR_PHASE_SYNC_MMA(1, 1, fy)
+    if (kt + 1 < nk) readB(st ^ 1, 0, fy);  // step kt + 1's B0 (read after the barrier that follows every wave's wait)
+    if (pf) {"""),
+        ("""    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+    mma(1, 0, fb0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };""",
+         """    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+    mma(1, 0, fx);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };"""),
+        ("""  if (wmu == 1) __builtin_amdgcn_s_barrier();  // skew the wave groups by one barrier
+  int st = 0;
+  while (true) {""",
+         """  if (wmu == 1) __builtin_amdgcn_s_barrier();  // skew the wave groups by one barrier
+  int st = 0;
+  const int t_first = t;
+  readB(0, 0, fb0);
+  while (true) {"""),
+        ("""    for (int kt = 0; kt < nk; ++kt) {
+      kstep(kt, st, more, nm0, nn0);
+      st ^= 1;
+    }
+
+    if (wmu == 0) __builtin_amdgcn_s_barrier();  // realign: group 1 has finished its last MFMA phase""",
+         """    if (t != t_first) readB(st, 0, fb0);  // the tile's step-0 B0 (not held through the epilogue)
+    for (int kt = 0; kt < nk; kt += 2) {  // nk even (host)
+      kstep(kt, st, more, nm0, nn0, fb0, fb1);
+      kstep(kt + 1, st ^ 1, more, nm0, nn0, fb1, fb0);
+    }
+
+    if (wmu == 0) __builtin_amdgcn_s_barrier();  // realign: group 1 has finished its last MFMA phase"""),
+        ("  return K >= 128 && M * lda * 2 <= kMax && N * ldw * 2 <= kMax;",
+         "  return K >= 128 && K % 128 == 0 && M * lda * 2 <= kMax && N * ldw * 2 <= kMax;"),
+    ],
     # DIAGNOSTIC (wrong results): no operand DMAs inside the K loop
     "nodma": [
         ("  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {\n    const int ns = st ^ 1;\n"
