@@ -17,6 +17,8 @@
 // the MFMAs of tile k, one barrier per K tile.
 #include "nr_common.h"
 
+#include <atomic>
+
 
 namespace nr {
 
@@ -1765,30 +1767,34 @@ __global__ __launch_bounds__(256, 1) void gemm256w4_kernel(int64_t M, int64_t N,
 // Workgroups of a persistent GEMM launch: the device's CU count rounded down
 // to a multiple of the 8 XCDs, unless the caller has set a budget for a
 // CU-masked stream (nr_set_persistent_workgroups).
-static int g_persist_wgs = 0;
+// Process-wide knobs are atomics: the C-ABI is callable from several host
+// threads at once (one stream each).
+static std::atomic<int> g_persist_wgs{0};
 
 extern "C" int nr_set_persistent_workgroups(int n) {
   if (n < 0 || n % 8) {
     set_error("nr_set_persistent_workgroups: n=%d must be 0 or a positive multiple of 8", n);
     return NR_ERR_INVALID;
   }
-  g_persist_wgs = n;
+  g_persist_wgs.store(n);
   return NR_OK;
 }
 
-extern "C" int nr_persistent_workgroups(void) { return g_persist_wgs; }
+extern "C" int nr_persistent_workgroups(void) { return g_persist_wgs.load(); }
 
 static int num_cus() {
-  if (g_persist_wgs) return g_persist_wgs;
-  static int n_cu = 0;
-  if (!n_cu) {
+  if (const int b = g_persist_wgs.load()) return b;
+  static std::atomic<int> n_cu{0};  // racing first calls store the same value
+  int c = n_cu.load(std::memory_order_relaxed);
+  if (!c) {
     int dev = 0;
     hipDeviceProp_t prop;
     const int n = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
                       ? prop.multiProcessorCount : 256;
-    n_cu = n >= 8 ? n / 8 * 8 : 8;
+    c = n >= 8 ? n / 8 * 8 : 8;
+    n_cu.store(c, std::memory_order_relaxed);
   }
-  return n_cu;
+  return c;
 }
 
 // The persistent kernel's operand stream needs >= 2 K steps per tile and
@@ -2106,7 +2112,7 @@ __global__ __launch_bounds__(256) void tail_fixup_kernel(int64_t rows, int64_t N
 // row's bits depend on how the table is cut into chunks / rank shards (round-3
 // GPU run: the chunked one-rank RCCL transform differed from one launch), for
 // ~15 us per K = 4096 GEMM (profiles/round3/split_tail_ab.jsonl)
-static int g_split_tail = 0;
+static std::atomic<int> g_split_tail{0};
 
 // Scratch the split tail may need (f32 partials), for any M: at most #CUs tiles
 // of 256 x 256 f32 are in the tail's slices.
@@ -2133,7 +2139,7 @@ int gemm_split_tail_dispatch(int epi, bool lnf, int64_t M, int64_t N, int64_t K,
   const int ncu = num_cus();
   const int64_t ntn = N / G2BN;
   const int64_t ntm = (M + G2BM - 1) / G2BM;
-  if (!g_split_tail || N % G2BN || K < 4096 || ntn > ncu || ncu % ntn) return whole(M, 0);
+  if (!g_split_tail.load() || N % G2BN || K < 4096 || ntn > ncu || ncu % ntn) return whole(M, 0);
   const int64_t per_round = ncu / ntn;                 // M-tiles per full round
   const int64_t ntm_main = ntm / per_round * per_round;
   const int64_t tail_tiles = (ntm - ntm_main) * ntn;
@@ -2195,7 +2201,7 @@ int gemm_split_tail_dispatch(int epi, bool lnf, int64_t M, int64_t N, int64_t K,
 }  // namespace nr
 
 extern "C" int nr_set_split_tail(int on) {
-  nr::g_split_tail = on ? 1 : 0;
+  nr::g_split_tail.store(on ? 1 : 0);
   return NR_OK;
 }
 
