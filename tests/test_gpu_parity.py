@@ -666,3 +666,47 @@ def test_full_size_shared_histories_dedupe_bit_identical(gpu_device):
         out[mode] = s.cpu()
         del eng
     assert torch.equal(out[None], out[False])
+
+
+def test_threads_on_their_own_streams_bit_identical(gpu_device):
+    """SURVEY §8(b) threading contract: C-ABI calls are reentrant across host
+    threads and streams (caller-owned workspaces, thread-local error strings
+    and residency caches, atomic process-wide knobs).  Two engines (latent and
+    FinalAttention, bf16), each driven by its own host thread on its own
+    stream for three full passes at once (transform + inverse norms +
+    pool/score: persistent GEMMs of both engines share the CUs), give the
+    scores of a serial pass bit for bit."""
+    import threading
+    imps = synthetic.mind_impressions(3000, 4000, seed=21)
+    table = W.news_table(21, 3000, 1024, name="threads")
+    engines, want = [], []
+    for pooler in ("latent", "final"):
+        eng = PoolScoreEngine(_model(pooler, gpu_device, 21), dtype=torch.bfloat16, device=gpu_device).load_news(table)
+        eng.load_impressions(imps.hist_idx, imps.hist_len, imps.cand_idx, imps.cand_len, dedupe=False)
+        s, _ = eng.step()
+        torch.cuda.synchronize()
+        engines.append(eng)
+        want.append(s.clone())
+    got, errs = [[None] * 3 for _ in engines], []
+
+    def run(k):
+        try:
+            st = torch.cuda.Stream(device=gpu_device)
+            with torch.cuda.stream(st):
+                for r in range(3):
+                    s, _ = engines[k].step()
+                    got[k][r] = s.clone()
+            st.synchronize()
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(len(engines))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    torch.cuda.synchronize()
+    assert not errs, errs
+    for k in range(len(engines)):
+        for r in range(3):
+            assert torch.equal(got[k][r], want[k]), (k, r)
