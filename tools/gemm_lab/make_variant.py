@@ -295,6 +295,42 @@ VARIANTS = {
         ("  return K >= 128 && M * lda * 2 <= kMax && N * ldw * 2 <= kMax;",
          "  return K >= 128 && K % 128 == 0 && M * lda * 2 <= kMax && N * ldw * 2 <= kMax;"),
     ],
+    # on top of the shipped spread (P1 A1', P2 A0, P3 B0, P4 B1): B0 moved to the read-free P4
+    "dma4": [
+        ("""    readA(st, 1);
+    if (pf) dmaB(0, st, kf);
+    NR_PHASE_SYNC_MMA(1, 1, fb1)
+    if (pf) {
+      dmaB(1, st, kf);""",
+         """    readA(st, 1);
+    NR_PHASE_SYNC_MMA(1, 1, fb1)
+    if (pf) {
+      dmaB(0, st, kf);
+      dmaB(1, st, kf);"""),
+    ],
+    # dma4 + the deferred A1 in P2 instead of P1 (P1: 12 reads only; P2: 4 reads + A1' + A0; P3: 8 reads; P4: B0 + B1)
+    "dma6": [
+        ("""    readB(st, 0, fb0);
+    if (a1p) dmaA(1, st ^ 1, a1k);
+    NR_PHASE_SYNC_MMA(0, 0, fb0)
+    readB(st, 1, fb1);
+    if (pf) {""",
+         """    readB(st, 0, fb0);
+    NR_PHASE_SYNC_MMA(0, 0, fb0)
+    readB(st, 1, fb1);
+    if (a1p) dmaA(1, st ^ 1, a1k);
+    if (pf) {"""),
+        ("""    readA(st, 1);
+    if (pf) dmaB(0, st, kf);
+    NR_PHASE_SYNC_MMA(1, 1, fb1)
+    if (pf) {
+      dmaB(1, st, kf);""",
+         """    readA(st, 1);
+    NR_PHASE_SYNC_MMA(1, 1, fb1)
+    if (pf) {
+      dmaB(0, st, kf);
+      dmaB(1, st, kf);"""),
+    ],
     # DIAGNOSTIC (wrong results): no operand DMAs inside the K loop
     "nodma": [
         ("  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {\n    const int ns = st ^ 1;\n"
