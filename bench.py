@@ -289,6 +289,39 @@ def config2_leg(dev, n_news: int = 8192) -> dict:
     return out
 
 
+def hipblaslt_yardstick(pooler: str, n: int, ours_ms: float, dev, reps: int = 5) -> dict:
+    """The same per-news transform GEMM shapes (M = n) as bare torch.matmul
+    (hipBLASLt: bf16, no bias, no LayerNorm, no epilogue, so less work than
+    the fused transform) summed, beside the fused transform's own time: a
+    vendor-library yardstick for transform_peak_frac.  Yardstick only; the
+    product path never calls it."""
+    shapes = ([(4096, 1024), (4096, 4096), (1024, 4096), (4096, 1024), (1024, 4096)] if pooler == "final" else
+              [(512, 1024), (1024, 512), (8192, 1024), (1024, 4096)])  # (N, K); latent ff1 = GEGLU's 2F
+    g = torch.Generator(device=dev).manual_seed(7)
+    tot = 0.0
+    per = []
+    for nn, kk in shapes:
+        a = torch.randn((n, kk), device=dev, generator=g).bfloat16()
+        w = torch.randn((nn, kk), device=dev, generator=g).bfloat16()
+        torch.matmul(a, w.T)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            torch.matmul(a, w.T)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        per.append(round(ms, 4))
+        tot += ms
+        del a, w
+    torch.cuda.empty_cache()
+    fl = tx_flops(n, pooler)
+    return {"shapes_NK": shapes, "hipblaslt_ms_each": per, "hipblaslt_sum_ms": round(tot, 4),
+            "hipblaslt_peak_frac": round(fl / (tot * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS["bf16"], 3),
+            "fused_transform_ms": round(float(ours_ms), 4), "fused_over_hipblaslt_time": round(ours_ms / tot, 3)}
+
+
 def encoder_bf16_leg(dev, n_news: int = 16384) -> dict:
     """BASELINE configs[2]'s embedding step in bf16: the 24-layer XLM-R-large-
     shaped title encoder (packed varlen, nr_encoder_forward) over n_news
@@ -676,6 +709,8 @@ def main():
         extra["shared_histories"] = sh
         del im
         extra["metrics_ms"] = round(metrics_ms(head), 3)
+        if args.dtype == "bf16":
+            extra["transform_vs_hipblaslt"] = hipblaslt_yardstick(args.pooler, n_news, head.split_ms[0], dev)
         # PCIe-side costs (never part of `value`): the CSR index upload incl. its host-side
         # offsets (load_impressions is idempotent) and the score download
         torch.cuda.synchronize()
