@@ -17,6 +17,10 @@
  *    are graph-capturable.
  *  - Return NR_OK (0) or a negative code; nr_last_error() returns the
  *    thread-local message of the last failure.  No exception crosses the ABI.
+ *  - Reentrant: host threads may call concurrently, each on its own stream
+ *    (scratch is the caller's workspace; error strings and residency caches
+ *    are thread-local; the two process-wide knobs below are atomics).  A
+ *    row's output bits do not depend on how the rows were cut into calls.
  *  - Matrices are row-major with explicit leading dimensions in ELEMENTS.
  *    Linear weights use torch's nn.Linear layout W[out_features][in_features],
  *    so GEMMs compute C = A · Wᵀ.
@@ -82,8 +86,8 @@ int nr_init(int device);
  * For callers that run the transform on a CU-masked stream beside other
  * work (hipExtStreamCreateWithCUMask): set it to the stream's CU count.
  * n = 0 restores the default; otherwise n must be a positive multiple of 8
- * (the kernel maps blockIdx % 8 to an XCD).  Process-wide, not thread-safe
- * against concurrent launches. */
+ * (the kernel maps blockIdx % 8 to an XCD).  Process-wide (an atomic): a
+ * launch on another thread uses whichever value it reads. */
 int nr_set_persistent_workgroups(int n);
 
 /* The current budget (0 = the default, one workgroup per CU), so a caller can
