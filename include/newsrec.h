@@ -413,6 +413,25 @@ int nr_col_sum(int dtype, int64_t rows, int64_t cols, const void* src, int64_t l
 int nr_ln_param_grad(int dtype_in, int64_t n, int64_t dim, const void* x, int64_t ldx, const int64_t* row_idx,
                      float eps, const float* dy, int64_t lddy, float* dgamma, float* dbeta, void* stream);
 
+/* LatentAttentionModel training (f32; latent_attention.py:157-163 through autograd):
+ * PreNorm LayerNorm input gradient (stats recomputed from x, dim 1024):
+ * dx = rstd (dxh - mean(dxh) - xhat mean(dxh xhat)) [+ dres], dxh = dy gamma
+ * (gamma NULL = 1; dres may alias dx). */
+int nr_layernorm_bwd(int64_t n, int64_t dim, const float* x, int64_t ldx, const float* gamma, float eps,
+                     const float* dy, int64_t lddy, const float* dres, int64_t ldr, float* dx, int64_t lddx,
+                     void* stream);
+
+/* Softmax backward over groups of 64 columns (one head's 64 latents):
+ * ds = p (dp - sum_group(p dp)). */
+int nr_softmax64_bwd(int64_t rows, int64_t cols, const float* p, int64_t ldp, const float* dp, int64_t lddp,
+                     float* ds, int64_t ldds, void* stream);
+
+/* GEGLU (latent_attention.py:24-27, exact-erf gelu): z = a gelu(g) with
+ * a = G[:, :f], g = G[:, f:]; backward dG = [dz gelu(g), dz a gelu'(g)]. */
+int nr_geglu_fwd(int64_t rows, int64_t f, const float* g, int64_t ldg, float* z, int64_t ldz, void* stream);
+int nr_geglu_bwd(int64_t rows, int64_t f, const float* g, int64_t ldg, const float* dz, int64_t lddz, float* dg,
+                 int64_t lddg, void* stream);
+
 /* *out += sum x^2 (the global grad norm of clip_grad_norm_, trainer.py:1067-1071). */
 int nr_sumsq(int64_t n, const float* x, float* out, void* stream);
 

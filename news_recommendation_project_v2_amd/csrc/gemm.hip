@@ -766,7 +766,7 @@ __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t v) {  // v_pk_max_i16 w
 // not inline asm, so the compiler's own wait insertion sees them: it then knows
 // the older stores have retired and keeps its waits for the epilogue's
 // residual loads counted instead of vmcnt(0).
-constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78, kVmcnt11 = 0x0F7B, kVmcnt6 = 0x0F76, kVmcnt9 = 0x0F79;
+constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78, kVmcnt6 = 0x0F76, kVmcnt9 = 0x0F79;
 
 // LNF (LayerNorm folded into the epilogue): per tile, every wave's (u, c)
 // column slices (2 x 256 B) and the tile's 256 row stats (2 KiB), in two

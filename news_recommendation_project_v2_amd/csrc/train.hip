@@ -354,6 +354,122 @@ __global__ __launch_bounds__(256) void ln_param_grad_kernel(int64_t n, const TI*
   }
 }
 
+// ----------------------------------------------------------------- latent attention training (f32)
+// Per-item pieces of LatentAttentionModel's backward (latent_attention.py:157-163):
+// PreNorm LayerNorm input gradient, the per-head softmax (64 latents) backward,
+// and GEGLU forward / backward (x, gates = chunk(2); x * gelu(gates), exact erf).
+
+// dx = rstd (dxh - mean(dxh) - xhat mean(dxh xhat)) + dres,  dxh = dy * gamma;
+// one wave per row (D = 1024, 16 columns per lane), stats recomputed from x
+// with the forward's two-pass arithmetic.  dres may alias dx (in place).
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(int64_t n, const float* __restrict__ x, int64_t ldx,
+                                                            const float* __restrict__ gamma, float eps,
+                                                            const float* __restrict__ dy, int64_t lddy,
+                                                            const float* dres, int64_t ldr, float* dx,
+                                                            int64_t lddx) {
+  constexpr int D = 1024, NJ = D / 256;
+  const int lane = threadIdx.x & 63;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (int64_t)gridDim.x * 4) {
+    float v[NJ][4], g[NJ][4];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const float4 a = *reinterpret_cast<const float4*>(x + row * ldx + j * 256 + lane * 4);
+      v[j][0] = a.x; v[j][1] = a.y; v[j][2] = a.z; v[j][3] = a.w;
+      s += (a.x + a.y) + (a.z + a.w);
+    }
+    const float mean = wave_sum(s) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { const float d = v[j][t] - mean; q = fmaf(d, d, q); }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const float4 d4 = *reinterpret_cast<const float4*>(dy + row * lddy + j * 256 + lane * 4);
+      const float4 g4 = gamma ? *reinterpret_cast<const float4*>(gamma + j * 256 + lane * 4)
+                              : float4{1.f, 1.f, 1.f, 1.f};
+      const float dd[4] = {d4.x, d4.y, d4.z, d4.w}, gg[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        v[j][t] = (v[j][t] - mean) * rstd;  // xhat
+        g[j][t] = dd[t] * gg[t];            // dxhat
+        s1 += g[j][t];
+        s2 = fmaf(g[j][t], v[j][t], s2);
+      }
+    }
+    const float m1 = wave_sum(s1) / (float)D, m2 = wave_sum(s2) / (float)D;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float o[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t] = rstd * (g[j][t] - m1 - v[j][t] * m2);
+      if (dres) {
+        const float4 r4 = *reinterpret_cast<const float4*>(dres + row * ldr + j * 256 + lane * 4);
+        o[0] += r4.x; o[1] += r4.y; o[2] += r4.z; o[3] += r4.w;
+      }
+      *reinterpret_cast<float4*>(dx + row * lddx + j * 256 + lane * 4) = float4{o[0], o[1], o[2], o[3]};
+    }
+  }
+}
+
+// dS = P * (dP - sum_group(P * dP)) over groups of 64 columns (one head's
+// latents; SDPA softmax, latent_attention.py:72).  One wave per (row, group).
+__global__ __launch_bounds__(256) void softmax64_bwd_kernel(int64_t n_groups, int64_t groups_per_row,
+                                                            const float* __restrict__ p, int64_t ldp,
+                                                            const float* __restrict__ dp, int64_t lddp,
+                                                            float* __restrict__ ds, int64_t ldds) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t gi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); gi < n_groups; gi += (int64_t)gridDim.x * 4) {
+    const int64_t row = gi / groups_per_row, col = (gi % groups_per_row) * 64 + lane;
+    const float pv = p[row * ldp + col], dv = dp[row * lddp + col];
+    const float dot = wave_sum(pv * dv);
+    ds[row * ldds + col] = pv * (dv - dot);
+  }
+}
+
+__device__ __forceinline__ float gelu_exact(float g) { return 0.5f * g * (1.0f + erff(g * 0.70710678118654752440f)); }
+
+// z[:, j] = a_j * gelu(g_j),  a = G[:, :F], g = G[:, F:]  (GEGLU, latent_attention.py:24-27)
+__global__ __launch_bounds__(256) void geglu_fwd_kernel(int64_t rows, int64_t f, const float* __restrict__ G,
+                                                        int64_t ldg, float* __restrict__ z, int64_t ldz) {
+  const int64_t total = rows * f;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < total; i += (int64_t)gridDim.x * 1024) {
+    const int64_t r = i / f, c = i % f;  // f % 4 == 0: the 4 columns share a row
+    const float4 a = *reinterpret_cast<const float4*>(G + r * ldg + c);
+    const float4 g = *reinterpret_cast<const float4*>(G + r * ldg + f + c);
+    *reinterpret_cast<float4*>(z + r * ldz + c) =
+        float4{a.x * gelu_exact(g.x), a.y * gelu_exact(g.y), a.z * gelu_exact(g.z), a.w * gelu_exact(g.w)};
+  }
+}
+
+// dG[:, j] = dz_j gelu(g_j);  dG[:, F + j] = dz_j a_j gelu'(g_j),
+// gelu'(g) = Phi(g) + g phi(g)  (the derivative torch's gelu backward uses)
+__global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t rows, int64_t f, const float* __restrict__ G,
+                                                        int64_t ldg, const float* __restrict__ dz, int64_t lddz,
+                                                        float* __restrict__ dG, int64_t lddg) {
+  const int64_t total = rows * f;
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < total; i += (int64_t)gridDim.x * 1024) {
+    const int64_t r = i / f, c = i % f;
+    const float4 a4 = *reinterpret_cast<const float4*>(G + r * ldg + c);
+    const float4 g4 = *reinterpret_cast<const float4*>(G + r * ldg + f + c);
+    const float4 d4 = *reinterpret_cast<const float4*>(dz + r * lddz + c);
+    const float a[4] = {a4.x, a4.y, a4.z, a4.w}, g[4] = {g4.x, g4.y, g4.z, g4.w}, d[4] = {d4.x, d4.y, d4.z, d4.w};
+    float da[4], dg[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float cdf = 0.5f * (1.0f + erff(g[t] * 0.70710678118654752440f));
+      const float pdf = 0.39894228040143267794f * expf(-0.5f * g[t] * g[t]);
+      da[t] = d[t] * g[t] * cdf;
+      dg[t] = d[t] * a[t] * (cdf + g[t] * pdf);
+    }
+    *reinterpret_cast<float4*>(dG + r * lddg + c) = float4{da[0], da[1], da[2], da[3]};
+    *reinterpret_cast<float4*>(dG + r * lddg + f + c) = float4{dg[0], dg[1], dg[2], dg[3]};
+  }
+}
+
 // ----------------------------------------------------------------- grad norm + AdamW
 // Sum of squares: 16-B lane loads, grid-stride over <= 1024 blocks, block
 // reduction in LDS, ONE atomic per block (per-wave atomics on a single address
@@ -677,5 +793,79 @@ extern "C" int nr_splitk_fixup(int dtype_out, int epilogue, int64_t rows, int64_
   else NR_FIX(NR_EPI_NONE);
 #undef NR_FIX
   NR_CHECK_LAUNCH("nr_splitk_fixup");
+  return NR_OK;
+}
+
+static unsigned rowwave_grid(int64_t units) {  // 4 waves (units) per block, <= 2048 blocks, grid-strided
+  const int64_t b = (units + 3) / 4;
+  return (unsigned)(b < 2048 ? (b > 0 ? b : 1) : 2048);
+}
+
+extern "C" int nr_layernorm_bwd(int64_t n, int64_t dim, const float* x, int64_t ldx, const float* gamma, float eps,
+                                const float* dy, int64_t lddy, const float* dres, int64_t ldr, float* dx,
+                                int64_t lddx, void* stream) {
+  clear_error();
+  NR_CHECK_ARG(dim == 1024, "nr_layernorm_bwd: dim %lld unsupported", (long long)dim);
+  NR_CHECK_ARG(n >= 0 && ldx >= dim && lddy >= dim && lddx >= dim && (!dres || ldr >= dim), "nr_layernorm_bwd: bad args");
+  if (n == 0) return NR_OK;
+  NR_CHECK_ARG(x && dy && dx, "nr_layernorm_bwd: null pointer");
+  NR_CHECK_DEVICE("nr_layernorm_bwd", x, gamma, dy, dres, dx);
+  NR_CHECK_ARG(ldx % 4 == 0 && lddy % 4 == 0 && lddx % 4 == 0 && (!dres || ldr % 4 == 0) &&
+                   (((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)dres | (uintptr_t)gamma) & 15) == 0,
+               "nr_layernorm_bwd: rows must be 16-byte aligned");
+  hipLaunchKernelGGL(layernorm_bwd_kernel, dim3(rowwave_grid(n)), dim3(256), 0, (hipStream_t)stream, n, x, ldx, gamma,
+                     eps, dy, lddy, dres, ldr, dx, lddx);
+  NR_CHECK_LAUNCH("nr_layernorm_bwd");
+  return NR_OK;
+}
+
+extern "C" int nr_softmax64_bwd(int64_t rows, int64_t cols, const float* p, int64_t ldp, const float* dp,
+                                int64_t lddp, float* ds, int64_t ldds, void* stream) {
+  clear_error();
+  NR_CHECK_ARG(rows >= 0 && cols > 0 && cols % 64 == 0 && ldp >= cols && lddp >= cols && ldds >= cols,
+               "nr_softmax64_bwd: bad args (cols must be a multiple of 64)");
+  if (rows == 0) return NR_OK;
+  NR_CHECK_ARG(p && dp && ds, "nr_softmax64_bwd: null pointer");
+  NR_CHECK_DEVICE("nr_softmax64_bwd", p, dp, ds);
+  const int64_t gpr = cols / 64, ng = rows * gpr;
+  hipLaunchKernelGGL(softmax64_bwd_kernel, dim3(rowwave_grid(ng)), dim3(256), 0, (hipStream_t)stream, ng, gpr, p, ldp,
+                     dp, lddp, ds, ldds);
+  NR_CHECK_LAUNCH("nr_softmax64_bwd");
+  return NR_OK;
+}
+
+static unsigned elem4_grid(int64_t total) {
+  const int64_t b = (total / 4 + 255) / 256;
+  return (unsigned)(b < 4096 ? (b > 0 ? b : 1) : 4096);
+}
+
+extern "C" int nr_geglu_fwd(int64_t rows, int64_t f, const float* g, int64_t ldg, float* z, int64_t ldz,
+                            void* stream) {
+  clear_error();
+  NR_CHECK_ARG(rows >= 0 && f > 0 && f % 4 == 0 && ldg >= 2 * f && ldz >= f && ldg % 4 == 0 && ldz % 4 == 0,
+               "nr_geglu_fwd: bad args");
+  if (rows == 0) return NR_OK;
+  NR_CHECK_ARG(g && z, "nr_geglu_fwd: null pointer");
+  NR_CHECK_DEVICE("nr_geglu_fwd", g, z);
+  NR_CHECK_ARG((((uintptr_t)g | (uintptr_t)z) & 15) == 0, "nr_geglu_fwd: 16-byte alignment required");
+  hipLaunchKernelGGL(geglu_fwd_kernel, dim3(elem4_grid(rows * f)), dim3(256), 0, (hipStream_t)stream, rows, f, g, ldg,
+                     z, ldz);
+  NR_CHECK_LAUNCH("nr_geglu_fwd");
+  return NR_OK;
+}
+
+extern "C" int nr_geglu_bwd(int64_t rows, int64_t f, const float* g, int64_t ldg, const float* dz, int64_t lddz,
+                            float* dg, int64_t lddg, void* stream) {
+  clear_error();
+  NR_CHECK_ARG(rows >= 0 && f > 0 && f % 4 == 0 && ldg >= 2 * f && lddz >= f && lddg >= 2 * f && ldg % 4 == 0 &&
+                   lddz % 4 == 0 && lddg % 4 == 0,
+               "nr_geglu_bwd: bad args");
+  if (rows == 0) return NR_OK;
+  NR_CHECK_ARG(g && dz && dg, "nr_geglu_bwd: null pointer");
+  NR_CHECK_DEVICE("nr_geglu_bwd", g, dz, dg);
+  NR_CHECK_ARG((((uintptr_t)g | (uintptr_t)dz | (uintptr_t)dg) & 15) == 0, "nr_geglu_bwd: 16-byte alignment required");
+  hipLaunchKernelGGL(geglu_bwd_kernel, dim3(elem4_grid(rows * f)), dim3(256), 0, (hipStream_t)stream, rows, f, g, ldg,
+                     dz, lddz, dg, lddg);
+  NR_CHECK_LAUNCH("nr_geglu_bwd");
   return NR_OK;
 }

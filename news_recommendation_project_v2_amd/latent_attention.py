@@ -92,6 +92,82 @@ def lnfold_weights(w: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, bia
     return {f"W{tag}_ln": wf.contiguous(), f"uc{tag}": torch.stack([u, c]).to(torch.float32).contiguous()}
 
 
+def _pad64(n: int) -> int:
+    return max(64, (n + 63) // 64 * 64)
+
+
+class _LatentItemFn(torch.autograd.Function):
+    """Per-item hiddens of LatentAttentionModel (latent_attention.py:157-163) with
+    their backward on the HIP kernels, f32 (exact-f32 MFMA GEMMs), over packed
+    valid rows padded with zeros to a multiple of 64 (the weight-grad GEMMs' K):
+
+      X  = LN_q(E)                          nr_layernorm
+      P  = softmax64(X Aᵀ)                  nr_gemm SOFTMAX64   (A = the folded K·W_q / √512, [512, D])
+      H1 = P Btᵀ + E                        nr_gemm RESADD      (Bt = the folded W_o·Vᵀ, [D, 512])
+      Y  = LN_f(H1);  G = Y W1ᵀ + b1        nr_layernorm, nr_gemm
+      Z  = a ⊙ gelu(g), (a, g) = G.chunk(2) nr_geglu_fwd
+      H  = Z W2ᵀ + b2 + H1                  nr_gemm RESADD
+
+    Backward: data grads through transposed weights (nr_transpose + nr_gemm),
+    nr_geglu_bwd, nr_softmax64_bwd, nr_layernorm_bwd (the residual grads added
+    in the same pass), weight grads dOutᵀ·In as one grouped GEMM, bias and LN
+    parameter grads by column sums / nr_ln_param_grad.  A and Bt are built from
+    the module's parameters by differentiable torch ops (LatentAttentionModel.
+    _fold_train: 64-latent weight algebra, the reference's own to_kv(latents)),
+    so autograd carries dA and dBt on to latents, norm_context, to_q, to_kv and
+    to_out.  The padding rows carry zero gradient."""
+
+    @staticmethod
+    def forward(ctx, rows, A, Bt, gq, bq, gf, bf, W1, b1, W2, b2):
+        Hs, D = rows.shape
+        Hp = _pad64(Hs)
+        dev = rows.device
+        E = torch.zeros((Hp, D), dtype=torch.float32, device=dev)
+        E[:Hs] = rows
+        A, Bt, W1, W2 = A.contiguous(), Bt.contiguous(), W1.contiguous(), W2.contiguous()
+        X = ops.layernorm(E, gq.contiguous(), bq.contiguous(), 1e-5)
+        P = ops.gemm(X, A, None, epilogue="softmax64")
+        H1 = ops.gemm(P, Bt, None, epilogue="resadd", residual=E)
+        Y = ops.layernorm(H1, gf.contiguous(), bf.contiguous(), 1e-5)
+        G = ops.gemm(Y, W1, b1.contiguous())
+        Z = ops.geglu_fwd(G)
+        H = ops.gemm(Z, W2, b2.contiguous(), epilogue="resadd", residual=H1)
+        ctx.save_for_backward(E, X, P, H1, Y, G, Z, A, Bt, gq, gf, W1, W2)
+        ctx.Hs = Hs
+        return H[:Hs]
+
+    @staticmethod
+    def backward(ctx, dH):
+        E, X, P, H1, Y, G, Z, A, Bt, gq, gf, W1, W2 = ctx.saved_tensors
+        Hs = ctx.Hs
+        Hp, D = E.shape
+        dev = E.device
+        dHp = torch.zeros((Hp, D), dtype=torch.float32, device=dev)
+        dHp[:Hs] = dH.float()
+        T = ops.transpose
+        dZ = ops.gemm(dHp, T(W2))
+        dG = ops.geglu_bwd(G, dZ)
+        dY = ops.gemm(dG, T(W1))
+        dH1 = ops.layernorm_bwd(H1, gf.contiguous(), dY, 1e-5, residual=dHp)
+        dP = ops.gemm(dH1, T(Bt))
+        dS = ops.softmax64_bwd(P, dP)
+        dX = ops.gemm(dS, T(A))
+        dE = ops.layernorm_bwd(E, gq.contiguous(), dX, 1e-5, residual=dH1)
+        gW2 = torch.empty(W2.shape, dtype=torch.float32, device=dev)
+        gW1 = torch.empty(W1.shape, dtype=torch.float32, device=dev)
+        gBt = torch.empty(Bt.shape, dtype=torch.float32, device=dev)
+        gA = torch.empty(A.shape, dtype=torch.float32, device=dev)
+        ops.gemm_grouped([(T(dHp), T(Z), gW2), (T(dG), T(Y), gW1), (T(dH1), T(P), gBt), (T(dS), T(X), gA)])
+        gb2 = torch.zeros(D, dtype=torch.float32, device=dev)
+        gb1 = torch.zeros(W1.shape[0], dtype=torch.float32, device=dev)
+        ops.col_sum(dHp, gb2)
+        ops.col_sum(dG, gb1)
+        ggf, gbf, ggq, gbq = (torch.zeros(D, dtype=torch.float32, device=dev) for _ in range(4))
+        ops.ln_param_grad(H1, None, 1e-5, dY, ggf, gbf)
+        ops.ln_param_grad(E, None, 1e-5, dX, ggq, gbq)
+        return dE[:Hs], gA, gBt, ggq, gbq, ggf, gbf, gW1, gb1, gW2, gb2
+
+
 class LatentAttentionModel(torch.nn.Module):
     """forward(embeddings [B, L, D], attention_mask [B, L] | None).
 
@@ -182,14 +258,54 @@ class LatentAttentionModel(torch.nn.Module):
         dtype = dtype or rows.dtype
         return ops.latent_transform(rows.to(dtype).contiguous(), self.hip_weights(dtype))
 
+    def _fold_train(self):
+        """A [h*64, D] and Bt [D, h*64] of the fold (module doc) as differentiable
+        f32 device ops on the parameters: the reference's to_kv(LN_c(latents))
+        (latent_attention.py:161-162) once per batch instead of once per row."""
+        attn_blk = self.cross_attend_blocks[0]
+        attn = attn_blk.fn
+        h = attn.heads
+        lat_n = torch.nn.functional.layer_norm(self.latents, self.latents.shape[-1:], attn_blk.norm_context.weight,
+                                               attn_blk.norm_context.bias, attn_blk.norm_context.eps)
+        kv = lat_n @ attn.to_kv.weight.T                              # [nl, 2 inner]
+        inner = kv.shape[1] // 2
+        dh = inner // h
+        nl, d = self.latents.shape[0], attn.to_q.weight.shape[1]
+        k = kv[:, :inner].reshape(nl, h, dh).permute(1, 0, 2)        # [h, nl, dh]
+        v = kv[:, inner:].reshape(nl, h, dh).permute(1, 2, 0)        # [h, dh, nl]
+        a = torch.matmul(k, attn.to_q.weight.reshape(h, dh, d)) * (1.0 / math.sqrt(dh))   # [h, nl, D]
+        bt = torch.matmul(attn.to_out.weight.reshape(d, h, dh).permute(1, 0, 2), v)      # [h, D, nl]
+        return a.reshape(h * nl, d), bt.permute(1, 0, 2).reshape(d, h * nl)
+
+    def _train_items(self, rows: torch.Tensor) -> torch.Tensor:
+        params = list(self.parameters())
+        if any(p.dtype != torch.float32 for p in params):
+            raise NewsRecHIPError("LatentAttentionModel autograd path trains f32 parameters (as the reference does)")
+        attn_blk, ff_blk = self.cross_attend_blocks
+        A, Bt = self._fold_train()
+        ff = ff_blk.fn.net
+        return _LatentItemFn.apply(rows.float(), A, Bt, attn_blk.norm.weight, attn_blk.norm.bias, ff_blk.norm.weight,
+                                   ff_blk.norm.bias, ff[0].weight, ff[0].bias, ff[2].weight, ff[2].bias)
+
     def forward(self, embeddings: torch.Tensor, attention_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         if embeddings.device.type != "cuda":
             raise NewsRecHIPError("LatentAttentionModel.forward runs on the MI355X HIP path only (got a CPU tensor)")
         b, l, d = embeddings.shape
+        train = self.training or (torch.is_grad_enabled() and (embeddings.requires_grad or
+                                                               any(p.requires_grad for p in self.parameters())))
         if attention_mask is None:
-            table = self.item_table(embeddings.reshape(b * l, d).float())
+            rows = embeddings.reshape(b * l, d)
+            table = self._train_items(rows) if train else self.item_table(rows.float())
             return table.reshape(b, l, d)
         from .modeling_utils import flatten_valid, pool_rows
         rows, off = flatten_valid(embeddings, attention_mask)
-        table = self.item_table(rows.float())
-        return pool_rows("latent", table, off)
+        if not train:
+            return pool_rows("latent", self.item_table(rows.float()), off)
+        # autograd: per-item hiddens on the HIP kernels, then the reference's masked mean
+        # and F.normalize (latent_attention.py:166-170) on the [B, D] users
+        H = self._train_items(rows)
+        counts = off[1:] - off[:-1]
+        seg = torch.repeat_interleave(torch.arange(b, device=H.device), counts)
+        s = torch.zeros((b, d), dtype=H.dtype, device=H.device).index_add(0, seg, H)
+        u = s / counts.unsqueeze(1).to(H.dtype)
+        return torch.nn.functional.normalize(u, p=2, dim=-1) if self.output_normalize else u

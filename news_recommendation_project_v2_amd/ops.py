@@ -594,3 +594,54 @@ def adamw(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor, st
     _lib.call("nr_adamw", p.numel(), _ptr(p), _ptr(g), _ptr(m), _ptr(v), _ptr(p_bf16), step, ctypes.c_float(lr),
               ctypes.c_float(betas[0]), ctypes.c_float(betas[1]), ctypes.c_float(eps), ctypes.c_float(weight_decay),
               ctypes.c_float(max_norm), _ptr(sumsq_t), _stream(dev))
+
+
+def _f32(t: torch.Tensor, name: str) -> None:
+    if t.dtype != torch.float32:
+        raise _lib.NewsRecHIPError(f"{name}: the latent-attention training kernels take f32 (got {t.dtype})")
+
+
+def layernorm_bwd(x: torch.Tensor, gamma: Optional[torch.Tensor], dy: torch.Tensor, eps: float = 1e-5,
+                  residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Input gradient of LayerNorm(x; gamma) for upstream dy (+ residual grad), f32."""
+    for t, n in ((x, "x"), (dy, "dy")):
+        _f32(t, n)
+    out = torch.empty_like(x) if out is None else out
+    dev = _dev(x, gamma, dy, residual, out)
+    _lib.call("nr_layernorm_bwd", x.shape[0], x.shape[1], _ptr(x), _rowmajor(x, "x"), _ptr(gamma),
+              ctypes.c_float(eps), _ptr(dy), _rowmajor(dy, "dy"), _ptr(residual),
+              _rowmajor(residual, "residual") if residual is not None else 0, _ptr(out), _rowmajor(out, "out"),
+              _stream(dev))
+    return out
+
+
+def softmax64_bwd(p: torch.Tensor, dp: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dS of a softmax over groups of 64 columns, from its output p and upstream dp (f32)."""
+    _f32(p, "p")
+    _f32(dp, "dp")
+    out = torch.empty_like(p) if out is None else out
+    dev = _dev(p, dp, out)
+    _lib.call("nr_softmax64_bwd", p.shape[0], p.shape[1], _ptr(p), _rowmajor(p, "p"), _ptr(dp), _rowmajor(dp, "dp"),
+              _ptr(out), _rowmajor(out, "out"), _stream(dev))
+    return out
+
+
+def geglu_fwd(g: torch.Tensor) -> torch.Tensor:
+    """a * gelu(gates) with a, gates = g.chunk(2, -1) (f32, exact erf)."""
+    _f32(g, "g")
+    f = g.shape[1] // 2
+    z = torch.empty((g.shape[0], f), dtype=torch.float32, device=g.device)
+    dev = _dev(g, z)
+    _lib.call("nr_geglu_fwd", g.shape[0], f, _ptr(g), _rowmajor(g, "g"), _ptr(z), f, _stream(dev))
+    return z
+
+
+def geglu_bwd(g: torch.Tensor, dz: torch.Tensor) -> torch.Tensor:
+    _f32(g, "g")
+    _f32(dz, "dz")
+    f = g.shape[1] // 2
+    dg = torch.empty_like(g)
+    dev = _dev(g, dz, dg)
+    _lib.call("nr_geglu_bwd", g.shape[0], f, _ptr(g), _rowmajor(g, "g"), _ptr(dz), _rowmajor(dz, "dz"), _ptr(dg),
+              _rowmajor(dg, "dg"), _stream(dev))
+    return dg

@@ -1,0 +1,151 @@
+"""LatentAttentionModel trains through the reference's own module API, like
+FinalAttention (tests/test_final_attention_autograd.py): ``model.train()``,
+forward on padded embeddings + mask, ``loss.backward()``, clip, AdamW -- the
+per-item hiddens and their backward on the HIP kernels
+(latent_attention._LatentItemFn: nr_gemm / nr_layernorm / nr_geglu_fwd|bwd /
+nr_softmax64_bwd / nr_layernorm_bwd / grouped weight-grad GEMMs), the 64-latent
+K/V fold as differentiable weight algebra.  BASELINE configs[4] names a
+latent-attention backward; no reference script trains this module, so the
+oracle is torch autograd of the reference's forward as restated in
+oracle/pool_ref.latent_attention_forward (latent_attention.py:157-170, pinned
+to the reference's golden outputs by tests/test_oracle_golden.py).
+Tolerances as tests/test_train.py: outputs 1e-4, each gradient within 1e-3
+of its tensor's max."""
+import numpy as np
+import pytest
+import torch
+
+from news_recommendation_project_v2_amd import weights as W
+from news_recommendation_project_v2_amd.latent_attention import LatentAttentionModel
+from oracle import pool_ref
+
+
+def _batch(seed=0, lens=(11, 3, 1, 7, 2, 5), L=11, D=1024):
+    rng = np.random.default_rng(seed)
+    B = len(lens)
+    mask = np.zeros((B, L), dtype=np.int64)
+    for b, n in enumerate(lens):
+        mask[b, :n] = 1
+    emb = (rng.standard_normal((B, L, D)) * mask[..., None]).astype(np.float32)
+    return torch.from_numpy(emb), torch.from_numpy(mask)
+
+
+def _rel_close(got, want, name, tol=1e-3):
+    got, want = got.detach().cpu().float(), want.detach().cpu().float()
+    scale = float(want.abs().max()) or 1.0
+    err = float((got - want).abs().max())
+    assert err <= tol * scale, f"{name}: max |d| {err:.3e} vs max |ref| {scale:.3e}"
+
+
+def _model(dev, sd):
+    m = LatentAttentionModel()
+    m.load_state_dict(sd)
+    return m.to(dev).train()
+
+
+@pytest.mark.gpu
+def test_latent_attention_backward_matches_oracle(gpu_device):
+    sd = W.latent_attention_state_dict(1234, ln_random=True)
+    m = _model(gpu_device, sd)
+    emb, mask = _batch()
+    R = torch.randn(emb.shape[0], 1024, generator=torch.Generator().manual_seed(3))
+    e_d = emb.to(gpu_device).requires_grad_(True)
+    out = m(e_d, mask.to(gpu_device))
+    (out * R.to(gpu_device)).sum().backward()
+
+    ref_sd = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    e_c = emb.clone().requires_grad_(True)
+    want = pool_ref.latent_attention_forward(ref_sd, e_c, mask)
+    (want * R).sum().backward()
+
+    _rel_close(out, want, "users", tol=1e-4)
+    _rel_close(e_d.grad, e_c.grad, "d embeddings")
+    for name, prm in m.named_parameters():
+        assert prm.grad is not None, name
+        _rel_close(prm.grad, ref_sd[name].grad, f"d {name}")
+
+
+@pytest.mark.gpu
+def test_latent_attention_unpooled_backward(gpu_device):
+    """mask=None (latent_attention.py:165: per-item hiddens [B, L, D]) through
+    autograd, 130 items (padding to 192 rows inside), vs the oracle."""
+    sd = W.latent_attention_state_dict(7, ln_random=True)
+    m = _model(gpu_device, sd)
+    g = torch.Generator().manual_seed(4)
+    emb = torch.randn(10, 13, 1024, generator=g)
+    R = torch.randn(10, 13, 1024, generator=g)
+    e_d = emb.to(gpu_device).requires_grad_(True)
+    out = m(e_d)
+    (out * R.to(gpu_device)).sum().backward()
+    ref_sd = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    e_c = emb.clone().requires_grad_(True)
+    want = pool_ref.latent_hiddens(ref_sd, e_c)
+    (want * R).sum().backward()
+    _rel_close(out, want, "hiddens", tol=1e-4)
+    _rel_close(e_d.grad, e_c.grad, "d embeddings")
+    for name, prm in m.named_parameters():
+        _rel_close(prm.grad, ref_sd[name].grad, f"d {name}")
+
+
+@pytest.mark.gpu
+def test_latent_attention_training_step_matches_oracle(gpu_device):
+    """trainer.py:1046-1069's loop with the latent pooler in the FinalAttention
+    slot: forward, cosine + MarginRankingLoss(2), backward, clip_grad_norm_(0.5),
+    AdamW(lr 1e-6, wd 0.01): the loss, the clipped gradients and the first
+    update agree with the same loop over the oracle's restatement; eval mode
+    afterwards still runs the inference path (no autograd, nr_latent_transform)."""
+    import torch.nn.functional as F
+    sd = W.latent_attention_state_dict(1234, ln_random=True)
+    m = _model(gpu_device, sd)
+    emb, mask = _batch(1)
+    g = torch.Generator().manual_seed(5)
+    pos, neg = torch.randn(6, 1024, generator=g), torch.randn(6, 1024, generator=g)
+
+    def step(model, e, msk, P, N, params):
+        before = [q.detach().clone() for q in params]
+        out = model(e, msk)
+        res = F.cosine_similarity(out.repeat(2, 1), torch.cat([P, N]))
+        loss = torch.nn.MarginRankingLoss(2)(res[:6], res[6:], torch.ones(6, device=res.device))
+        opt = torch.optim.AdamW(params, lr=1e-6, weight_decay=0.01)
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, 0.5)
+        opt.step()
+        return float(loss), [q.grad.detach().cpu() for q in params], [(q.detach() - b).cpu() for q, b in
+                                                                      zip(params, before)]
+
+    names = [n for n, _ in m.named_parameters()]
+    loss_gpu, g_gpu, u_gpu = step(m, emb.to(gpu_device), mask.to(gpu_device), pos.to(gpu_device),
+                                  neg.to(gpu_device), list(m.parameters()))
+    ref_sd = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    loss_ref, g_ref, u_ref = step(lambda e, msk: pool_ref.latent_attention_forward(ref_sd, e, msk), emb, mask, pos,
+                                  neg, [ref_sd[n] for n in names])
+    assert abs(loss_gpu - loss_ref) <= 1e-5 * max(1.0, abs(loss_ref))
+    for name, a, b, ua, ub in zip(names, g_gpu, g_ref, u_gpu, u_ref):
+        _rel_close(a, b, f"clipped d {name}")
+        thr = max(1e-2 * float(b.abs().max()), 1e-6)
+        sure = (a.abs() > thr) & (b.abs() > thr)
+        assert int(sure.sum()) > 0, name
+        np.testing.assert_allclose(ua[sure].numpy(), ub[sure].numpy(), rtol=0, atol=2e-8, err_msg=name)
+    m.eval()
+    with torch.no_grad():
+        u_eval = m(emb.to(gpu_device), mask.to(gpu_device))
+    want = pool_ref.latent_attention_forward({k: v.detach() for k, v in ref_sd.items()}, emb, mask)
+    _rel_close(u_eval, want, "users after the step (eval path)", tol=1e-4)
+
+
+def test_train_fold_matches_the_float64_fold():
+    """CPU: the differentiable f32 fold the training path builds (A, Bt from
+    latents / norm_context / to_q / to_kv / to_out) equals the float64 host fold
+    the inference path loads, and carries gradients to those parameters."""
+    m = LatentAttentionModel()
+    m.load_state_dict(W.latent_attention_state_dict(3, ln_random=True))
+    A, Bt = m._fold_train()
+    fw = m.folded_weights()
+    torch.testing.assert_close(A.double(), fw["A"], rtol=0, atol=1e-5 * float(fw["A"].abs().max()))
+    torch.testing.assert_close(Bt.double(), fw["Bt"], rtol=0, atol=1e-5 * float(fw["Bt"].abs().max()))
+    (A.sum() + Bt.sum()).backward()
+    blk = m.cross_attend_blocks[0]
+    for p in (m.latents, blk.norm_context.weight, blk.norm_context.bias, blk.fn.to_q.weight, blk.fn.to_kv.weight,
+              blk.fn.to_out.weight):
+        assert p.grad is not None and float(p.grad.abs().sum()) > 0
