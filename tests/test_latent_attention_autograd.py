@@ -111,7 +111,7 @@ def test_latent_attention_training_step_matches_oracle(gpu_device):
         loss.backward()
         torch.nn.utils.clip_grad_norm_(params, 0.5)
         opt.step()
-        return float(loss), [q.grad.detach().cpu() for q in params], [(q.detach() - b).cpu() for q, b in
+        return float(loss.detach()), [q.grad.detach().cpu() for q in params], [(q.detach() - b).cpu() for q, b in
                                                                       zip(params, before)]
 
     names = [n for n, _ in m.named_parameters()]
@@ -126,7 +126,10 @@ def test_latent_attention_training_step_matches_oracle(gpu_device):
         thr = max(1e-2 * float(b.abs().max()), 1e-6)
         sure = (a.abs() > thr) & (b.abs() > thr)
         assert int(sure.sum()) > 0, name
-        np.testing.assert_allclose(ua[sure].numpy(), ub[sure].numpy(), rtol=0, atol=2e-8, err_msg=name)
+        # the update is (p_after - p_before) in f32: for the O(1) latents that difference is
+        # resolved to an ulp of p (up to 1.2e-7), so allow one ulp of the parameter
+        np.testing.assert_allclose(ua[sure].numpy(), ub[sure].numpy(), rtol=0, atol=1.2e-7 if name == "latents"
+                                   else 2e-8, err_msg=name)
     m.eval()
     with torch.no_grad():
         u_eval = m(emb.to(gpu_device), mask.to(gpu_device))
