@@ -131,7 +131,8 @@ class AttentionAttentionComponent(PipelineComponent):
     """Config-5 training of the token-attention model + FinalAttention
     (components.py:883-952): ``train`` builds an AttentionAttentionTrainer on the
     impressions that have a history and runs ``num_epochs``; ``transform`` is the
-    identity.  Extra keyword arguments (batch_size, dtype, lr, dropout, seed) go
+    identity.  ``pooler="latent"`` trains LatentAttentionModel in FinalAttention's
+    slot (f32).  Extra keyword arguments (batch_size, dtype, lr, dropout, seed) go
     to the trainer."""
 
     required_keys = {"impression_rev_ind_array", "impression_len_list", "history_rev_ind_array",
@@ -142,10 +143,12 @@ class AttentionAttentionComponent(PipelineComponent):
                  final_attention_model_path: Optional[Path] = None, log_dir: Optional[Path] = None,
                  token_ckpt_dir: Optional[Path] = None, final_attn_ckpt_dir: Optional[Path] = None, num_epochs=5,
                  exp_name: str = "", max_neg_ratio: Optional[float] = None, max_pos_ratio: Optional[float] = None,
-                 rng=None, **trainer_kw):
+                 rng=None, pooler: str = "final", **trainer_kw):
         self.db_name = db_name
         self.token_attention = get_token_attn_model(token_attention_model_path)
-        self.final_attention = get_final_attention_model(final_attention_model_path)
+        # pooler="latent": BASELINE configs[4]'s pairing (token encoder + LatentAttentionModel, f32)
+        self.final_attention = (get_latent_attention_model(final_attention_model_path) if pooler == "latent" else
+                                get_final_attention_model(final_attention_model_path))
         self.num_epochs = num_epochs
         self.exp_name = exp_name
         self.rng = rng if rng is not None else np.random.default_rng(1234)

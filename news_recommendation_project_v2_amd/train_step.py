@@ -295,3 +295,119 @@ class FinalAttentionTrainStep:
         Hp = _pad64(Hs)
         fwd = 2.0 * Hp * (D * H + H * H + H * D + D * H + H * D)
         return 3.0 * fwd
+
+
+class LatentAttentionTrainStep:
+    """Config-5 step with ``LatentAttentionModel`` in the pooler slot (BASELINE
+    configs[4]: "backward for encoder + latent attention"; the reference
+    trainer's loop, trainer.py:1044-1069, with the latent pooler): f32, exact-f32
+    MFMA GEMMs.
+
+      E     = g_mlp_LN(last token of each unique news)      nr_gather_layernorm
+      S     = E[hist]                                        nr_gather_rows
+      H     = per-item latent hiddens of S                   latent_attention._LatentItemFn (HIP fwd + bwd)
+      users = normalize(segment mean of H)                   latent_attention.py:166-170
+      loss  = MarginRankingLoss(2)(cos(users, E[pos]), cos(users, E[neg]))   nr_cosine_margin
+      dE   += scatter(dS); token LN grads                    nr_scatter_add_rows, nr_ln_param_grad
+      clip_grad_norm_(0.5) + AdamW                           nr_sumsq, nr_adamw
+
+    The latent block's backward runs through torch autograd over
+    ``_LatentItemFn`` (its per-item GEMM / LayerNorm / softmax / GEGLU backward
+    are HIP kernels) and the 64-latent weight fold; the parameters are views of
+    one flat f32 buffer (as in FinalAttentionTrainStep), so ``state_dict()``
+    stays current and AdamW is one launch."""
+
+    def __init__(self, token_model, latent_model, dtype: torch.dtype = torch.float32, lr: float = 1e-6,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.01, max_norm: float = 0.5,
+                 dropout: float = 0.0, seed: int = 1234, device=None):
+        if dtype != torch.float32:
+            raise NewsRecHIPError("the latent-attention train step runs in f32 (exact-f32 MFMA)")
+        layers = list(token_model.encoder.layer)
+        if len(layers) != 1:
+            raise NewsRecHIPError("training supports NUM_HIDDEN_LAYERS == 1 (config.py:35)")
+        self.device = device or torch.device("cuda")
+        self.dtype = dtype
+        self.lr, self.betas, self.eps, self.wd, self.max_norm = lr, betas, eps, weight_decay, max_norm
+        self.seed = seed
+        self.step_count = 0
+        self.ln = layers[0].g_mlp_layernorm
+        self.ln_eps = float(self.ln.eps)
+        self.model = latent_model
+        lat = list(latent_model.named_parameters())
+        self.names = ["ln.weight", "ln.bias"] + [f"latent.{n}" for n, _ in lat]
+        params = [self.ln.weight, self.ln.bias] + [p for _, p in lat]
+        offs, o = [], 0
+        for p in params:
+            offs.append(o)
+            o += (p.numel() + 63) // 64 * 64
+        dev = self.device
+        self.flat = torch.zeros(o, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros_like(self.flat)
+        self.m = torch.zeros_like(self.flat)
+        self.v = torch.zeros_like(self.flat)
+        self.views, self.gviews = {}, {}
+        self._lat_params = []
+        with torch.no_grad():
+            for name, prm, off in zip(self.names, params, offs):
+                n = prm.numel()
+                view = self.flat[off:off + n].view(prm.shape)
+                view.copy_(prm.detach().to(dev, torch.float32))
+                prm.data = view
+                self.views[name] = view
+                self.gviews[name] = self.grad[off:off + n].view(prm.shape)
+                if name.startswith("latent."):
+                    self._lat_params.append((name, prm))
+        self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+
+    def forward_backward(self, batch: TrainBatch):
+        """Loss (device scalar) and gradients into ``self.grad`` (zeroed first).
+        Returns (loss, users, E) for inspection."""
+        U, B = batch.tok_last.shape[0], batch.B
+        self.grad.zero_()
+        self.loss.zero_()
+        E = ops.gather_layernorm(batch.tok_last, None, self.views["ln.weight"].view(1, D),
+                                 self.views["ln.bias"].view(1, D), self.ln_eps)
+        S = ops.gather_rows(E, batch.hist_idx, out_dtype=torch.float32).requires_grad_(True)
+        for _, p in self._lat_params:
+            p.grad = None
+        with torch.enable_grad():
+            Hh = self.model._train_items(S)
+            counts = batch.hist_off[1:] - batch.hist_off[:-1]
+            seg = torch.repeat_interleave(torch.arange(B, device=Hh.device), counts)
+            u = torch.zeros((B, D), dtype=torch.float32, device=Hh.device).index_add(0, seg, Hh)
+            u = torch.nn.functional.normalize(u / counts.unsqueeze(1).to(torch.float32), p=2, dim=-1)
+        users = u.detach().contiguous()
+        du = torch.empty((B, D), dtype=torch.float32, device=self.device)
+        dE = torch.zeros((U, D), dtype=torch.float32, device=self.device)
+        ops.cosine_margin(users, E, batch.pos, batch.neg, MARGIN, self.loss, du, dE)
+        u.backward(du)
+        ops.scatter_add_rows(S.grad, batch.hist_idx, dE)
+        ops.ln_param_grad(batch.tok_last, None, self.ln_eps, dE, self.gviews["ln.weight"], self.gviews["ln.bias"])
+        for name, p in self._lat_params:
+            self.gviews[name].copy_(p.grad)
+            p.grad = None
+        return self.loss, users, E
+
+    def optimizer_step(self) -> None:
+        """clip_grad_norm_(max_norm) + AdamW, one launch each (trainer.py:1067-1069)."""
+        self.step_count += 1
+        self.sumsq.zero_()
+        ops.sumsq(self.grad, self.sumsq)
+        ops.adamw(self.flat, self.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps, self.wd,
+                  self.max_norm, self.sumsq if self.max_norm > 0 else None, None)
+
+    def step(self, batch: TrainBatch) -> torch.Tensor:
+        loss, _, _ = self.forward_backward(batch)
+        out = loss.clone()
+        self.optimizer_step()
+        return out
+
+    def grad_dict(self) -> dict:
+        return dict(self.gviews)
+
+    def flops_per_step(self, Hs: int) -> float:
+        """MFMA FLOPs of the per-item GEMMs (forward + data-grad + weight-grad)."""
+        Hp = _pad64(Hs)
+        fwd = 2.0 * Hp * (D * 512 + 512 * D + D * 8192 + 4096 * D)
+        return 3.0 * fwd

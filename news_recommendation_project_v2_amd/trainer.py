@@ -30,7 +30,7 @@ import torch
 
 from .config import DEVICE
 from .data_utils import FinalAttentionTrainDataset, lengths_to_offsets, train_batch_csr
-from .train_step import FinalAttentionTrainStep, TrainBatch
+from .train_step import FinalAttentionTrainStep, LatentAttentionTrainStep, TrainBatch
 
 DEFAULT_TRAIN_BATCH = 256
 
@@ -57,8 +57,15 @@ class AttentionAttentionTrainer:
         self.token_attention_model = token_attention_model
         self.final_attention_model = final_attention_model
         self.train_batch_size = batch_size
-        self.engine = FinalAttentionTrainStep(token_attention_model, final_attention_model, dtype=dtype, lr=lr,
-                                              dropout=dropout, seed=seed, device=DEVICE)
+        if getattr(final_attention_model, "pooler_kind", "final") == "latent":
+            if dtype != torch.float32:
+                raise ValueError("the latent-attention pooler trains in f32 (dtype=torch.float32)")
+            # BASELINE configs[4]'s pairing: token encoder + LatentAttentionModel (f32)
+            self.engine = LatentAttentionTrainStep(token_attention_model, final_attention_model, lr=lr, seed=seed,
+                                                   device=DEVICE)
+        else:
+            self.engine = FinalAttentionTrainStep(token_attention_model, final_attention_model, dtype=dtype, lr=lr,
+                                                  dropout=dropout, seed=seed, device=DEVICE)
         self.train_dataset = FinalAttentionTrainDataset(
             history_rev_index=train_history_rev_index, history_len_list=train_history_len_list,
             news_rev_index=train_news_rev_index, impression_len_list=train_impression_len_list,

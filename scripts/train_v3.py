@@ -58,8 +58,10 @@ def main():
     ap.add_argument("--model-path", default=MODEL_PATH)
     ap.add_argument("--exp-name", default="attn_attn")
     ap.add_argument("--synthetic", action="store_true")
+    ap.add_argument("--pooler", choices=["final", "latent"], default="final",
+                    help="latent: LatentAttentionModel in FinalAttention's slot (BASELINE configs[4]; f32)")
     args = ap.parse_args()
-    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    dtype = torch.bfloat16 if args.dtype == "bf16" and args.pooler == "final" else torch.float32
     rng = np.random.default_rng(1234)
 
     if args.synthetic:
@@ -80,7 +82,8 @@ def main():
     comp = AttentionAttentionComponent(db_name=str(args.db_name), log_dir=args.log_dir,
                                        token_ckpt_dir=args.ckpt_dir / "token_attn",
                                        final_attn_ckpt_dir=args.ckpt_dir / "final_attn", exp_name=args.exp_name,
-                                       num_epochs=args.epochs, rng=rng, batch_size=args.batch_size, dtype=dtype)
+                                       num_epochs=args.epochs, rng=rng, batch_size=args.batch_size, dtype=dtype,
+                                       pooler=args.pooler)
     steps.append(("attn_attn", comp))
     t0 = time.time()
     Pipeline("train_subset", steps).train(ctx)

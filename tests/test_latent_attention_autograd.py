@@ -152,3 +152,71 @@ def test_train_fold_matches_the_float64_fold():
     for p in (m.latents, blk.norm_context.weight, blk.norm_context.bias, blk.fn.to_q.weight, blk.fn.to_kv.weight,
               blk.fn.to_out.weight):
         assert p.grad is not None and float(p.grad.abs().sum()) > 0
+
+
+@pytest.mark.gpu
+def test_latent_train_step_matches_oracle(gpu_device, tmp_path):
+    """Config 5 with the latent pooler (train_step.LatentAttentionTrainStep, the
+    engine AttentionAttentionTrainer picks for a LatentAttentionModel): token
+    LayerNorm of each unique news' last token -> history gather -> latent
+    hiddens -> masked mean + normalize -> cosine vs pos / neg -> MarginRankingLoss(2)
+    -> backward -> clip_grad_norm_(0.5) -> AdamW, on the first batch of the
+    reference trainer's golden data set (tests/golden/train_step.npz), against
+    the same loop in torch autograd over the oracle's latent forward."""
+    import torch.nn.functional as F
+    from test_train import _dataset, _device_batch, _oracle_batch, _setup
+    from news_recommendation_project_v2_amd.modeling_utils import get_token_attn_model
+    from news_recommendation_project_v2_amd.train_step import LatentAttentionTrainStep
+    g, states, labels = _setup()
+    ds = _dataset(g, labels)
+    lo, hi = 0, int(g["batch_size"])
+    tok_sd = W.token_attn_state_dict(1234)
+    lat_sd = W.latent_attention_state_dict(1234, ln_random=True)
+    tm = get_token_attn_model()
+    tm.load_state_dict(tok_sd)
+    lm = _model(gpu_device, lat_sd)
+    eng = LatentAttentionTrainStep(tm, lm, device=gpu_device)
+    batch = _device_batch(ds, states, lo, hi, gpu_device, tmp_path)
+    loss, _, _ = eng.forward_backward(batch)
+    grads = {k: v.detach().cpu().clone() for k, v in eng.grad_dict().items()}
+    eng.optimizer_step()
+    after = {k: v.detach().cpu().clone() for k, v in eng.views.items()}
+
+    ln = tm.encoder.layer[0].g_mlp_layernorm
+    last, hg, pos, neg, B = _oracle_batch(ds, states, lo, hi)
+    ref = {"ln.weight": tok_sd["encoder.layer.0.g_mlp_layernorm.weight"].clone().requires_grad_(True),
+           "ln.bias": tok_sd["encoder.layer.0.g_mlp_layernorm.bias"].clone().requires_grad_(True)}
+    ref.update({f"latent.{k}": v.clone().requires_grad_(True) for k, v in lat_sd.items()})
+    E = F.layer_norm(last, (1024,), ref["ln.weight"], ref["ln.bias"], ln.eps)
+    L = max(len(h) for h in hg)
+    mask = torch.zeros(B, L, dtype=torch.int64)
+    emb = torch.zeros(B, L, 1024)
+    rows = []
+    for b, h in enumerate(hg):
+        mask[b, :len(h)] = 1
+        rows.append(torch.cat([E[torch.as_tensor(h)], torch.zeros(L - len(h), 1024)]))
+    emb = torch.stack(rows)
+    users = pool_ref.latent_attention_forward({k[7:]: v for k, v in ref.items() if k.startswith("latent.")}, emb, mask)
+    res = F.cosine_similarity(users.repeat(2, 1), E[torch.as_tensor(np.concatenate([pos, neg]))])
+    want = torch.nn.MarginRankingLoss(2)(res[:B], res[B:], torch.ones(B))
+    want.backward()
+    assert abs(float(loss) - float(want)) <= 1e-5 * max(1.0, abs(float(want)))
+    names = list(ref)
+    for k in names:  # the raw gradients (the engine folds the clip into AdamW)
+        _rel_close(grads[k], ref[k].grad, f"d {k}")
+    params = list(ref.values())
+    torch.nn.utils.clip_grad_norm_(params, 0.5)
+    before = {k: v.detach().clone() for k, v in ref.items()}
+    opt = torch.optim.AdamW(params, lr=1e-6, weight_decay=0.01)
+    opt.step()
+    norm = float(eng.sumsq.sqrt())
+    assert norm > 0
+    for k in names:
+        assert k in grads, k
+        upd_ref = ref[k].detach() - before[k]
+        upd = after[k] - before[k]
+        thr = max(1e-2 * float(upd_ref.abs().max()), 1e-12)
+        sure = (upd_ref.abs() > thr) & (upd.abs() > thr)
+        assert int(sure.sum()) > 0, k
+        tol = 1.2e-7 if k == "latent.latents" or k.startswith("ln.") else 3e-8
+        np.testing.assert_allclose(upd[sure].numpy(), upd_ref[sure].numpy(), rtol=0, atol=tol, err_msg=k)
