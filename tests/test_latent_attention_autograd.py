@@ -220,3 +220,25 @@ def test_latent_train_step_matches_oracle(gpu_device, tmp_path):
         assert int(sure.sum()) > 0, k
         tol = 1.2e-7 if k == "latent.latents" or k.startswith("ln.") else 3e-8
         np.testing.assert_allclose(upd[sure].numpy(), upd_ref[sure].numpy(), rtol=0, atol=tol, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_train_v3_latent_pooler_synthetic(gpu_device, tmp_path, monkeypatch):
+    """scripts/train_v3.py --pooler latent end to end on synthetic data: the
+    trainer runs LatentAttentionTrainStep, logs finite losses and saves a
+    LatentAttentionModel state dict that loads back into the module."""
+    import json
+    import runpy
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1] / "scripts"
+    monkeypatch.setattr(sys, "argv", ["train_v3.py", "--synthetic", "--pooler", "latent", "--num-impressions", "200",
+                                      "--epochs", "2", "--batch-size", "64", "--db-name", str(tmp_path / "tok.db"),
+                                      "--log-dir", str(tmp_path / "logs"), "--ckpt-dir", str(tmp_path / "models")])
+    runpy.run_path(str(root / "train_v3.py"), run_name="__main__")
+    recs = [json.loads(x) for x in (tmp_path / "logs" / "train_final_history_score.jsonl").read_text().splitlines()]
+    assert [r["epoch"] for r in recs] == [1, 2] and all(0.0 < r["loss"] < 4.0 for r in recs)
+    sd = torch.load(tmp_path / "models" / "final_attn" / "Epoch_2.pt", weights_only=True)
+    m = LatentAttentionModel()
+    m.load_state_dict(sd)
+    assert sd["latents"].shape == (64, 1024)
