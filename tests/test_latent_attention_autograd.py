@@ -215,8 +215,10 @@ def test_latent_train_step_matches_oracle(gpu_device, tmp_path):
         assert k in grads, k
         upd_ref = ref[k].detach() - before[k]
         upd = after[k] - before[k]
-        thr = max(1e-2 * float(upd_ref.abs().max()), 1e-12)
-        sure = (upd_ref.abs() > thr) & (upd.abs() > thr)
+        # where |g| is well above AdamW's eps the first step moves an element by ~lr: compare
+        # there (as tests/test_final_attention_autograd.py); near eps it is sign-of-noise
+        thr = 1e-2 * float(grads[k].abs().max())
+        sure = grads[k].abs() > thr
         assert int(sure.sum()) > 0, k
         tol = 1.2e-7 if k == "latent.latents" or k.startswith("ln.") else 3e-8
         np.testing.assert_allclose(upd[sure].numpy(), upd_ref[sure].numpy(), rtol=0, atol=tol, err_msg=k)
