@@ -132,7 +132,7 @@ class AttentionAttentionComponent(PipelineComponent):
     (components.py:883-952): ``train`` builds an AttentionAttentionTrainer on the
     impressions that have a history and runs ``num_epochs``; ``transform`` is the
     identity.  ``pooler="latent"`` trains LatentAttentionModel in FinalAttention's
-    slot (f32).  Extra keyword arguments (batch_size, dtype, lr, dropout, seed) go
+    slot.  Extra keyword arguments (batch_size, dtype, lr, dropout, seed) go
     to the trainer."""
 
     required_keys = {"impression_rev_ind_array", "impression_len_list", "history_rev_ind_array",
@@ -146,7 +146,7 @@ class AttentionAttentionComponent(PipelineComponent):
                  rng=None, pooler: str = "final", **trainer_kw):
         self.db_name = db_name
         self.token_attention = get_token_attn_model(token_attention_model_path)
-        # pooler="latent": BASELINE configs[4]'s pairing (token encoder + LatentAttentionModel, f32)
+        # pooler="latent": BASELINE configs[4]'s pairing (token encoder + LatentAttentionModel)
         self.final_attention = (get_latent_attention_model(final_attention_model_path) if pooler == "latent" else
                                 get_final_attention_model(final_attention_model_path))
         self.num_epochs = num_epochs

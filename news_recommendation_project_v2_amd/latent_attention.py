@@ -98,7 +98,7 @@ def _pad64(n: int) -> int:
 
 class _LatentItemFn(torch.autograd.Function):
     """Per-item hiddens of LatentAttentionModel (latent_attention.py:157-163) with
-    their backward on the HIP kernels, f32 (exact-f32 MFMA GEMMs), over packed
+    their backward on the HIP kernels, over packed
     valid rows padded with zeros to a multiple of 64 (the weight-grad GEMMs' K):
 
       X  = LN_q(E)                          nr_layernorm
@@ -115,48 +115,56 @@ class _LatentItemFn(torch.autograd.Function):
     the module's parameters by differentiable torch ops (LatentAttentionModel.
     _fold_train: 64-latent weight algebra, the reference's own to_kv(latents)),
     so autograd carries dA and dBt on to latents, norm_context, to_q, to_kv and
-    to_out.  The padding rows carry zero gradient."""
+    to_out.  The padding rows carry zero gradient.  GEMM operands are f32 (exact-f32
+    MFMA, the module API's default) or, with ``mm_dtype=bfloat16`` (the config-5
+    train step's bf16 mode), bf16 with f32 accumulation and f32 outputs."""
 
     @staticmethod
-    def forward(ctx, rows, A, Bt, gq, bq, gf, bf, W1, b1, W2, b2):
+    def forward(ctx, rows, A, Bt, gq, bq, gf, bf, W1, b1, W2, b2, mm_dtype=torch.float32):
         Hs, D = rows.shape
         Hp = _pad64(Hs)
         dev = rows.device
         E = torch.zeros((Hp, D), dtype=torch.float32, device=dev)
         E[:Hs] = rows
         A, Bt, W1, W2 = A.contiguous(), Bt.contiguous(), W1.contiguous(), W2.contiguous()
+        f32 = torch.float32
+        # GEMM operands in mm_dtype (bf16: MFMA bf16 operands, f32 accumulate and f32
+        # outputs -- the LN / softmax / GEGLU kernels and the residual stream stay f32)
+        c = (lambda t: t) if mm_dtype == f32 else (lambda t: ops.gather_rows(t, None, out_dtype=mm_dtype))
         X = ops.layernorm(E, gq.contiguous(), bq.contiguous(), 1e-5)
-        P = ops.gemm(X, A, None, epilogue="softmax64")
-        H1 = ops.gemm(P, Bt, None, epilogue="resadd", residual=E)
+        P = ops.gemm(c(X), c(A), None, epilogue="softmax64", out_dtype=f32)
+        H1 = ops.gemm(c(P), c(Bt), None, epilogue="resadd", residual=E, out_dtype=f32)
         Y = ops.layernorm(H1, gf.contiguous(), bf.contiguous(), 1e-5)
-        G = ops.gemm(Y, W1, b1.contiguous())
+        G = ops.gemm(c(Y), c(W1), b1.contiguous(), out_dtype=f32)
         Z = ops.geglu_fwd(G)
-        H = ops.gemm(Z, W2, b2.contiguous(), epilogue="resadd", residual=H1)
+        H = ops.gemm(c(Z), c(W2), b2.contiguous(), epilogue="resadd", residual=H1, out_dtype=f32)
         ctx.save_for_backward(E, X, P, H1, Y, G, Z, A, Bt, gq, gf, W1, W2)
-        ctx.Hs = Hs
+        ctx.Hs, ctx.mm_dtype = Hs, mm_dtype
         return H[:Hs]
 
     @staticmethod
     def backward(ctx, dH):
         E, X, P, H1, Y, G, Z, A, Bt, gq, gf, W1, W2 = ctx.saved_tensors
-        Hs = ctx.Hs
+        Hs, lo = ctx.Hs, ctx.mm_dtype
         Hp, D = E.shape
         dev = E.device
-        dHp = torch.zeros((Hp, D), dtype=torch.float32, device=dev)
+        f32 = torch.float32
+        dHp = torch.zeros((Hp, D), dtype=f32, device=dev)
         dHp[:Hs] = dH.float()
-        T = ops.transpose
-        dZ = ops.gemm(dHp, T(W2))
+        c = (lambda t: t) if lo == f32 else (lambda t: ops.gather_rows(t, None, out_dtype=lo))
+        T = lambda t: ops.transpose(t, out_dtype=lo)
+        dZ = ops.gemm(c(dHp), T(W2), out_dtype=f32)
         dG = ops.geglu_bwd(G, dZ)
-        dY = ops.gemm(dG, T(W1))
+        dY = ops.gemm(c(dG), T(W1), out_dtype=f32)
         dH1 = ops.layernorm_bwd(H1, gf.contiguous(), dY, 1e-5, residual=dHp)
-        dP = ops.gemm(dH1, T(Bt))
+        dP = ops.gemm(c(dH1), T(Bt), out_dtype=f32)
         dS = ops.softmax64_bwd(P, dP)
-        dX = ops.gemm(dS, T(A))
+        dX = ops.gemm(c(dS), T(A), out_dtype=f32)
         dE = ops.layernorm_bwd(E, gq.contiguous(), dX, 1e-5, residual=dH1)
-        gW2 = torch.empty(W2.shape, dtype=torch.float32, device=dev)
-        gW1 = torch.empty(W1.shape, dtype=torch.float32, device=dev)
-        gBt = torch.empty(Bt.shape, dtype=torch.float32, device=dev)
-        gA = torch.empty(A.shape, dtype=torch.float32, device=dev)
+        gW2 = torch.empty(W2.shape, dtype=f32, device=dev)
+        gW1 = torch.empty(W1.shape, dtype=f32, device=dev)
+        gBt = torch.empty(Bt.shape, dtype=f32, device=dev)
+        gA = torch.empty(A.shape, dtype=f32, device=dev)
         ops.gemm_grouped([(T(dHp), T(Z), gW2), (T(dG), T(Y), gW1), (T(dH1), T(P), gBt), (T(dS), T(X), gA)])
         gb2 = torch.zeros(D, dtype=torch.float32, device=dev)
         gb1 = torch.zeros(W1.shape[0], dtype=torch.float32, device=dev)
@@ -165,7 +173,7 @@ class _LatentItemFn(torch.autograd.Function):
         ggf, gbf, ggq, gbq = (torch.zeros(D, dtype=torch.float32, device=dev) for _ in range(4))
         ops.ln_param_grad(H1, None, 1e-5, dY, ggf, gbf)
         ops.ln_param_grad(E, None, 1e-5, dX, ggq, gbq)
-        return dE[:Hs], gA, gBt, ggq, gbq, ggf, gbf, gW1, gb1, gW2, gb2
+        return dE[:Hs], gA, gBt, ggq, gbq, ggf, gbf, gW1, gb1, gW2, gb2, None
 
 
 class LatentAttentionModel(torch.nn.Module):
@@ -277,7 +285,7 @@ class LatentAttentionModel(torch.nn.Module):
         bt = torch.matmul(attn.to_out.weight.reshape(d, h, dh).permute(1, 0, 2), v)      # [h, D, nl]
         return a.reshape(h * nl, d), bt.permute(1, 0, 2).reshape(d, h * nl)
 
-    def _train_items(self, rows: torch.Tensor) -> torch.Tensor:
+    def _train_items(self, rows: torch.Tensor, mm_dtype: torch.dtype = torch.float32) -> torch.Tensor:
         params = list(self.parameters())
         if any(p.dtype != torch.float32 for p in params):
             raise NewsRecHIPError("LatentAttentionModel autograd path trains f32 parameters (as the reference does)")
@@ -285,7 +293,7 @@ class LatentAttentionModel(torch.nn.Module):
         A, Bt = self._fold_train()
         ff = ff_blk.fn.net
         return _LatentItemFn.apply(rows.float(), A, Bt, attn_blk.norm.weight, attn_blk.norm.bias, ff_blk.norm.weight,
-                                   ff_blk.norm.bias, ff[0].weight, ff[0].bias, ff[2].weight, ff[2].bias)
+                                   ff_blk.norm.bias, ff[0].weight, ff[0].bias, ff[2].weight, ff[2].bias, mm_dtype)
 
     def forward(self, embeddings: torch.Tensor, attention_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         if embeddings.device.type != "cuda":

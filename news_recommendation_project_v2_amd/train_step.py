@@ -300,8 +300,9 @@ class FinalAttentionTrainStep:
 class LatentAttentionTrainStep:
     """Config-5 step with ``LatentAttentionModel`` in the pooler slot (BASELINE
     configs[4]: "backward for encoder + latent attention"; the reference
-    trainer's loop, trainer.py:1044-1069, with the latent pooler): f32, exact-f32
-    MFMA GEMMs.
+    trainer's loop, trainer.py:1044-1069, with the latent pooler): GEMMs on f32
+    operands (exact-f32 MFMA) or bf16 operands (bf16 MFMA, f32 accumulate and f32
+    activations / residual stream / LN, softmax and GEGLU kernels).
 
       E     = g_mlp_LN(last token of each unique news)      nr_gather_layernorm
       S     = E[hist]                                        nr_gather_rows
@@ -320,8 +321,8 @@ class LatentAttentionTrainStep:
     def __init__(self, token_model, latent_model, dtype: torch.dtype = torch.float32, lr: float = 1e-6,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.01, max_norm: float = 0.5,
                  dropout: float = 0.0, seed: int = 1234, device=None):
-        if dtype != torch.float32:
-            raise NewsRecHIPError("the latent-attention train step runs in f32 (exact-f32 MFMA)")
+        if dtype not in (torch.float32, torch.bfloat16):
+            raise NewsRecHIPError("latent-attention train step dtype must be float32 or bfloat16")
         layers = list(token_model.encoder.layer)
         if len(layers) != 1:
             raise NewsRecHIPError("training supports NUM_HIDDEN_LAYERS == 1 (config.py:35)")
@@ -372,7 +373,7 @@ class LatentAttentionTrainStep:
         for _, p in self._lat_params:
             p.grad = None
         with torch.enable_grad():
-            Hh = self.model._train_items(S)
+            Hh = self.model._train_items(S, mm_dtype=self.dtype)
             counts = batch.hist_off[1:] - batch.hist_off[:-1]
             seg = torch.repeat_interleave(torch.arange(B, device=Hh.device), counts)
             u = torch.zeros((B, D), dtype=torch.float32, device=Hh.device).index_add(0, seg, Hh)

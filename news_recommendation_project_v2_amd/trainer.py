@@ -58,11 +58,9 @@ class AttentionAttentionTrainer:
         self.final_attention_model = final_attention_model
         self.train_batch_size = batch_size
         if getattr(final_attention_model, "pooler_kind", "final") == "latent":
-            if dtype != torch.float32:
-                raise ValueError("the latent-attention pooler trains in f32 (dtype=torch.float32)")
-            # BASELINE configs[4]'s pairing: token encoder + LatentAttentionModel (f32)
-            self.engine = LatentAttentionTrainStep(token_attention_model, final_attention_model, lr=lr, seed=seed,
-                                                   device=DEVICE)
+            # BASELINE configs[4]'s pairing: token encoder + LatentAttentionModel
+            self.engine = LatentAttentionTrainStep(token_attention_model, final_attention_model, dtype=dtype, lr=lr,
+                                                   seed=seed, device=DEVICE)
         else:
             self.engine = FinalAttentionTrainStep(token_attention_model, final_attention_model, dtype=dtype, lr=lr,
                                                   dropout=dropout, seed=seed, device=DEVICE)

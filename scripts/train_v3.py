@@ -59,9 +59,9 @@ def main():
     ap.add_argument("--exp-name", default="attn_attn")
     ap.add_argument("--synthetic", action="store_true")
     ap.add_argument("--pooler", choices=["final", "latent"], default="final",
-                    help="latent: LatentAttentionModel in FinalAttention's slot (BASELINE configs[4]; f32)")
+                    help="latent: LatentAttentionModel in FinalAttention's slot (BASELINE configs[4])")
     args = ap.parse_args()
-    dtype = torch.bfloat16 if args.dtype == "bf16" and args.pooler == "final" else torch.float32
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     rng = np.random.default_rng(1234)
 
     if args.synthetic:

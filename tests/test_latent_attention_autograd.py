@@ -244,3 +244,32 @@ def test_train_v3_latent_pooler_synthetic(gpu_device, tmp_path, monkeypatch):
     m = LatentAttentionModel()
     m.load_state_dict(sd)
     assert sd["latents"].shape == (64, 1024)
+
+
+@pytest.mark.gpu
+def test_latent_train_step_bf16_close_to_f32(gpu_device, tmp_path):
+    """The bf16 mode of LatentAttentionTrainStep (bf16 MFMA operands, f32
+    activations) against its f32 mode on the golden trainer batch: loss within
+    2 %, every gradient's cosine with the f32 one > 0.99 (the criterion of
+    tests/test_train.py for FinalAttention)."""
+    from test_train import _dataset, _device_batch, _setup
+    from news_recommendation_project_v2_amd.modeling_utils import get_token_attn_model
+    from news_recommendation_project_v2_amd.train_step import LatentAttentionTrainStep
+    g, states, labels = _setup()
+    ds = _dataset(g, labels)
+    batch = _device_batch(ds, states, 0, int(g["batch_size"]), gpu_device, tmp_path)
+    out = {}
+    for dt in (torch.float32, torch.bfloat16):
+        tm = get_token_attn_model()
+        tm.load_state_dict(W.token_attn_state_dict(1234))
+        eng = LatentAttentionTrainStep(tm, _model(gpu_device, W.latent_attention_state_dict(1234, ln_random=True)),
+                                       dtype=dt, device=gpu_device)
+        loss, _, _ = eng.forward_backward(batch)
+        out[dt] = (float(loss), {k: v.detach().double().flatten().clone() for k, v in eng.grad_dict().items()})
+    l32, g32 = out[torch.float32]
+    l16, g16 = out[torch.bfloat16]
+    assert abs(l16 - l32) <= 2e-2 * abs(l32)
+    for k in g32:
+        a, b = g32[k], g16[k]
+        cos = float((a @ b) / (a.norm() * b.norm() + 1e-30))
+        assert cos > 0.99, (k, cos)
