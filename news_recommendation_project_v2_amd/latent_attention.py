@@ -176,6 +176,32 @@ class _LatentItemFn(torch.autograd.Function):
         return dE[:Hs], gA, gBt, ggq, gbq, ggf, gbf, gW1, gb1, gW2, gb2, None
 
 
+class _SegmentMeanFn(torch.autograd.Function):
+    """Masked mean over each batch row's valid items (latent_attention.py:166-168)
+    on the packed rows: forward is the pooling kernel's mean pass (nr_pool_score
+    pooling-only, NR_POOL_MEAN: one wave per segment, fixed summation order, so
+    the result is deterministic, unlike an atomic index_add); backward spreads
+    du / count back over the segment's rows.  An empty segment gives 0/0 = NaN,
+    as the reference's s / d does."""
+
+    @staticmethod
+    def forward(ctx, H, off):
+        ctx.save_for_backward(off)
+        ctx.n_rows = H.shape[0]
+        return ops.pool_rows("mean", H.contiguous(), off)
+
+    @staticmethod
+    def backward(ctx, du):
+        (off,) = ctx.saved_tensors
+        counts = off[1:] - off[:-1]
+        per_row = (du / counts.unsqueeze(1).to(du.dtype)).repeat_interleave(counts, dim=0, output_size=ctx.n_rows)
+        return per_row, None
+
+
+def segment_mean(H: torch.Tensor, off: torch.Tensor) -> torch.Tensor:
+    return _SegmentMeanFn.apply(H, off)
+
+
 class LatentAttentionModel(torch.nn.Module):
     """forward(embeddings [B, L, D], attention_mask [B, L] | None).
 
@@ -311,9 +337,5 @@ class LatentAttentionModel(torch.nn.Module):
             return pool_rows("latent", self.item_table(rows.float()), off)
         # autograd: per-item hiddens on the HIP kernels, then the reference's masked mean
         # and F.normalize (latent_attention.py:166-170) on the [B, D] users
-        H = self._train_items(rows)
-        counts = off[1:] - off[:-1]
-        seg = torch.repeat_interleave(torch.arange(b, device=H.device), counts)
-        s = torch.zeros((b, d), dtype=H.dtype, device=H.device).index_add(0, seg, H)
-        u = s / counts.unsqueeze(1).to(H.dtype)
+        u = segment_mean(self._train_items(rows), off)
         return torch.nn.functional.normalize(u, p=2, dim=-1) if self.output_normalize else u

@@ -307,7 +307,7 @@ class LatentAttentionTrainStep:
       E     = g_mlp_LN(last token of each unique news)      nr_gather_layernorm
       S     = E[hist]                                        nr_gather_rows
       H     = per-item latent hiddens of S                   latent_attention._LatentItemFn (HIP fwd + bwd)
-      users = normalize(segment mean of H)                   latent_attention.py:166-170
+      users = normalize(segment mean of H)                   nr_pool_score (mean pass), latent_attention.py:166-170
       loss  = MarginRankingLoss(2)(cos(users, E[pos]), cos(users, E[neg]))   nr_cosine_margin
       dE   += scatter(dS); token LN grads                    nr_scatter_add_rows, nr_ln_param_grad
       clip_grad_norm_(0.5) + AdamW                           nr_sumsq, nr_adamw
@@ -364,6 +364,7 @@ class LatentAttentionTrainStep:
     def forward_backward(self, batch: TrainBatch):
         """Loss (device scalar) and gradients into ``self.grad`` (zeroed first).
         Returns (loss, users, E) for inspection."""
+        from .latent_attention import segment_mean
         U, B = batch.tok_last.shape[0], batch.B
         self.grad.zero_()
         self.loss.zero_()
@@ -373,11 +374,8 @@ class LatentAttentionTrainStep:
         for _, p in self._lat_params:
             p.grad = None
         with torch.enable_grad():
-            Hh = self.model._train_items(S, mm_dtype=self.dtype)
-            counts = batch.hist_off[1:] - batch.hist_off[:-1]
-            seg = torch.repeat_interleave(torch.arange(B, device=Hh.device), counts)
-            u = torch.zeros((B, D), dtype=torch.float32, device=Hh.device).index_add(0, seg, Hh)
-            u = torch.nn.functional.normalize(u / counts.unsqueeze(1).to(torch.float32), p=2, dim=-1)
+            u = segment_mean(self.model._train_items(S, mm_dtype=self.dtype), batch.hist_off)
+            u = torch.nn.functional.normalize(u, p=2, dim=-1)
         users = u.detach().contiguous()
         du = torch.empty((B, D), dtype=torch.float32, device=self.device)
         dE = torch.zeros((U, D), dtype=torch.float32, device=self.device)

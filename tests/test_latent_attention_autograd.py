@@ -63,6 +63,8 @@ def test_latent_attention_backward_matches_oracle(gpu_device):
     for name, prm in m.named_parameters():
         assert prm.grad is not None, name
         _rel_close(prm.grad, ref_sd[name].grad, f"d {name}")
+    # deterministic: no atomics on the forward path (the segment mean is the pooling kernel's)
+    assert torch.equal(m(e_d, mask.to(gpu_device)), out)
 
 
 @pytest.mark.gpu
