@@ -279,8 +279,13 @@ def test_latent_unpooled_forward_golden(gpu_device):
     g = golden("pool_latent")
     m = _model("latent", gpu_device, int(g["weight_seed"]))
     table = W.news_table(1234, int(g["n_news"]), 1024, name=str(g["table_name"])).to(gpu_device)
-    out = m(table[torch.tensor(g["unpooled_in_rows"], device=gpu_device)], None)
+    with torch.no_grad():  # the inference path (grad recording takes the autograd path, as in torch)
+        out = m(table[torch.tensor(g["unpooled_in_rows"], device=gpu_device)], None)
     np.testing.assert_allclose(out.cpu().numpy(), g["unpooled_out"], rtol=0, atol=1e-4)
+    # recorded for autograd (eval mode, grad enabled): the differentiable path, same values
+    rec = m(table[torch.tensor(g["unpooled_in_rows"], device=gpu_device)], None)
+    assert rec.requires_grad
+    np.testing.assert_allclose(rec.detach().cpu().numpy(), g["unpooled_out"], rtol=0, atol=1e-4)
 
 
 @pytest.mark.parametrize("pooler", ["final", "latent"])
