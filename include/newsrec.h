@@ -422,15 +422,17 @@ int nr_layernorm_bwd(int64_t n, int64_t dim, const float* x, int64_t ldx, const 
                      void* stream);
 
 /* Softmax backward over groups of 64 columns (one head's 64 latents):
- * ds = p (dp - sum_group(p dp)). */
-int nr_softmax64_bwd(int64_t rows, int64_t cols, const float* p, int64_t ldp, const float* dp, int64_t lddp,
-                     float* ds, int64_t ldds, void* stream);
+ * ds = p (dp - sum_group(p dp)); ds f32 or bf16 (dtype_out). */
+int nr_softmax64_bwd(int dtype_out, int64_t rows, int64_t cols, const float* p, int64_t ldp, const float* dp,
+                     int64_t lddp, void* ds, int64_t ldds, void* stream);
 
 /* GEGLU (latent_attention.py:24-27, exact-erf gelu): z = a gelu(g) with
- * a = G[:, :f], g = G[:, f:]; backward dG = [dz gelu(g), dz a gelu'(g)]. */
-int nr_geglu_fwd(int64_t rows, int64_t f, const float* g, int64_t ldg, float* z, int64_t ldz, void* stream);
-int nr_geglu_bwd(int64_t rows, int64_t f, const float* g, int64_t ldg, const float* dz, int64_t lddz, float* dg,
-                 int64_t lddg, void* stream);
+ * a = G[:, :f], g = G[:, f:]; backward dG = [dz gelu(g), dz a gelu'(g)].  Inputs f32;
+ * z / dG f32 or bf16 (dtype_out: the bf16-operand training mode's GEMM inputs). */
+int nr_geglu_fwd(int dtype_out, int64_t rows, int64_t f, const float* g, int64_t ldg, void* z, int64_t ldz,
+                 void* stream);
+int nr_geglu_bwd(int dtype_out, int64_t rows, int64_t f, const float* g, int64_t ldg, const float* dz, int64_t lddz,
+                 void* dg, int64_t lddg, void* stream);
 
 /* *out += sum x^2 (the global grad norm of clip_grad_norm_, trainer.py:1067-1071). */
 int nr_sumsq(int64_t n, const float* x, float* out, void* stream);

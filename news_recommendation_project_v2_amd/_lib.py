@@ -109,9 +109,9 @@ SIGNATURES = {
     "nr_ln_param_grad": (_i, [_i, _l, _l, _p, _l, _p, _f, _p, _l, _p, _p, _p]),
     "nr_sumsq": (_i, [_l, _p, _p, _p]),
     "nr_layernorm_bwd": (_i, [_l, _l, _p, _l, _p, _f, _p, _l, _p, _l, _p, _l, _p]),
-    "nr_softmax64_bwd": (_i, [_l, _l, _p, _l, _p, _l, _p, _l, _p]),
-    "nr_geglu_fwd": (_i, [_l, _l, _p, _l, _p, _l, _p]),
-    "nr_geglu_bwd": (_i, [_l, _l, _p, _l, _p, _l, _p, _l, _p]),
+    "nr_softmax64_bwd": (_i, [_i, _l, _l, _p, _l, _p, _l, _p, _l, _p]),
+    "nr_geglu_fwd": (_i, [_i, _l, _l, _p, _l, _p, _l, _p]),
+    "nr_geglu_bwd": (_i, [_i, _l, _l, _p, _l, _p, _l, _p, _l, _p]),
     "nr_adamw": (_i, [_l, _p, _p, _p, _p, _p, _l, _f, _f, _f, _f, _f, _f, _p, _p]),
     "nr_encoder_workspace_bytes": (_l, [_i, _l, _l]),
     "nr_encoder_forward": (_i, [_i, _i, _p, _p, _l, _p, _l, _p, _p, _p, _f, _l, _l, _p, _p, _i, _p, _p, _p, _p, _l,

@@ -417,39 +417,51 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(int64_t n, const flo
 
 // dS = P * (dP - sum_group(P * dP)) over groups of 64 columns (one head's
 // latents; SDPA softmax, latent_attention.py:72).  One wave per (row, group).
+template <typename TO>
 __global__ __launch_bounds__(256) void softmax64_bwd_kernel(int64_t n_groups, int64_t groups_per_row,
                                                             const float* __restrict__ p, int64_t ldp,
                                                             const float* __restrict__ dp, int64_t lddp,
-                                                            float* __restrict__ ds, int64_t ldds) {
+                                                            TO* __restrict__ ds, int64_t ldds) {
   const int lane = threadIdx.x & 63;
   for (int64_t gi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); gi < n_groups; gi += (int64_t)gridDim.x * 4) {
     const int64_t row = gi / groups_per_row, col = (gi % groups_per_row) * 64 + lane;
     const float pv = p[row * ldp + col], dv = dp[row * lddp + col];
     const float dot = wave_sum(pv * dv);
-    ds[row * ldds + col] = pv * (dv - dot);
+    stf<TO>(ds + row * ldds + col, pv * (dv - dot));
   }
 }
 
 __device__ __forceinline__ float gelu_exact(float g) { return 0.5f * g * (1.0f + erff(g * 0.70710678118654752440f)); }
 
 // z[:, j] = a_j * gelu(g_j),  a = G[:, :F], g = G[:, F:]  (GEGLU, latent_attention.py:24-27)
+template <typename TO>
+__device__ __forceinline__ void st4(TO* p, float a, float b, float c, float d) {
+  if constexpr (sizeof(TO) == 4) {
+    *reinterpret_cast<float4*>(p) = float4{a, b, c, d};
+  } else {
+    p[0] = (TO)a; p[1] = (TO)b; p[2] = (TO)c; p[3] = (TO)d;
+  }
+}
+
+template <typename TO>
 __global__ __launch_bounds__(256) void geglu_fwd_kernel(int64_t rows, int64_t f, const float* __restrict__ G,
-                                                        int64_t ldg, float* __restrict__ z, int64_t ldz) {
+                                                        int64_t ldg, TO* __restrict__ z, int64_t ldz) {
   const int64_t total = rows * f;
   for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < total; i += (int64_t)gridDim.x * 1024) {
     const int64_t r = i / f, c = i % f;  // f % 4 == 0: the 4 columns share a row
     const float4 a = *reinterpret_cast<const float4*>(G + r * ldg + c);
     const float4 g = *reinterpret_cast<const float4*>(G + r * ldg + f + c);
-    *reinterpret_cast<float4*>(z + r * ldz + c) =
-        float4{a.x * gelu_exact(g.x), a.y * gelu_exact(g.y), a.z * gelu_exact(g.z), a.w * gelu_exact(g.w)};
+    st4<TO>(z + r * ldz + c, a.x * gelu_exact(g.x), a.y * gelu_exact(g.y), a.z * gelu_exact(g.z),
+            a.w * gelu_exact(g.w));
   }
 }
 
 // dG[:, j] = dz_j gelu(g_j);  dG[:, F + j] = dz_j a_j gelu'(g_j),
 // gelu'(g) = Phi(g) + g phi(g)  (the derivative torch's gelu backward uses)
+template <typename TO>
 __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t rows, int64_t f, const float* __restrict__ G,
                                                         int64_t ldg, const float* __restrict__ dz, int64_t lddz,
-                                                        float* __restrict__ dG, int64_t lddg) {
+                                                        TO* __restrict__ dG, int64_t lddg) {
   const int64_t total = rows * f;
   for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i < total; i += (int64_t)gridDim.x * 1024) {
     const int64_t r = i / f, c = i % f;
@@ -465,8 +477,8 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t rows, int64_t f,
       da[t] = d[t] * g[t] * cdf;
       dg[t] = d[t] * a[t] * (cdf + g[t] * pdf);
     }
-    *reinterpret_cast<float4*>(dG + r * lddg + c) = float4{da[0], da[1], da[2], da[3]};
-    *reinterpret_cast<float4*>(dG + r * lddg + f + c) = float4{dg[0], dg[1], dg[2], dg[3]};
+    st4<TO>(dG + r * lddg + c, da[0], da[1], da[2], da[3]);
+    st4<TO>(dG + r * lddg + f + c, dg[0], dg[1], dg[2], dg[3]);
   }
 }
 
@@ -819,17 +831,22 @@ extern "C" int nr_layernorm_bwd(int64_t n, int64_t dim, const float* x, int64_t 
   return NR_OK;
 }
 
-extern "C" int nr_softmax64_bwd(int64_t rows, int64_t cols, const float* p, int64_t ldp, const float* dp,
-                                int64_t lddp, float* ds, int64_t ldds, void* stream) {
+extern "C" int nr_softmax64_bwd(int dtype_out, int64_t rows, int64_t cols, const float* p, int64_t ldp, const float* dp,
+                                int64_t lddp, void* ds, int64_t ldds, void* stream) {
   clear_error();
+  NR_CHECK_ARG(dtype_out == NR_F32 || dtype_out == NR_BF16, "nr_softmax64_bwd: dtype_out must be f32 or bf16");
   NR_CHECK_ARG(rows >= 0 && cols > 0 && cols % 64 == 0 && ldp >= cols && lddp >= cols && ldds >= cols,
                "nr_softmax64_bwd: bad args (cols must be a multiple of 64)");
   if (rows == 0) return NR_OK;
   NR_CHECK_ARG(p && dp && ds, "nr_softmax64_bwd: null pointer");
   NR_CHECK_DEVICE("nr_softmax64_bwd", p, dp, ds);
   const int64_t gpr = cols / 64, ng = rows * gpr;
-  hipLaunchKernelGGL(softmax64_bwd_kernel, dim3(rowwave_grid(ng)), dim3(256), 0, (hipStream_t)stream, ng, gpr, p, ldp,
-                     dp, lddp, ds, ldds);
+  if (dtype_out == NR_F32)
+    hipLaunchKernelGGL((softmax64_bwd_kernel<float>), dim3(rowwave_grid(ng)), dim3(256), 0, (hipStream_t)stream, ng,
+                       gpr, p, ldp, dp, lddp, (float*)ds, ldds);
+  else
+    hipLaunchKernelGGL((softmax64_bwd_kernel<__bf16>), dim3(rowwave_grid(ng)), dim3(256), 0, (hipStream_t)stream, ng,
+                       gpr, p, ldp, dp, lddp, (__bf16*)ds, ldds);
   NR_CHECK_LAUNCH("nr_softmax64_bwd");
   return NR_OK;
 }
@@ -839,24 +856,30 @@ static unsigned elem4_grid(int64_t total) {
   return (unsigned)(b < 4096 ? (b > 0 ? b : 1) : 4096);
 }
 
-extern "C" int nr_geglu_fwd(int64_t rows, int64_t f, const float* g, int64_t ldg, float* z, int64_t ldz,
+extern "C" int nr_geglu_fwd(int dtype_out, int64_t rows, int64_t f, const float* g, int64_t ldg, void* z, int64_t ldz,
                             void* stream) {
   clear_error();
+  NR_CHECK_ARG(dtype_out == NR_F32 || dtype_out == NR_BF16, "nr_geglu_fwd: dtype_out must be f32 or bf16");
   NR_CHECK_ARG(rows >= 0 && f > 0 && f % 4 == 0 && ldg >= 2 * f && ldz >= f && ldg % 4 == 0 && ldz % 4 == 0,
                "nr_geglu_fwd: bad args");
   if (rows == 0) return NR_OK;
   NR_CHECK_ARG(g && z, "nr_geglu_fwd: null pointer");
   NR_CHECK_DEVICE("nr_geglu_fwd", g, z);
   NR_CHECK_ARG((((uintptr_t)g | (uintptr_t)z) & 15) == 0, "nr_geglu_fwd: 16-byte alignment required");
-  hipLaunchKernelGGL(geglu_fwd_kernel, dim3(elem4_grid(rows * f)), dim3(256), 0, (hipStream_t)stream, rows, f, g, ldg,
-                     z, ldz);
+  if (dtype_out == NR_F32)
+    hipLaunchKernelGGL((geglu_fwd_kernel<float>), dim3(elem4_grid(rows * f)), dim3(256), 0, (hipStream_t)stream, rows,
+                       f, g, ldg, (float*)z, ldz);
+  else
+    hipLaunchKernelGGL((geglu_fwd_kernel<__bf16>), dim3(elem4_grid(rows * f)), dim3(256), 0, (hipStream_t)stream, rows,
+                       f, g, ldg, (__bf16*)z, ldz);
   NR_CHECK_LAUNCH("nr_geglu_fwd");
   return NR_OK;
 }
 
-extern "C" int nr_geglu_bwd(int64_t rows, int64_t f, const float* g, int64_t ldg, const float* dz, int64_t lddz,
-                            float* dg, int64_t lddg, void* stream) {
+extern "C" int nr_geglu_bwd(int dtype_out, int64_t rows, int64_t f, const float* g, int64_t ldg, const float* dz,
+                            int64_t lddz, void* dg, int64_t lddg, void* stream) {
   clear_error();
+  NR_CHECK_ARG(dtype_out == NR_F32 || dtype_out == NR_BF16, "nr_geglu_bwd: dtype_out must be f32 or bf16");
   NR_CHECK_ARG(rows >= 0 && f > 0 && f % 4 == 0 && ldg >= 2 * f && lddz >= f && lddg >= 2 * f && ldg % 4 == 0 &&
                    lddz % 4 == 0 && lddg % 4 == 0,
                "nr_geglu_bwd: bad args");
@@ -864,8 +887,12 @@ extern "C" int nr_geglu_bwd(int64_t rows, int64_t f, const float* g, int64_t ldg
   NR_CHECK_ARG(g && dz && dg, "nr_geglu_bwd: null pointer");
   NR_CHECK_DEVICE("nr_geglu_bwd", g, dz, dg);
   NR_CHECK_ARG((((uintptr_t)g | (uintptr_t)dz | (uintptr_t)dg) & 15) == 0, "nr_geglu_bwd: 16-byte alignment required");
-  hipLaunchKernelGGL(geglu_bwd_kernel, dim3(elem4_grid(rows * f)), dim3(256), 0, (hipStream_t)stream, rows, f, g, ldg,
-                     dz, lddz, dg, lddg);
+  if (dtype_out == NR_F32)
+    hipLaunchKernelGGL((geglu_bwd_kernel<float>), dim3(elem4_grid(rows * f)), dim3(256), 0, (hipStream_t)stream, rows,
+                       f, g, ldg, dz, lddz, (float*)dg, lddg);
+  else
+    hipLaunchKernelGGL((geglu_bwd_kernel<__bf16>), dim3(elem4_grid(rows * f)), dim3(256), 0, (hipStream_t)stream, rows,
+                       f, g, ldg, dz, lddz, (__bf16*)dg, lddg);
   NR_CHECK_LAUNCH("nr_geglu_bwd");
   return NR_OK;
 }

@@ -131,13 +131,14 @@ class _LatentItemFn(torch.autograd.Function):
         # GEMM operands in mm_dtype (bf16: MFMA bf16 operands, f32 accumulate and f32
         # outputs -- the LN / softmax / GEGLU kernels and the residual stream stay f32)
         c = (lambda t: t) if mm_dtype == f32 else (lambda t: ops.gather_rows(t, None, out_dtype=mm_dtype))
-        X = ops.layernorm(E, gq.contiguous(), bq.contiguous(), 1e-5)
-        P = ops.gemm(c(X), c(A), None, epilogue="softmax64", out_dtype=f32)
+        # X, Y, Z feed only GEMMs (here and as weight-grad operands): written in mm_dtype
+        X = ops.layernorm(E, gq.contiguous(), bq.contiguous(), 1e-5, out_dtype=mm_dtype)
+        P = ops.gemm(X, c(A), None, epilogue="softmax64", out_dtype=f32)
         H1 = ops.gemm(c(P), c(Bt), None, epilogue="resadd", residual=E, out_dtype=f32)
-        Y = ops.layernorm(H1, gf.contiguous(), bf.contiguous(), 1e-5)
-        G = ops.gemm(c(Y), c(W1), b1.contiguous(), out_dtype=f32)
-        Z = ops.geglu_fwd(G)
-        H = ops.gemm(c(Z), c(W2), b2.contiguous(), epilogue="resadd", residual=H1, out_dtype=f32)
+        Y = ops.layernorm(H1, gf.contiguous(), bf.contiguous(), 1e-5, out_dtype=mm_dtype)
+        G = ops.gemm(Y, c(W1), b1.contiguous(), out_dtype=f32)
+        Z = ops.geglu_fwd(G, out_dtype=mm_dtype)
+        H = ops.gemm(Z, c(W2), b2.contiguous(), epilogue="resadd", residual=H1, out_dtype=f32)
         ctx.save_for_backward(E, X, P, H1, Y, G, Z, A, Bt, gq, gf, W1, W2)
         ctx.Hs, ctx.mm_dtype = Hs, mm_dtype
         return H[:Hs]
@@ -154,12 +155,12 @@ class _LatentItemFn(torch.autograd.Function):
         c = (lambda t: t) if lo == f32 else (lambda t: ops.gather_rows(t, None, out_dtype=lo))
         T = lambda t: ops.transpose(t, out_dtype=lo)
         dZ = ops.gemm(c(dHp), T(W2), out_dtype=f32)
-        dG = ops.geglu_bwd(G, dZ)
-        dY = ops.gemm(c(dG), T(W1), out_dtype=f32)
+        dG = ops.geglu_bwd(G, dZ, out_dtype=lo)  # feeds GEMMs and the b1 column sum only
+        dY = ops.gemm(dG, T(W1), out_dtype=f32)
         dH1 = ops.layernorm_bwd(H1, gf.contiguous(), dY, 1e-5, residual=dHp)
         dP = ops.gemm(c(dH1), T(Bt), out_dtype=f32)
-        dS = ops.softmax64_bwd(P, dP)
-        dX = ops.gemm(c(dS), T(A), out_dtype=f32)
+        dS = ops.softmax64_bwd(P, dP, out_dtype=lo)
+        dX = ops.gemm(dS, T(A), out_dtype=f32)
         dE = ops.layernorm_bwd(E, gq.contiguous(), dX, 1e-5, residual=dH1)
         gW2 = torch.empty(W2.shape, dtype=f32, device=dev)
         gW1 = torch.empty(W1.shape, dtype=f32, device=dev)

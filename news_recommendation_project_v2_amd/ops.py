@@ -615,33 +615,34 @@ def layernorm_bwd(x: torch.Tensor, gamma: Optional[torch.Tensor], dy: torch.Tens
     return out
 
 
-def softmax64_bwd(p: torch.Tensor, dp: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dS of a softmax over groups of 64 columns, from its output p and upstream dp (f32)."""
+def softmax64_bwd(p: torch.Tensor, dp: torch.Tensor, out_dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    """dS of a softmax over groups of 64 columns, from its output p and upstream dp
+    (f32 inputs; dS f32 or bf16)."""
     _f32(p, "p")
     _f32(dp, "dp")
-    out = torch.empty_like(p) if out is None else out
+    out = torch.empty(p.shape, dtype=out_dtype, device=p.device)
     dev = _dev(p, dp, out)
-    _lib.call("nr_softmax64_bwd", p.shape[0], p.shape[1], _ptr(p), _rowmajor(p, "p"), _ptr(dp), _rowmajor(dp, "dp"),
-              _ptr(out), _rowmajor(out, "out"), _stream(dev))
+    _lib.call("nr_softmax64_bwd", _dtype(out, "out"), p.shape[0], p.shape[1], _ptr(p), _rowmajor(p, "p"), _ptr(dp),
+              _rowmajor(dp, "dp"), _ptr(out), _rowmajor(out, "out"), _stream(dev))
     return out
 
 
-def geglu_fwd(g: torch.Tensor) -> torch.Tensor:
-    """a * gelu(gates) with a, gates = g.chunk(2, -1) (f32, exact erf)."""
+def geglu_fwd(g: torch.Tensor, out_dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    """a * gelu(gates) with a, gates = g.chunk(2, -1) (f32 in, exact erf; out f32 or bf16)."""
     _f32(g, "g")
     f = g.shape[1] // 2
-    z = torch.empty((g.shape[0], f), dtype=torch.float32, device=g.device)
+    z = torch.empty((g.shape[0], f), dtype=out_dtype, device=g.device)
     dev = _dev(g, z)
-    _lib.call("nr_geglu_fwd", g.shape[0], f, _ptr(g), _rowmajor(g, "g"), _ptr(z), f, _stream(dev))
+    _lib.call("nr_geglu_fwd", _dtype(z, "z"), g.shape[0], f, _ptr(g), _rowmajor(g, "g"), _ptr(z), f, _stream(dev))
     return z
 
 
-def geglu_bwd(g: torch.Tensor, dz: torch.Tensor) -> torch.Tensor:
+def geglu_bwd(g: torch.Tensor, dz: torch.Tensor, out_dtype: torch.dtype = torch.float32) -> torch.Tensor:
     _f32(g, "g")
     _f32(dz, "dz")
     f = g.shape[1] // 2
-    dg = torch.empty_like(g)
+    dg = torch.empty(g.shape, dtype=out_dtype, device=g.device)
     dev = _dev(g, dz, dg)
-    _lib.call("nr_geglu_bwd", g.shape[0], f, _ptr(g), _rowmajor(g, "g"), _ptr(dz), _rowmajor(dz, "dz"), _ptr(dg),
-              _rowmajor(dg, "dg"), _stream(dev))
+    _lib.call("nr_geglu_bwd", _dtype(dg, "dg"), g.shape[0], f, _ptr(g), _rowmajor(g, "g"), _ptr(dz), _rowmajor(dz, "dz"),
+              _ptr(dg), _rowmajor(dg, "dg"), _stream(dev))
     return dg

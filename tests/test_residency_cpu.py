@@ -70,9 +70,9 @@ def _calls(P):
         "nr_ln_param_grad": (F32, 2, 1024, P, 1024, P, f(1e-12), P, 1024, P, P, None),
         "nr_sumsq": (16, P, P, None),
         "nr_layernorm_bwd": (2, 1024, P, 1024, P, f(1e-5), P, 1024, None, 0, P, 1024, None),
-        "nr_softmax64_bwd": (2, 128, P, 128, P, 128, P, 128, None),
-        "nr_geglu_fwd": (2, 64, P, 128, P, 64, None),
-        "nr_geglu_bwd": (2, 64, P, 128, P, 64, P, 128, None),
+        "nr_softmax64_bwd": (F32, 2, 128, P, 128, P, 128, P, 128, None),
+        "nr_geglu_fwd": (BF16, 2, 64, P, 128, P, 64, None),
+        "nr_geglu_bwd": (F32, 2, 64, P, 128, P, 64, P, 128, None),
         "nr_adamw": (16, P, P, P, P, None, 1, f(1e-6), f(0.9), f(0.999), f(1e-8), f(0.01), f(0.5), P, None),
         "nr_splitk_fixup": (F32, _lib.NR_EPI_NONE, 2, 256, 2, P, P, None, 0, P, 256, 0, 0, f(0.0), f(1.0), None),
     }
