@@ -371,8 +371,8 @@ class LatentAttentionTrainStep:
         E = ops.gather_layernorm(batch.tok_last, None, self.views["ln.weight"].view(1, D),
                                  self.views["ln.bias"].view(1, D), self.ln_eps)
         S = ops.gather_rows(E, batch.hist_idx, out_dtype=torch.float32).requires_grad_(True)
-        for _, p in self._lat_params:
-            p.grad = None
+        for name, p in self._lat_params:
+            p.grad = self.gviews[name]  # autograd accumulates in place into the (zeroed) flat grad slices
         with torch.enable_grad():
             u = segment_mean(self.model._train_items(S, mm_dtype=self.dtype), batch.hist_off)
             u = torch.nn.functional.normalize(u, p=2, dim=-1)
@@ -384,7 +384,9 @@ class LatentAttentionTrainStep:
         ops.scatter_add_rows(S.grad, batch.hist_idx, dE)
         ops.ln_param_grad(batch.tok_last, None, self.ln_eps, dE, self.gviews["ln.weight"], self.gviews["ln.bias"])
         for name, p in self._lat_params:
-            self.gviews[name].copy_(p.grad)
+            g = self.gviews[name]
+            if p.grad is not None and p.grad.data_ptr() != g.data_ptr():
+                g.copy_(p.grad)  # autograd replaced the slice instead of accumulating into it
             p.grad = None
         return self.loss, users, E
 
