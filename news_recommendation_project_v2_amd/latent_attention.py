@@ -124,8 +124,9 @@ class _LatentItemFn(torch.autograd.Function):
         Hs, D = rows.shape
         Hp = _pad64(Hs)
         dev = rows.device
-        E = torch.zeros((Hp, D), dtype=torch.float32, device=dev)
+        E = torch.empty((Hp, D), dtype=torch.float32, device=dev)
         E[:Hs] = rows
+        E[Hs:].zero_()
         A, Bt, W1, W2 = A.contiguous(), Bt.contiguous(), W1.contiguous(), W2.contiguous()
         f32 = torch.float32
         # GEMM operands in mm_dtype (bf16: MFMA bf16 operands, f32 accumulate and f32
@@ -150,8 +151,9 @@ class _LatentItemFn(torch.autograd.Function):
         Hp, D = E.shape
         dev = E.device
         f32 = torch.float32
-        dHp = torch.zeros((Hp, D), dtype=f32, device=dev)
-        dHp[:Hs] = dH.float()
+        dHp = torch.empty((Hp, D), dtype=f32, device=dev)
+        dHp[:Hs] = dH
+        dHp[Hs:].zero_()
         c = (lambda t: t) if lo == f32 else (lambda t: ops.gather_rows(t, None, out_dtype=lo))
         T = lambda t: ops.transpose(t, out_dtype=lo)
         dZ = ops.gemm(c(dHp), T(W2), out_dtype=f32)
