@@ -297,6 +297,24 @@ def config2_leg(dev, n_news: int = 8192) -> dict:
     return out
 
 
+def host_parse_leg(n_news: int, rows: int = 100_000) -> dict:
+    """SURVEY §8(d) 'report separately: host parsing (A1)': the native behaviours
+    parser (split_impressions_and_history, libnewsrec_host.so) on the first
+    `rows` MIND-large-dev-shaped behaviours lines (synthetic text of the
+    headline's impressions), host time."""
+    from news_recommendation_project_v2_amd import native
+    imps = synthetic.mind_impressions(n_news, rows, seed=1234)
+    hist, impr = synthetic.to_behaviors(imps)
+    nbytes = sum(map(len, impr)) + sum(len(h) for h in hist if h)
+    native.split_behaviors(impr[:1000], hist[:1000])  # load the library
+    t0 = time.perf_counter()
+    out = native.split_behaviors(impr, hist)
+    dt = time.perf_counter() - t0
+    assert out is not None
+    return {"rows": rows, "text_MB": round(nbytes / 1e6, 1), "seconds": round(dt, 3),
+            "rows_per_s": round(rows / dt, 1), "MB_per_s": round(nbytes / dt / 1e6, 1)}
+
+
 def hipblaslt_yardstick(pooler: str, n: int, ours_ms: float, dev, reps: int = 5) -> dict:
     """The same per-news transform GEMM shapes (M = n) as bare torch.matmul
     (hipBLASLt: bf16, no bias, no LayerNorm, no epilogue, so less work than
@@ -717,6 +735,7 @@ def main():
         extra["shared_histories"] = sh
         del im
         extra["metrics_ms"] = round(metrics_ms(head), 3)
+        extra["host_parse_A1"] = host_parse_leg(n_news)
         if args.dtype == "bf16":
             extra["transform_vs_hipblaslt"] = hipblaslt_yardstick(args.pooler, n_news, head.split_ms[0], dev)
         # PCIe-side costs (never part of `value`): the CSR index upload incl. its host-side
