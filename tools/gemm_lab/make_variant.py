@@ -331,6 +331,17 @@ VARIANTS = {
       dmaB(0, st, kf);
       dmaB(1, st, kf);"""),
     ],
+    # the persistent kernel's MFMA phases without s_setprio (gemm256t only)
+    "noprio_t": [
+        ("""  __builtin_amdgcn_s_setprio(1);                       \\
+  mma(QM, NI, FB);                                     \\
+  __builtin_amdgcn_s_setprio(0);                       \\
+  __builtin_amdgcn_s_barrier();
+  // K step kt of the current tile (stage st).""",
+         """  mma(QM, NI, FB);                                     \\
+  __builtin_amdgcn_s_barrier();
+  // K step kt of the current tile (stage st)."""),
+    ],
     # DIAGNOSTIC (wrong results): no operand DMAs inside the K loop
     "nodma": [
         ("  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {\n    const int ns = st ^ 1;\n"
