@@ -15,13 +15,15 @@ computes between loading the table and ranking.
 Multi-GPU (one process per GPU, RCCL over xGMI).  ``--gpus N`` with no
 WORLD_SIZE in the environment re-launches this script under
 ``torch.distributed.run`` with N ranks (as a child process, before any GPU
-call).  Default ``--scaling strong`` = configs[3]: ONE MIND-large-dev set;
-every rank transforms 1/N of the news table, one RCCL all-gather gives every
-GPU the whole table, impressions are split into N contiguous cost-balanced
-ranges (``partition_by_cost``) and each rank pools + scores its range.  The
-step is timed from a barrier to the last rank's completion (max over ranks)
-and ``value`` = the set's candidates / that time.  ``--scaling weak`` (and
-the ``weak_scaling`` extra at N > 1) gives every rank its own full set.
+call).  Every rank transforms 1/N of the news table and one RCCL all-gather
+gives every GPU the whole table (the path's one exchange step); impressions
+are the shard unit.  Default ``--scaling weak``: every rank pools + scores
+its own full MIND-large-dev-sized impression set (per-GPU work fixed as N
+grows, rank 0's set = the N = 1 set); ``value`` = all ranks' candidates / the
+step time, timed from a barrier to the last rank's completion (max over
+ranks).  ``--scaling strong`` (and the ``strong_scaling`` extra at N > 1) is
+configs[3] as ONE eval job: one set split into N contiguous cost-balanced
+ranges (``partition_by_cost``).
 
 Also reported in the same JSON line:
   roofline      the pool+score kernel (dominant; a random-row gather served by
@@ -532,9 +534,15 @@ def dry_run(args, rank: int, world: int) -> None:
     plumbing without the GPU (what the CPU test suite can check)."""
     n_news, n_imp = synthetic.SHAPES[args.shape]
     n_imp = args.impressions or n_imp
-    full = synthetic.mind_impressions(n_news, n_imp, seed=1234)
-    b = partition_by_cost(full.hist_len, full.cand_len, world, 1024 * 2, 1024 * 2)
-    mine = full.slice(int(b[rank]), int(b[rank + 1]))
+    if args.scaling == "strong":
+        full = synthetic.mind_impressions(n_news, n_imp, seed=1234)
+        b = partition_by_cost(full.hist_len, full.cand_len, world, 1024 * 2, 1024 * 2)
+        mine = full.slice(int(b[rank]), int(b[rank + 1]))
+        expected = full.n_cand
+    else:  # every rank its own set; rank r's candidates summed over the ranks
+        b = None
+        mine = synthetic.mind_impressions(n_news, n_imp, seed=1234 + rank)
+        expected = sum(synthetic.mind_impressions(n_news, n_imp, seed=1234 + r).n_cand for r in range(world))
     rows = (n_news + world - 1) // world
     local = torch.full((rows, 4), float(rank))
     table = torch.empty((rows * world, 4))
@@ -549,8 +557,9 @@ def dry_run(args, rank: int, world: int) -> None:
     if rank == 0:
         print(json.dumps({"metric": "scored candidates/sec on MIND-large impressions; AUC parity vs CPU ref",
                           "dry_run": True, "value": None, "n_gpus": world, "scaling": args.scaling,
-                          "partition": [int(x) for x in b], "candidates_total": int(c[0]),
-                          "impressions_total": int(c[1]), "candidates_expected": full.n_cand,
+                          "partition": [int(x) for x in b] if b is not None else None,
+                          "candidates_total": int(c[0]),
+                          "impressions_total": int(c[1]), "candidates_expected": int(expected),
                           "allgather_ok": ok, "allgather_s": float(t.item())}), flush=True)
 
 
@@ -563,8 +572,9 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--shape", default="mind_large_dev", choices=list(synthetic.SHAPES))
     ap.add_argument("--impressions", type=int, default=0, help="override the shape's impression count")
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
-                    help="strong: one set partitioned over the ranks (configs[3]); weak: a full set per rank")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak",
+                    help="weak (default): a full MIND-large-dev-sized set per rank, the per-GPU work fixed as N "
+                         "grows; strong: one set partitioned over the ranks (configs[3] as one eval job)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: test mode, ranks may share one GPU (tables staged through the host)")
     ap.add_argument("--cpu-shape", default="mind_small_dev", choices=list(synthetic.SHAPES))
@@ -662,7 +672,7 @@ def main():
         extra["allgather_GBs_in_per_gpu"] = round(gb_in / (g_ms * 1e-3) / 1e9, 1) if g_ms > 0 else None
         extra["transform_chunks"] = head.tab.chunks
 
-    if world > 1 and not args.no_extra and args.scaling == "strong":
+    if world > 1 and not args.no_extra:
         # the opt-in overlapped build (2 chunks, each chunk's all-gather beside the next
         # chunk's transform): its step time, and its table against the default's bit for bit
         ref_table = head.tab.full.clone()
@@ -676,15 +686,22 @@ def main():
                                          "table_bit_identical": bool(same.item())}
         del r, ref_table
         torch.cuda.empty_cache()
-        # weak scaling as an extra: every rank its own full MIND-large-dev-sized set
-        own = synthetic.mind_impressions(n_news, n_imp, seed=1234 + rank)
-        r = Run(args.pooler, args.dtype, own, table, dev, rank, world)
+        # the other scaling mode as an extra
+        if args.scaling == "strong":  # every rank its own full MIND-large-dev-sized set
+            other = synthetic.mind_impressions(n_news, n_imp, seed=1234 + rank)
+        else:  # configs[3] as ONE eval job: the rank-0 set partitioned over the ranks
+            one = synthetic.mind_impressions(n_news, n_imp, seed=1234)
+            ob = partition_by_cost(one.hist_len, one.cand_len, world, kw * 1024 * es, 1024 * es)
+            other = one.slice(int(ob[rank]), int(ob[rank + 1]))
+            del one
+        r = Run(args.pooler, args.dtype, other, table, dev, rank, world)
         d = timed(r.step, max(3, args.steps // 2), 2, world, dev, host_reduce) / max(3, args.steps // 2)
-        c = torch.tensor([own.n_cand], dtype=torch.int64, device="cpu" if host_reduce else dev)
+        c = torch.tensor([other.n_cand], dtype=torch.int64, device="cpu" if host_reduce else dev)
         dist.all_reduce(c)
-        extra["weak_scaling"] = {"value": round(int(c.item()) / d, 1), "ms_per_step": round(d * 1e3, 3),
-                                 "impressions_per_gpu": own.n_imp}
-        del r, own
+        key = "weak_scaling" if args.scaling == "strong" else "strong_scaling"
+        extra[key] = {"value": round(int(c.item()) / d, 1), "ms_per_step": round(d * 1e3, 3),
+                      "impressions_per_gpu_rank0": other.n_imp}
+        del r, other
         torch.cuda.empty_cache()
 
     if world == 1 and not args.no_extra:
