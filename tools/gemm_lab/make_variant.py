@@ -4,6 +4,12 @@ of csrc/gemm.hip with one named change, link it with the other objects into
 tools/gemm_lab/libnewsrec_<name>.so for tools/gemm_ab.py.
 
     python tools/gemm_lab/make_variant.py flatdma
+
+Each variant is a set of exact-text patches against gemm.hip AS IT WAS when
+that A/B ran (recorded in DESIGN.md §3.2 / profiles/round*/): adopted ones
+(quarters, dma2, fastexp) are in the source now, and patches written against
+an older main loop no longer apply (the script then stops at the failing
+assert instead of building a wrong library).
 """
 import subprocess
 import sys
