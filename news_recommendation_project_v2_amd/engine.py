@@ -41,6 +41,23 @@ def _may_repeat(hist_idx: np.ndarray, hist_len: np.ndarray) -> bool:
     return 1.0 - len(np.unique(key)) / len(hist_len) >= DEDUPE_MIN_SHARE
 
 
+def _check_segments(idx: np.ndarray, lens: np.ndarray, what: str) -> int:
+    """Validate one CSR index set on the host; returns its largest row (-1 if
+    empty).  Negative lengths, a length sum that does not match the index
+    array (the offsets would run past it on the device) and negative rows are
+    refused; rows past a table are refused once the table size is known."""
+    if len(lens) and int(lens.min()) < 0:
+        raise ValueError(f"{what} lengths must be >= 0")
+    if int(lens.sum()) != len(idx):
+        raise ValueError(f"{what} lengths sum to {int(lens.sum())} but {len(idx)} indices were given")
+    if not len(idx):
+        return -1
+    lo, hi = int(idx.min()), int(idx.max())
+    if lo < 0:
+        raise IndexError(f"{what} index {lo} is negative (rows are 0-based indices into the news table)")
+    return hi
+
+
 class PoolScoreEngine:
     def __init__(self, model: torch.nn.Module, dtype: torch.dtype = torch.float32,
                  device: Optional[torch.device] = None):
@@ -64,6 +81,7 @@ class PoolScoreEngine:
             self.hist_src = query_news_embeddings.to(self.device, self.dtype).contiguous()
         else:
             self.hist_src = self.cand_table
+        self._check_rows()
         return self
 
     def load_impressions(self, hist_idx, hist_len, cand_idx, cand_len, dedupe: Optional[bool] = None):
@@ -77,11 +95,18 @@ class PoolScoreEngine:
             raise ValueError("Number of rows should be consistent")  # data_model_helper.py:183-185
         hist_idx = np.ascontiguousarray(hist_idx, dtype=np.int32)
         hist_len = np.asarray(hist_len, dtype=np.int64)
+        cand_idx = np.ascontiguousarray(cand_idx, dtype=np.int32)
+        cand_len_a = np.asarray(cand_len, dtype=np.int64)
+        # the kernels index tables with these rows: an out-of-range row would be an
+        # out-of-bounds device read, so refuse it here as torch indexing does (IndexError)
+        self._max_row = {"hist": _check_segments(hist_idx, hist_len, "history"),
+                         "cand": _check_segments(cand_idx, cand_len_a, "candidate")}
+        self._check_rows()
         self.hist_idx = torch.as_tensor(hist_idx).to(dev)
         self.hist_off = torch.as_tensor(lengths_to_offsets(hist_len)).to(dev)
-        self.cand_idx = torch.as_tensor(np.ascontiguousarray(cand_idx, dtype=np.int32)).to(dev)
-        self.cand_off = torch.as_tensor(lengths_to_offsets(cand_len)).to(dev)
-        self.n_cand = int(np.asarray(cand_len, dtype=np.int64).sum())
+        self.cand_idx = torch.as_tensor(cand_idx).to(dev)
+        self.cand_off = torch.as_tensor(lengths_to_offsets(cand_len_a)).to(dev)
+        self.n_cand = int(cand_len_a.sum())
         self.n_imp = len(cand_len)
         self.user_idx = None
         self.shared_history_share = 0.0
@@ -121,6 +146,17 @@ class PoolScoreEngine:
     def inv_norms(self) -> torch.Tensor:
         self.cand_inv = ops.row_inv_norm(self.cand_table, 1e-8, out=self.cand_inv)
         return self.cand_inv
+
+    def _check_rows(self) -> None:
+        """Host-side: every index row of the loaded impressions exists in the loaded
+        tables (no device sync; the maxima were taken at load_impressions)."""
+        mr = getattr(self, "_max_row", None)
+        if mr is None:
+            return
+        for name, table in (("hist", self.hist_src), ("cand", self.cand_table)):
+            if table is not None and mr[name] >= table.shape[0]:
+                raise IndexError(f"{'history' if name == 'hist' else 'candidate'} index {mr[name]} is out of bounds "
+                                 f"for dimension 0 with size {table.shape[0]}")
 
     def pool_score(self, want_users: bool = False, scores: Optional[torch.Tensor] = None):
         if self.user_idx is not None:  # distinct histories pooled once, then scored per impression

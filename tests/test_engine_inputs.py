@@ -1,0 +1,62 @@
+"""Host-side input validation of PoolScoreEngine.load_impressions / load_news.
+
+The device kernels index the news tables with the CSR rows, so a row past a
+table (or offsets that run past the index array) would be an out-of-bounds
+device read.  The reference gathers rows by array indexing (e.g.
+data_model_helper.py:284), which raises IndexError; the engine refuses the same
+inputs on the host before any upload.  CPU-only: validation runs before .to().
+"""
+import numpy as np
+import pytest
+import torch
+
+from news_recommendation_project_v2_amd.engine import PoolScoreEngine
+
+
+def _engine(n_rows=None):
+    eng = PoolScoreEngine.__new__(PoolScoreEngine)
+    eng.device = torch.device("cpu")
+    eng.dtype = torch.float32
+    eng.cand_table = eng.hist_src = None
+    if n_rows is not None:
+        eng.cand_table = eng.hist_src = torch.zeros(n_rows, 4)
+    return eng
+
+
+def _i(*v):
+    return np.asarray(v, dtype=np.int32)
+
+
+def test_candidate_row_past_table_raises():
+    eng = _engine(10)
+    with pytest.raises(IndexError, match="candidate index 10 is out of bounds"):
+        eng.load_impressions(_i(1, 2), [2], _i(3, 10), [2])
+
+
+def test_history_row_past_table_raises():
+    eng = _engine(10)
+    with pytest.raises(IndexError, match="history index 12"):
+        eng.load_impressions(_i(12), [1], _i(3), [1])
+
+
+def test_negative_row_raises():
+    eng = _engine(10)
+    with pytest.raises(IndexError, match="negative"):
+        eng.load_impressions(_i(-1), [1], _i(3), [1])
+
+
+def test_lengths_must_cover_index_array():
+    eng = _engine(10)
+    with pytest.raises(ValueError, match="sum to 3 but 2"):
+        eng.load_impressions(_i(1, 2), [3], _i(3), [1])
+    with pytest.raises(ValueError, match=">= 0"):
+        eng.load_impressions(_i(1, 2), [3, -1], _i(3, 4), [1, 1])
+
+
+def test_table_loaded_after_impressions_is_checked():
+    eng = _engine(None)
+    eng._max_row = {"hist": 4, "cand": 7}
+    eng._check_rows()  # no tables yet: nothing to check
+    with pytest.raises(IndexError, match="candidate index 7 is out of bounds for dimension 0 with size 5"):
+        eng.load_news(torch.zeros(5, 4), torch.zeros(8, 4))
+    eng.load_news(torch.zeros(8, 4), torch.zeros(5, 4))  # history 4 < 5, candidate 7 < 8
