@@ -383,6 +383,90 @@ VARIANTS = {
          "hipLaunchKernelGGL((gemm256w4_kernel<NR_EPI_SOFTMAX64, true>), grid, dim3(256),"),
     ],
     # no s_setprio around the MFMA phases
+    # GEGLU epilogue: the gelu of two accumulator values at once on float2 vectors, so the
+    # erfc polynomial and the affine steps issue as v_pk_fma_f32 / v_pk_mul_f32 (SGPR
+    # splat coefficients) instead of scalar v_fmaak_f32; per element the same fma
+    # sequence (bit-identical), rcp / exp stay scalar
+    "gelu2": [
+        ("__device__ __forceinline__ float epi_exp(float x) { return __expf(x); }\n",
+         """__device__ __forceinline__ float epi_exp(float x) { return __expf(x); }
+
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2v fma2(f32x2v a, f32x2v b, f32x2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2v gelu_erf2(f32x2v g) {
+  const f32x2v x = g * 0.70710678118654752440f;
+  const f32x2v z = __builtin_elementwise_abs(x);
+  f32x2v t = fma2((f32x2v)0.5f, z, (f32x2v)1.0f);
+  t.x = __builtin_amdgcn_rcpf(t.x);
+  t.y = __builtin_amdgcn_rcpf(t.y);
+  f32x2v p = (f32x2v)0.17087277f;
+  p = fma2(p, t, (f32x2v)-0.82215223f);
+  p = fma2(p, t, (f32x2v)1.48851587f);
+  p = fma2(p, t, (f32x2v)-1.13520398f);
+  p = fma2(p, t, (f32x2v)0.27886807f);
+  p = fma2(p, t, (f32x2v)-0.18628806f);
+  p = fma2(p, t, (f32x2v)0.09678418f);
+  p = fma2(p, t, (f32x2v)0.37409196f);
+  p = fma2(p, t, (f32x2v)1.00002368f);
+  const f32x2v w = fma2(t, p, fma2(-z, z, (f32x2v)-1.26551223f));
+  const f32x2v ans = t * (f32x2v){__expf(w.x), __expf(w.y)};
+  const f32x2v pos = g * fma2((f32x2v)-0.5f, ans, (f32x2v)1.0f);
+  const f32x2v neg = (0.5f * g) * ans;
+  return (f32x2v){x.x >= 0.f ? pos.x : neg.x, x.y >= 0.f ? pos.y : neg.y};
+}
+"""),
+        ("""          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = acc[mi][ni][r] * gelu_erf(acc[mi][ni + 2][r]);
+          pk[ni] = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};""",
+         """          const f32x2v o0 = (f32x2v){acc[mi][ni][0], acc[mi][ni][1]} *
+                            gelu_erf2((f32x2v){acc[mi][ni + 2][0], acc[mi][ni + 2][1]});
+          const f32x2v o1 = (f32x2v){acc[mi][ni][2], acc[mi][ni][3]} *
+                            gelu_erf2((f32x2v){acc[mi][ni + 2][2], acc[mi][ni + 2][3]});
+          pk[ni] = uint2{pack_bf16x2(o0.x, o0.y), pack_bf16x2(o1.x, o1.y)};"""),
+    ],
+    # gelu2 with the two float2 chains of a 4-column group interleaved statement by
+    # statement (two independent v_pk_fma_f32 chains instead of one dependent one)
+    "gelu4": [
+        ("__device__ __forceinline__ float epi_exp(float x) { return __expf(x); }\n",
+         """__device__ __forceinline__ float epi_exp(float x) { return __expf(x); }
+
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2v fma2(f32x2v a, f32x2v b, f32x2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ void gelu_erf2x2(f32x2v& g0, f32x2v& g1) {
+  const f32x2v x0 = g0 * 0.70710678118654752440f, x1 = g1 * 0.70710678118654752440f;
+  const f32x2v z0 = __builtin_elementwise_abs(x0), z1 = __builtin_elementwise_abs(x1);
+  f32x2v t0 = fma2((f32x2v)0.5f, z0, (f32x2v)1.0f), t1 = fma2((f32x2v)0.5f, z1, (f32x2v)1.0f);
+  t0.x = __builtin_amdgcn_rcpf(t0.x);
+  t1.x = __builtin_amdgcn_rcpf(t1.x);
+  t0.y = __builtin_amdgcn_rcpf(t0.y);
+  t1.y = __builtin_amdgcn_rcpf(t1.y);
+  f32x2v p0 = (f32x2v)0.17087277f, p1 = (f32x2v)0.17087277f;
+#define NR_G4(c) p0 = fma2(p0, t0, (f32x2v)(c)); p1 = fma2(p1, t1, (f32x2v)(c));
+  NR_G4(-0.82215223f) NR_G4(1.48851587f) NR_G4(-1.13520398f) NR_G4(0.27886807f)
+  NR_G4(-0.18628806f) NR_G4(0.09678418f) NR_G4(0.37409196f) NR_G4(1.00002368f)
+#undef NR_G4
+  const f32x2v w0 = fma2(t0, p0, fma2(-z0, z0, (f32x2v)-1.26551223f));
+  const f32x2v w1 = fma2(t1, p1, fma2(-z1, z1, (f32x2v)-1.26551223f));
+  const f32x2v a0 = t0 * (f32x2v){__expf(w0.x), __expf(w0.y)};
+  const f32x2v a1 = t1 * (f32x2v){__expf(w1.x), __expf(w1.y)};
+  const f32x2v q0 = g0 * fma2((f32x2v)-0.5f, a0, (f32x2v)1.0f), q1 = g1 * fma2((f32x2v)-0.5f, a1, (f32x2v)1.0f);
+  const f32x2v n0 = (0.5f * g0) * a0, n1 = (0.5f * g1) * a1;
+  g0 = (f32x2v){x0.x >= 0.f ? q0.x : n0.x, x0.y >= 0.f ? q0.y : n0.y};
+  g1 = (f32x2v){x1.x >= 0.f ? q1.x : n1.x, x1.y >= 0.f ? q1.y : n1.y};
+}
+"""),
+        ("""          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = acc[mi][ni][r] * gelu_erf(acc[mi][ni + 2][r]);
+          pk[ni] = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};""",
+         """          f32x2v g0 = (f32x2v){acc[mi][ni + 2][0], acc[mi][ni + 2][1]};
+          f32x2v g1 = (f32x2v){acc[mi][ni + 2][2], acc[mi][ni + 2][3]};
+          gelu_erf2x2(g0, g1);
+          const f32x2v o0 = (f32x2v){acc[mi][ni][0], acc[mi][ni][1]} * g0;
+          const f32x2v o1 = (f32x2v){acc[mi][ni][2], acc[mi][ni][3]} * g1;
+          pk[ni] = uint2{pack_bf16x2(o0.x, o0.y), pack_bf16x2(o1.x, o1.y)};"""),
+    ],
     "noprio": [
         ("  __builtin_amdgcn_s_setprio(1);                       \\\n  mma(QM, NI, FB);                                     \\\n"
          "  __builtin_amdgcn_s_setprio(0);                       \\\n",
