@@ -352,7 +352,8 @@ int nr_row_stats(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ld
  * nr_embed_ln: out[t] = LN(word[ids[t]] + type[0] + pos_emb[pos[t]]), dim 1024.
  * nr_attention_varlen: qkv [T][3072] (q | k | v, 16 heads x 64 per part),
  *   cu_seqlens int32 [n_seq+1], qblock_off int32 [n_seq+1] = prefix sum of
- *   ceil(L_i / 32), n_qblocks = qblock_off[n_seq]; ctx [T][1024].
+ *   ceil(L_i / 32), n_qblocks >= qblock_off[n_seq] (an upper bound is allowed:
+ *   the exact count is read on the device), n_qblocks < 2^22; ctx [T][1024].
  */
 int nr_embed_ln(int dtype, int64_t n_tokens, const int32_t* ids, const int32_t* pos, const void* word,
                 const void* pos_emb, const void* type_emb, const float* gamma, const float* beta, float eps,

@@ -72,17 +72,29 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(int64_t T, const int32_t*
 // segments.  Scale 1/8 is folded into Q exactly (power of two).
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// Bijection of [0, n): dispatch slot s (XCD s % 8) -> a contiguous run of ids per XCD.
+__device__ __forceinline__ int xcd_contiguous(int s, int n) {
+  const int xcd = s & 7, q = n >> 3, r = n & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (s >> 3);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qkv, const int32_t* __restrict__ cu,
                                                         const int32_t* __restrict__ qoff, int32_t n_seq,
                                                         T* __restrict__ ctx) {
   constexpr int D = 1024, LD = 3 * D, HD = 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = blockIdx.y * 4 + wave;     // head
-  const int qb_global = blockIdx.x;        // global query-block index
-  // nr_encoder_forward launches an upper bound of query blocks (the exact count
-  // lives on the device): blocks past the last one exit (block-uniform)
-  if (qb_global >= qoff[n_seq]) return;
+  // 1-D grid of 4 x (an upper bound of) the query blocks; nr_encoder_forward
+  // launches the bound, the exact count lives on the device.  Dispatch slots
+  // past the 4 x total work items exit (block-uniform); the others are remapped
+  // XCD-contiguous (slot s runs on XCD s % 8), so the query blocks of one
+  // sequence, which re-read its K/V rows, share one XCD's L2.
+  const int total = qoff[n_seq];
+  const int slot = blockIdx.x;
+  if (slot >= 4 * total) return;
+  const int item = xcd_contiguous(slot, 4 * total);
+  const int h = (item / total) * 4 + wave;  // head
+  const int qb_global = item % total;       // global query-block index
   // 64-ary search for the sequence owning this query block (qoff: prefix of
   // ceil(L/32), qoff[n_seq] = total): each step probes 64 boundaries with one
   // wave load + ballot, so 20k sequences take 3 dependent loads, not 15.
@@ -510,8 +522,9 @@ extern "C" int nr_attention_varlen(int dtype, int32_t n_seq, int64_t n_qblocks, 
   if (n_seq <= 0 || n_qblocks <= 0) return NR_OK;
   NR_CHECK_ARG(qkv && cu_seqlens && qblock_off && ctx, "nr_attention_varlen: null pointer");
   NR_CHECK_DEVICE("nr_attention_varlen", qkv, cu_seqlens, qblock_off, ctx);
-  NR_CHECK_ARG(n_qblocks <= 0x7fffffff, "nr_attention_varlen: too many query blocks");
-  const dim3 grid((unsigned)n_qblocks, 4);  // 4 blocks x 4 waves = 16 heads
+  // 4 workgroups x 4 waves = 16 heads per query block; 256 x grid fits in 32 bits
+  NR_CHECK_ARG(n_qblocks <= (1 << 22) - 1, "nr_attention_varlen: too many query blocks");
+  const dim3 grid((unsigned)(4 * n_qblocks));
   hipStream_t s = (hipStream_t)stream;
   if (dtype == NR_F32)
     hipLaunchKernelGGL(nr::attention_kernel<float>, grid, dim3(256), 0, s, (const float*)qkv, cu_seqlens,
