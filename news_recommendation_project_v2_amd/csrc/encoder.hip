@@ -79,9 +79,9 @@ __device__ __forceinline__ int xcd_contiguous(int s, int n) {
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qkv, const int32_t* __restrict__ cu,
-                                                        const int32_t* __restrict__ qoff, int32_t n_seq,
-                                                        T* __restrict__ ctx) {
+__device__ __forceinline__ void attention_body(const T* __restrict__ qkv, const int32_t* __restrict__ cu,
+                                               const int32_t* __restrict__ qoff, int32_t n_seq,
+                                               T* __restrict__ ctx) {
   constexpr int D = 1024, LD = 3 * D, HD = 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // 1-D grid of 4 x (an upper bound of) the query blocks; nr_encoder_forward
@@ -209,6 +209,10 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
         const int vr = min(kb + 8 * i + (lane >> 3), L - 1);
         vt[i] = *reinterpret_cast<const uint4*>(qkv + (s0 + vr) * LD + vcol + 8 * (lane & 7));
       }
+      if (kb > 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // last block's V reads are done
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<uint4*>(lds + (8 * i + (lane >> 3)) * 192 + 16 * (lane & 7)) = vt[i];
       f32x16 sacc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
@@ -237,9 +241,6 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
           o[1][r] *= a;
         }
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<uint4*>(lds + (8 * i + (lane >> 3)) * 192 + 16 * (lane & 7)) = vt[i];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's V tile is in LDS
       // O += P V: A = P from the accumulator (k-step s: registers 8s..8s+7,
       // element j <-> key 16s + 8(j>>2) + 4lh + (j&3)); B = V read transposed,
@@ -293,6 +294,25 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
       op[32] = (T)(o[1][r] * inv);
     }
   }
+}
+
+// f32 (config 2) keeps the compiler's register budget.  bf16: one wave per
+// (query block, head) is a single dependent load -> MFMA -> softmax -> store
+// chain for the short titles, so occupancy hides the latency; the V tile goes
+// to LDS right after its load (its registers die before the S MFMA) and the
+// kernel is held to 128 VGPRs = 4 waves per SIMD with no spill (3 at the
+// compiler's choice of 146): 0.84x the time at 1 M tokens of length 20 / 66 /
+// 200, bit-identical (tools/attn_ab.py, profiles/round3/s6/attn_ab_occupancy.jsonl).
+__global__ __launch_bounds__(256) void attention_kernel_f32(const float* __restrict__ qkv,
+                                                            const int32_t* __restrict__ cu,
+                                                            const int32_t* __restrict__ qoff, int32_t n_seq,
+                                                            float* __restrict__ ctx) {
+  attention_body<float>(qkv, cu, qoff, n_seq, ctx);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void attention_kernel_bf16(
+    const __bf16* __restrict__ qkv, const int32_t* __restrict__ cu, const int32_t* __restrict__ qoff, int32_t n_seq,
+    __bf16* __restrict__ ctx) {
+  attention_body<__bf16>(qkv, cu, qoff, n_seq, ctx);
 }
 
 // ------------------------------------------------------------ whole forward
@@ -527,10 +547,10 @@ extern "C" int nr_attention_varlen(int dtype, int32_t n_seq, int64_t n_qblocks, 
   const dim3 grid((unsigned)(4 * n_qblocks));
   hipStream_t s = (hipStream_t)stream;
   if (dtype == NR_F32)
-    hipLaunchKernelGGL(nr::attention_kernel<float>, grid, dim3(256), 0, s, (const float*)qkv, cu_seqlens,
+    hipLaunchKernelGGL(nr::attention_kernel_f32, grid, dim3(256), 0, s, (const float*)qkv, cu_seqlens,
                        qblock_off, n_seq, (float*)ctx);
   else
-    hipLaunchKernelGGL(nr::attention_kernel<__bf16>, grid, dim3(256), 0, s, (const __bf16*)qkv, cu_seqlens,
+    hipLaunchKernelGGL(nr::attention_kernel_bf16, grid, dim3(256), 0, s, (const __bf16*)qkv, cu_seqlens,
                        qblock_off, n_seq, (__bf16*)ctx);
   NR_CHECK_LAUNCH("nr_attention_varlen");
   return NR_OK;
