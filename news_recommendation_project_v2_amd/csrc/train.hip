@@ -91,6 +91,43 @@ __global__ __launch_bounds__(256) void transpose16_kernel(int64_t rows, int64_t 
   }
 }
 
+// f32 -> bf16 transpose of a 64x64 tile with 16-B global accesses both ways
+// (the generic kernel above stores 2 B per lane): 16 lanes load one source
+// row as float4s into a 64x65 f32 LDS tile (rr + 4ch distinct mod 64: no bank
+// conflict), then each lane converts 8 consecutive source rows of one column
+// (8rc + oc distinct mod 64) and writes them as one 16-B store.  Same (__bf16)
+// rounding as the generic kernel, so the result is bit-identical.  Needs rows,
+// ldd multiples of 8, cols, lds multiples of 4 and 16-B aligned bases.
+__global__ __launch_bounds__(256) void transpose_f32_bf16_kernel(int64_t rows, int64_t cols,
+                                                                 const float* __restrict__ src, int64_t lds,
+                                                                 __bf16* __restrict__ dst, int64_t ldd) {
+  __shared__ float tile[64][65];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int rr = (t >> 4) + 16 * k, ch = t & 15;
+    const int64_t r = r0 + rr, c = c0 + 4 * ch;
+    float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < rows && c < cols) u = *reinterpret_cast<const float4*>(src + r * lds + c);
+    tile[rr][4 * ch] = u.x; tile[rr][4 * ch + 1] = u.y; tile[rr][4 * ch + 2] = u.z; tile[rr][4 * ch + 3] = u.w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int oc = (t >> 3) + 32 * k, rc = t & 7;
+    const int64_t c = c0 + oc, r = r0 + 8 * rc;
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t lo = __builtin_bit_cast(uint16_t, (__bf16)tile[8 * rc + 2 * j][oc]);
+      const uint32_t hi = __builtin_bit_cast(uint16_t, (__bf16)tile[8 * rc + 2 * j + 1][oc]);
+      w[j] = lo | (hi << 16);
+    }
+    if (c < cols && r < rows) *reinterpret_cast<uint4*>(dst + c * ldd + r) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 // ----------------------------------------------------------------- pooling fwd
 // FinalAttention pooling (modeling_utils.py:224-228) over consecutive slot rows:
 // xp row = [x | p] (p = exp(w)); u_d = sum x p / (sum p + 1e-10), z_d = sum p + 1e-10.
@@ -635,6 +672,13 @@ extern "C" int nr_transpose(int dtype_in, int dtype_out, int64_t rows, int64_t c
       ((uintptr_t)dst & 15) == 0) {
     hipLaunchKernelGGL(transpose16_kernel, grid, dim3(256), 0, (hipStream_t)stream, rows, cols,
                        (const uint16_t*)src, lds, (uint16_t*)dst, ldd);
+    NR_CHECK_LAUNCH("nr_transpose");
+    return NR_OK;
+  }
+  if (dtype_in == NR_F32 && dtype_out == NR_BF16 && rows % 8 == 0 && cols % 4 == 0 && lds % 4 == 0 &&
+      ldd % 8 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0) {
+    hipLaunchKernelGGL(transpose_f32_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream, rows, cols,
+                       (const float*)src, lds, (__bf16*)dst, ldd);
     NR_CHECK_LAUNCH("nr_transpose");
     return NR_OK;
   }

@@ -251,6 +251,19 @@ def test_gpu_train_step_bf16_close_to_f32(gpu_device, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(8320, 1024), (64, 4096), (72, 36), (8, 4), (1000, 200)])
+def test_gpu_transpose_f32_to_bf16(gpu_device, shape):
+    """f32 -> bf16 transposes (the latent backward's weight-grad operands): the
+    16-B-store kernel (rows % 8 == 0, cols % 4 == 0) and the generic one agree
+    with torch's own rounding bit for bit, full and partial 64x64 tiles."""
+    from news_recommendation_project_v2_amd import ops
+    x = torch.randn(*shape, device=gpu_device) * 3
+    tb = ops.transpose(x, out_dtype=torch.bfloat16)
+    assert tb.shape == (shape[1], shape[0])
+    assert torch.equal(tb, x.T.to(torch.bfloat16))
+
+
+@pytest.mark.gpu
 def test_gpu_train_kernels(gpu_device):
     from news_recommendation_project_v2_amd import ops
     x = torch.randn(300, 200, device=gpu_device)
