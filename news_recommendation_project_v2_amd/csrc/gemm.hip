@@ -1948,9 +1948,26 @@ static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* 
   eg.group_m = kGemmGroupM;
   // persistent kernel for bf16 -> bf16 (DRELU, a training-only epilogue that needs its
   // forward output at the END of the tile, stays on the one-tile-per-workgroup kernel)
-  if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2)
+  if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) {
     if (epi != NR_EPI_DRELU && persistent_ok(M, N, K, lda, ldw))
       return launch_gemm256_t(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
+    // A past the 32-bit buffer range (e.g. the title encoder's FFN2, [M x 4096]
+    // at M > 512 k tokens): persistent launches over row chunks of < 4 GiB of A.
+    // A row's K chain and epilogue do not depend on its chunk, so the result is
+    // the one-launch result; RELU_DROPOUT's mask hashes the global row index and
+    // stays on the tile kernel.
+    const int64_t mc = 0xFFFFFFFFll / (2 * lda) / 256 * 256;
+    if (epi != NR_EPI_DRELU && epi != NR_EPI_RELU_DROPOUT && mc >= 256 && persistent_ok(mc, N, K, lda, ldw)) {
+      for (int64_t m0 = 0; m0 < M; m0 += mc) {
+        const int64_t m = M - m0 < mc ? M - m0 : mc;
+        const int rc = launch_gemm256_t(epi, m, N, K, static_cast<const char*>(A) + 2 * m0 * lda, lda, W, ldw, bias,
+                                        R ? static_cast<const char*>(R) + 2 * m0 * ldr : nullptr, ldr,
+                                        static_cast<char*>(C) + 2 * m0 * ldc, ldc, eg, s);
+        if (rc != NR_OK) return rc;
+      }
+      return NR_OK;
+    }
+  }
   if constexpr (sizeof(TI) == 2) return launch_gemm256_p16<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
   return launch_gemm256_p<TI, TO>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
 }
