@@ -59,7 +59,7 @@ import torch.distributed as dist
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
-from news_recommendation_project_v2_amd import synthetic  # noqa: E402
+from news_recommendation_project_v2_amd import _lib, synthetic  # noqa: E402
 from news_recommendation_project_v2_amd import weights as W  # noqa: E402
 from news_recommendation_project_v2_amd.distributed import ShardedTable, partition_by_cost, sharded_step  # noqa: E402
 
@@ -287,7 +287,7 @@ def config2_leg(dev, n_news: int = 8192) -> dict:
                           "news_per_s": round(n_news / dt, 1),
                           "tflops": round(tok * 603_979_776 / dt / 1e12, 1)}
     del enc
-    torch.cuda.empty_cache()
+    _lib.empty_cache()
     n_news_s, n_imp_s = synthetic.SHAPES["mind_small_dev"]
     im = synthetic.mind_impressions(n_news_s, n_imp_s, seed=1234)
     r = Run("final", "fp32", im, news_table(n_news_s, dev), dev, 0, 1)
@@ -295,7 +295,7 @@ def config2_leg(dev, n_news: int = 8192) -> dict:
     out["eval_f32_final"] = {"impressions": im.n_imp, "candidates": im.n_cand, "ms_per_step": round(d * 1e3, 3),
                              "value": round(im.n_cand / d, 1)}
     del r
-    torch.cuda.empty_cache()
+    _lib.empty_cache()
     return out
 
 
@@ -343,7 +343,7 @@ def hipblaslt_yardstick(pooler: str, n: int, ours_ms: float, dev, reps: int = 5)
         per.append(round(ms, 4))
         tot += ms
         del a, w
-    torch.cuda.empty_cache()
+    _lib.empty_cache()
     fl = tx_flops(n, pooler)
     return {"shapes_NK": shapes, "hipblaslt_ms_each": per, "hipblaslt_sum_ms": round(tot, 4),
             "hipblaslt_peak_frac": round(fl / (tot * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS["bf16"], 3),
@@ -374,7 +374,7 @@ def encoder_bf16_leg(dev, n_news: int = 16384) -> dict:
     sq = float((np.asarray(p_lens, dtype=np.float64) ** 2).sum() + (np.asarray(q_lens, dtype=np.float64) ** 2).sum())
     flops = tok * 603_979_776 + 24 * 4 * 1024 * sq
     del enc
-    torch.cuda.empty_cache()
+    _lib.empty_cache()
     return {"news": n_news, "tokens": tok, "seconds": round(dt, 3), "tokens_per_s": round(tok / dt, 1),
             "news_per_s": round(n_news / dt, 1), "tflops": round(flops / dt / 1e12, 1),
             "peak_frac": round(flops / dt / 2.5e15, 3)}
@@ -515,7 +515,7 @@ def auc_gate_full(dev, poolers=("latent", "final"), dtype: str = "bf16") -> dict
         log(f"[bench] AUC gate {pooler}: cpu f32 {auc_ref:.7f} gpu {dtype} {g['auc']:.7f} |d| {diff:.2e} "
             f"(CPU reference {t_cpu:.1f}s)")
         del eng, s, ref
-        torch.cuda.empty_cache()
+        _lib.empty_cache()
     return {"impressions": imps.n_imp, "candidates": imps.n_cand, "by_pooler": out,
             "auc_equal_4dp": all(v["auc_equal_4dp"] for v in out.values()),
             "criterion": f"|AUC_gpu - AUC_cpu_ref| < {AUC_4DP}"}
@@ -685,7 +685,7 @@ def main():
                                          "value": round(total_cand / d, 1),
                                          "table_bit_identical": bool(same.item())}
         del r, ref_table
-        torch.cuda.empty_cache()
+        _lib.empty_cache()
         # the other scaling mode as an extra
         if args.scaling == "strong":  # every rank its own full MIND-large-dev-sized set
             other = synthetic.mind_impressions(n_news, n_imp, seed=1234 + rank)
@@ -702,7 +702,7 @@ def main():
         extra[key] = {"value": round(int(c.item()) / d, 1), "ms_per_step": round(d * 1e3, 3),
                       "impressions_per_gpu_rank0": other.n_imp}
         del r, other
-        torch.cuda.empty_cache()
+        _lib.empty_cache()
 
     if world == 1 and not args.no_extra:
         for pooler, dtype in [(args.pooler, "fp32" if args.dtype == "bf16" else "bf16"),
@@ -720,7 +720,7 @@ def main():
                 extra["auc"] = {args.dtype: auc_of(head), dtype: auc_of(r)}
                 extra["auc"]["abs_diff"] = abs(extra["auc"][args.dtype] - extra["auc"][dtype])
             del r
-            torch.cuda.empty_cache()
+            _lib.empty_cache()
         # throughput on the MIND-large *test* shape and cache sensitivity under Zipf(1.1) id popularity
         for tag, shape, zipf in [("mind_large_test", "mind_large_test", None), ("zipf1.1", args.shape, 1.1)]:
             nn_, ni_ = synthetic.SHAPES[shape]
@@ -734,7 +734,7 @@ def main():
                           "pool_score_ms": round(st[2], 3),
                           "pool_score_GBs": round(ps_bytes(im, args.pooler, es) / (st[2] * 1e-3) / 1e9, 1)}
             del r, tb, im
-            torch.cuda.empty_cache()
+            _lib.empty_cache()
         # MIND's user structure: ~256 k users' histories repeated over 376 k impressions
         # (synthetic.MIND_LARGE_DEV_USERS, an assumption); the engine then pools each
         # distinct history once (automatic at >= 15 % repeats), the fused pass beside it
@@ -748,7 +748,7 @@ def main():
             sh["repeated_history_share"] = round(r.eng.shared_history_share, 4) if mode is None else \
                 sh.get("repeated_history_share")
             del r
-            torch.cuda.empty_cache()
+            _lib.empty_cache()
         extra["shared_histories"] = sh
         del im
         extra["metrics_ms"] = round(metrics_ms(head), 3)

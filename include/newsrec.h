@@ -94,18 +94,18 @@ int nr_set_persistent_workgroups(int n);
  * restore what it found. */
 int nr_persistent_workgroups(void);
 
-/* Split-K tail of the bf16 per-news transforms (default OFF): the rows past the
- * last full round of 256x256 tiles of a K >= 4096 GEMM run as K-slices that
- * fill the CUs (f32 partials) + a fixup applying the same epilogue, instead of
- * a partly filled last round.  Results agree with on = 0 to bf16 rounding, but
- * which rows are split depends on M, so with it on a row's output depends on
- * how the table was cut (chunks, ranks); off, every row is computed the same
- * way for any M (the sharded transform is bit-identical to one launch).
- * Process-wide; for A/B measurements and tests. */
-int nr_set_split_tail(int on);
-
 /* Thread-local message of the last failed call ("" if none). */
 const char* nr_last_error(void);
+
+/* Residency checks.  Every entry point verifies that the pointers it hands to
+ * a kernel are device (or managed) memory and fails with NR_ERR_INVALID naming
+ * the argument otherwise.  Verified allocations are remembered per thread as
+ * address ranges; nr_residency_flush() drops every thread's ranges (call it
+ * after freeing device memory back to the driver, e.g. after
+ * torch.cuda.empty_cache(), so a reused address is verified again).
+ * nr_is_device_pointer(p) = 1 when p passes the same check, else 0. */
+int nr_residency_flush(void);
+int nr_is_device_pointer(const void* p);
 
 /*
  * C[M, N] = epilogue(A[M, K] · W[N, K]ᵀ).

@@ -75,9 +75,10 @@ SIGNATURES = {
     "nr_build_hash": (ctypes.c_char_p, []),
     "nr_init": (_i, [_i]),
     "nr_last_error": (ctypes.c_char_p, []),
+    "nr_residency_flush": (_i, []),
+    "nr_is_device_pointer": (_i, [_p]),
     "nr_set_persistent_workgroups": (_i, [_i]),
     "nr_persistent_workgroups": (_i, []),
-    "nr_set_split_tail": (_i, [_i]),
     "nr_gemm": (_i, [_i, _i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p]),
     "nr_gemm_relu_dropout": (_i, [_i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, ctypes.c_uint64, _f, _p]),
     "nr_gemm_drelu": (_i, [_i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _l, _p, _l, _f, _p]),
@@ -164,3 +165,13 @@ def check(rc: int, name: str) -> None:
 
 def call(name: str, *args) -> None:
     check(getattr(load(), name)(*args), name)
+
+
+def empty_cache() -> None:
+    """torch.cuda.empty_cache() + nr_residency_flush(): the segments torch
+    returns to the driver may be re-mapped later, so the library's cached
+    "verified device range" tables are dropped with them (include/newsrec.h)."""
+    import torch
+    torch.cuda.empty_cache()
+    if _LIB is not None:
+        _LIB.nr_residency_flush()

@@ -146,6 +146,8 @@ class AttentionAttentionComponent(PipelineComponent):
                  rng=None, pooler: str = "final", **trainer_kw):
         self.db_name = db_name
         self.token_attention = get_token_attn_model(token_attention_model_path)
+        if pooler not in ("final", "latent"):
+            raise ValueError(f"AttentionAttentionComponent: pooler must be 'final' or 'latent', got {pooler!r}")
         # pooler="latent": BASELINE configs[4]'s pairing (token encoder + LatentAttentionModel)
         self.final_attention = (get_latent_attention_model(final_attention_model_path) if pooler == "latent" else
                                 get_final_attention_model(final_attention_model_path))

@@ -2,6 +2,7 @@
 // which chain the GEMM / row kernels over row chunks with a caller workspace.
 #include "nr_common.h"
 
+#include <atomic>
 #include <mutex>
 #include <string.h>
 
@@ -23,7 +24,10 @@ void clear_error() { g_err[0] = 0; }
 // failing the call.  hipPointerGetAttributes costs ~µs, so
 // verified allocations are remembered as [base, base + size) ranges in a small
 // per-thread table (torch's caching allocator hands out sub-ranges of a few
-// large segments, so the table hits on almost every call).
+// large segments, so the table hits on almost every call).  A freed range may
+// later hold other memory, so the tables are dropped whenever the process-wide
+// generation moves (nr_residency_flush, called by the Python side after it
+// returns cached segments to the driver).
 namespace {
 struct Range {
   uintptr_t lo, hi;
@@ -31,10 +35,20 @@ struct Range {
 constexpr int kRanges = 64;
 thread_local Range t_ranges[kRanges];
 thread_local int t_next = 0;
+thread_local uint64_t t_gen = 0;
+std::atomic<uint64_t> g_res_gen{0};
 }  // namespace
+
+void residency_flush() { g_res_gen.fetch_add(1, std::memory_order_release); }
 
 bool device_accessible(const void* p) {
   const uintptr_t a = (uintptr_t)p;
+  const uint64_t gen = g_res_gen.load(std::memory_order_acquire);
+  if (gen != t_gen) {
+    for (int i = 0; i < kRanges; ++i) t_ranges[i] = Range{0, 0};
+    t_next = 0;
+    t_gen = gen;
+  }
   for (int i = 0; i < kRanges; ++i)
     if (a >= t_ranges[i].lo && a < t_ranges[i].hi) return true;
   hipPointerAttribute_t at;
@@ -100,6 +114,13 @@ extern "C" const char* nr_build_hash(void) { return kBuildTag + 14; }
 
 extern "C" const char* nr_last_error(void) { return nr::g_err; }
 
+extern "C" int nr_residency_flush(void) {
+  nr::residency_flush();
+  return NR_OK;
+}
+
+extern "C" int nr_is_device_pointer(const void* p) { return p && nr::device_accessible(p) ? 1 : 0; }
+
 extern "C" int nr_init(int device) {
   nr::clear_error();
   hipError_t e = hipSetDevice(device);
@@ -147,17 +168,6 @@ extern "C" int nr_final_attn_transform(int dtype, int64_t n, const void* emb, in
     int rc;
     if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RELU, m, H, D, e, emb_ld, W1, D, b1, nullptr, 0, w0, H, s))) return rc;
     if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RELU, m, H, H, w0, H, W2, H, b2, nullptr, 0, w1, H, s))) return rc;
-    if (dtype == NR_BF16) {
-      // N = 1024 GEMMs: their last partial round of tiles runs as K-slices (w0 / w1 are free then)
-      if ((rc = nr::gemm_split_tail_dispatch(NR_EPI_NONE, false, m, D, H, w1, H, W3, H, b3, nullptr, nullptr, nullptr, 0,
-                                             x, 2 * D, w0, m * H * es, s)))
-        return rc;
-      if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RELU, m, H, D, x, 2 * D, W4, D, b4, nullptr, 0, w0, H, s))) return rc;
-      if ((rc = nr::gemm_split_tail_dispatch(NR_EPI_EXP, false, m, D, H, w0, H, W5, H, nullptr, nullptr, nullptr, nullptr,
-                                             0, p, 2 * D, w1, m * H * es, s)))
-        return rc;
-      continue;
-    }
     if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_NONE, m, D, H, w1, H, W3, H, b3, nullptr, 0, x, 2 * D, s))) return rc;
     if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RELU, m, H, D, x, 2 * D, W4, D, b4, nullptr, 0, w0, H, s))) return rc;
     if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_EXP, m, D, H, w0, H, W5, H, nullptr, nullptr, 0, p, 2 * D, s))) return rc;
@@ -239,31 +249,22 @@ extern "C" int nr_latent_transform_lnfold(int dtype, int64_t n, const void* emb,
   const int64_t D = 1024, S = 512, F = 4096;
   const int64_t mc = n < nr::kChunk ? n : nr::kChunk;
   hipStream_t st = (hipStream_t)stream;
-  // workspace: [stats_q | stats_f] in the unfused path's LN-output region; the
-  // rest of it and the unfused path's f32 score region: scratch of the split tails
+  // workspace: [stats_q | stats_f] in the unfused path's LN-output region
   float* sq = (float*)ws;
   float* sf = sq + 2 * mc;
   char* wp = (char*)ws + mc * (D * es + S * 4);
   char* wf = wp + mc * S * es;
-  char* scratch = (char*)ws + ((mc * 16 + 255) / 256) * 256;
-  const int64_t scratch_bytes = wp - scratch;
   for (int64_t r0 = 0; r0 < n; r0 += nr::kChunk) {
     const int64_t m = (n - r0) < nr::kChunk ? (n - r0) : nr::kChunk;
     const char* e = (const char*)emb + r0 * emb_ld * es;
     char* h = (char*)table + r0 * D * es;
     int rc;
     if ((rc = nr::row_stats_dispatch(dtype, m, D, e, emb_ld, 1e-5f, sq, st))) return rc;
-    if ((rc = nr::gemm_split_tail_dispatch(NR_EPI_SOFTMAX64, true, m, S, D, e, emb_ld, Aq, D, nullptr, sq, ucq, nullptr,
-                                           0, wp, S, scratch, scratch_bytes, st)))
-      return rc;
+    if ((rc = nr::gemm_lnfold_dispatch(NR_EPI_SOFTMAX64, m, S, D, e, emb_ld, Aq, D, sq, ucq, wp, S, st))) return rc;
     if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RESADD, m, D, S, wp, S, Bt, S, nullptr, e, emb_ld, h, D, st))) return rc;
     if ((rc = nr::row_stats_dispatch(dtype, m, D, h, D, 1e-5f, sf, st))) return rc;
-    if ((rc = nr::gemm_split_tail_dispatch(NR_EPI_GEGLU, true, m, 2 * F, D, h, D, W1f, D, nullptr, sf, ucf, nullptr, 0,
-                                           wf, F, scratch, scratch_bytes, st)))
-      return rc;
-    if ((rc = nr::gemm_split_tail_dispatch(NR_EPI_RESADD, false, m, D, F, wf, F, W2, F, b2, nullptr, nullptr, h, D, h,
-                                           D, scratch, scratch_bytes, st)))
-      return rc;
+    if ((rc = nr::gemm_lnfold_dispatch(NR_EPI_GEGLU, m, 2 * F, D, h, D, W1f, D, sf, ucf, wf, F, st))) return rc;
+    if ((rc = nr::gemm_dispatch(dtype, dtype, NR_EPI_RESADD, m, D, F, wf, F, W2, F, b2, h, D, h, D, st))) return rc;
   }
   return NR_OK;
 }

@@ -766,27 +766,6 @@ __device__ __forceinline__ uint4 swap_pair16(uint2 a, uint2 b) {
   return uint4{sx[0], sy[0], sx[1], sy[1]};
 }
 
-// The 32x32 counterpart (guide T21): a swapped-operand 32x32 accumulator
-// leaves lane l with row l & 31, columns 8 g + 4 (l >> 5) .. +3 of group g;
-// for groups (2p, 2p + 1) packed as (a, b), one v_permlane32_swap per dword
-// gives lanes 0-31 columns 16 p .. +7 ([own a | upper's a]) and lanes 32-63
-// columns 16 p + 8 .. +15 ([lower's b | own b]).  Applied to a 16-B row segment
-// (a = its first 8 bytes, b = the last 8) it maps back to (group 2p, 2p + 1).
-__device__ __forceinline__ uint4 swap_pair32(uint2 a, uint2 b) {
-  const auto sx = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
-  const auto sy = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
-  return uint4{sx[0], sy[0], sx[1], sy[1]};
-}
-
-template <bool MF32>
-struct AccT {  // a wave's 128x64 accumulators: 8x4 tiles of 16x16, or 4x2 tiles of 32x32
-  typedef f32x4 type[8][4];
-};
-template <>
-struct AccT<true> {
-  typedef f32x16 type[4][2];
-};
-
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
@@ -810,7 +789,7 @@ constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78, kVmcnt6 = 0x0F76, kVmcnt9
 // its first K step while tile t's epilogue still reads slot t.
 constexpr int kLnSlot = 8 * 512 + 256 * 8;
 
-template <int EPI, bool LNF = false, bool MF32 = false>
+template <int EPI, bool LNF = false>
 __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, int64_t K,
                                                           const __bf16* __restrict__ A, int64_t lda,
                                                           const __bf16* __restrict__ W, int64_t ldw,
@@ -929,66 +908,35 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   const int bbase = G2BM * 128 + (wn * 64 + c16) * 128;
   const int cf0 = ((0 + q4) ^ sw) << 4, cf1 = ((4 + q4) ^ sw) << 4;
   typedef f32x4 frag_t;
-  // MF32 (v_mfma_f32_32x32x16_bf16): operand map row lane & 31, 16-B k chunk
-  // 2 s + lane / 32 of the 16-deep k slice s; a quadrant is 2 row tiles x 1 col tile
-  const int r32 = lane & 31, h32 = lane >> 5;
-  const int sw32 = (r32 >> 1) & 7;
-  const int abase32 = (wm * 128 + r32) * 128, bbase32 = G2BM * 128 + (wn * 64 + r32) * 128;
-  frag_t fa[4][2], fb0[2][2], fb1[2][2];  // 16x16x32: [row tile][k half]; 32x32x16: fa[i][s] = [2 x 4], fb[s >> 1][s & 1]
-  typename AccT<MF32>::type acc;
+  frag_t fa[4][2], fb0[2][2], fb1[2][2];  // [row tile][k half]
+  f32x4 acc[8][4];
   auto readA = [&](int stage, int qm) {
-    if constexpr (MF32) {
-      const unsigned char* sp = smem + stage * G2_STAGE + abase32 + qm * 64 * 128;
+    const unsigned char* sp = smem + stage * G2_STAGE + abase + qm * 4 * 2048;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-          fa[2 * i + (s4 >> 1)][s4 & 1] =
-              *reinterpret_cast<const frag_t*>(sp + i * 32 * 128 + (((2 * s4 + h32) ^ sw32) << 4));
-    } else {
-      const unsigned char* sp = smem + stage * G2_STAGE + abase + qm * 4 * 2048;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        fa[i][0] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf0);
-        fa[i][1] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf1);
-      }
+    for (int i = 0; i < 4; ++i) {
+      fa[i][0] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf0);
+      fa[i][1] = *reinterpret_cast<const frag_t*>(sp + i * 2048 + cf1);
     }
   };
   auto readB = [&](int stage, int qn, frag_t (&fb)[2][2]) {
-    if constexpr (MF32) {
-      const unsigned char* sp = smem + stage * G2_STAGE + bbase32 + qn * 32 * 128;
+    const unsigned char* sp = smem + stage * G2_STAGE + bbase + qn * 2 * 2048;
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) fb[s4 >> 1][s4 & 1] = *reinterpret_cast<const frag_t*>(sp + (((2 * s4 + h32) ^ sw32) << 4));
-    } else {
-      const unsigned char* sp = smem + stage * G2_STAGE + bbase + qn * 2 * 2048;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        fb[j][0] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf0);
-        fb[j][1] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf1);
-      }
+    for (int j = 0; j < 2; ++j) {
+      fb[j][0] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf0);
+      fb[j][1] = *reinterpret_cast<const frag_t*>(sp + j * 2048 + cf1);
     }
   };
   // swapped operands: D[n][m] = sum_k W[n][k] A[m][k] = C[m][n]
   auto mma = [&](int qm, int qn, const frag_t (&fb)[2][2]) {
-    if constexpr (MF32) {
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
+    for (int f = 0; f < 2; ++f)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc[2 * qm + i][qn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              __builtin_bit_cast(bf16x8, fb[s4 >> 1][s4 & 1]), __builtin_bit_cast(bf16x8, fa[2 * i + (s4 >> 1)][s4 & 1]),
-              acc[2 * qm + i][qn], 0, 0, 0);
-    } else {
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int f = 0; f < 2; ++f)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[4 * qm + i][2 * qn + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8, fb[j][f]), __builtin_bit_cast(bf16x8, fa[i][f]), acc[4 * qm + i][2 * qn + j],
-                0, 0, 0);
-    }
+        for (int j = 0; j < 2; ++j)
+          acc[4 * qm + i][2 * qn + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, fb[j][f]), __builtin_bit_cast(bf16x8, fa[i][f]), acc[4 * qm + i][2 * qn + j],
+              0, 0, 0);
   };
 #define NR_PHASE_SYNC_MMA(QM, NI, FB)                   \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
@@ -1076,32 +1024,14 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     if (more) tile_base(tn, nm0, nn0);
     // the accumulators start at the bias (acc = bias + A.W^T); this wave's
     // columns wn*64 + 16 ni + 4 q4 .. +3
-    if constexpr (MF32) {
-      // lane's columns of tile ni: 32 ni + 8 g + 4 h32 + (reg & 3), g = reg >> 2
-      f32x16 b16[2];
+    f32x4 b4[4];
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
+    for (int ni = 0; ni < 4; ++ni)
+      b4[ni] = bias ? *reinterpret_cast<const f32x4*>(bias_lds + (16 * ni + 4 * q4) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 b4 = bias ? *reinterpret_cast<const f32x4*>(bias_lds + (32 * ni + 8 * g + 4 * h32) * 4)
-                                : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) b16[ni][4 * g + r] = b4[r];
-        }
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = b16[ni];
-    } else {
-      f32x4 b4[4];
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        b4[ni] = bias ? *reinterpret_cast<const f32x4*>(bias_lds + (16 * ni + 4 * q4) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = b4[ni];
-    }
+      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = b4[ni];
     for (int kt = 0; kt < nk; ++kt) {
       kstep(kt, st, more, nm0, nn0);
       st ^= 1;
@@ -1115,142 +1045,6 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     // not store: with an in-place residual (R == C, the latent ff2) another
     // wave group's duplicate store of row M - 1 could land before this
     // group's residual load of it and add the residual twice.
-    if constexpr (MF32) {
-    // 32x32 accumulators: lane l holds row r32 of row tile mi, columns
-    // 32 ni + 8 g + 4 h32 + r (g = reg >> 2, r = reg & 3); after swap_pair32 of
-    // groups (2p, 2p + 1) the lane stores columns 32 ni + 16 p + 8 h32 .. +7
-    const int64_t row0 = (int64_t)m0 + wm * 128 + r32;  // + 32 mi
-    const int64_t col0 = (int64_t)n0 + wn * 64;
-    const int so = 8 * h32;  // lane's 8 store columns within a 16-column pair
-    f32x16 lu[2], lc[2];
-    const unsigned char* ln_st = ln_lds + lslot * kLnSlot + 8 * 512;
-    if constexpr (LNF) {
-      const unsigned char* uc = ln_lds + lslot * kLnSlot + wave * 512;
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 u4 = *reinterpret_cast<const f32x4*>(uc + (32 * ni + 8 * g + 4 * h32) * 4);
-          const f32x4 c4 = *reinterpret_cast<const f32x4*>(uc + 256 + (32 * ni + 8 * g + 4 * h32) * 4);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            lu[ni][4 * g + r] = u4[r];
-            lc[ni][4 * g + r] = c4[r];
-          }
-        }
-    }
-    uint4 rq[4][2][2];
-    if constexpr (EPI == NR_EPI_RESADD) {
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        const int64_t row = min(row0 + 32 * mi, M - 1);
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-          for (int pp = 0; pp < 2; ++pp)
-            rq[mi][ni][pp] = *reinterpret_cast<const uint4*>(R + row * ldr + col0 + 32 * ni + 16 * pp + so);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int64_t row = min(row0 + 32 * mi, M - 1);
-      const bool live = row0 + 32 * mi < M;
-      if constexpr (LNF) {
-        const float2 ms = *reinterpret_cast<const float2*>(ln_st + (wm * 128 + r32 + 32 * mi) * 8);
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[mi][ni][r] = fmaf(ms.y, fmaf(-ms.x, lu[ni][r], acc[mi][ni][r]), lc[ni][r]);
-      }
-      if constexpr (EPI == NR_EPI_GEGLU) {
-        // W rows interleaved in 32-row (a, g) blocks: tile 0 = a, tile 1 = g
-        uint2 pk[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float o[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = acc[mi][0][4 * g + r] * gelu_erf(acc[mi][1][4 * g + r]);
-          pk[g] = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
-        }
-#pragma unroll
-        for (int pp = 0; pp < 2; ++pp) {
-          const uint4 v = swap_pair32(pk[2 * pp], pk[2 * pp + 1]);
-          if (live) *reinterpret_cast<uint4*>(C + row * ldc + col0 / 2 + 16 * pp + so) = v;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      } else {
-        if constexpr (EPI == NR_EPI_RESADD) {
-#pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-            for (int pp = 0; pp < 2; ++pp) {
-              const uint4 q = swap_pair32(uint2{rq[mi][ni][pp].x, rq[mi][ni][pp].y}, uint2{rq[mi][ni][pp].z, rq[mi][ni][pp].w});
-              const uint32_t w[2][2] = {{q.x, q.y}, {q.z, q.w}};  // groups 2pp, 2pp + 1
-#pragma unroll
-              for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                  const uint32_t u = w[h][r >> 1];
-                  acc[mi][ni][4 * (2 * pp + h) + r] += (r & 1) ? bf16_hi(u) : bf16_lo(u);
-                }
-            }
-        }
-        float v[2][16];
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float x = acc[mi][ni][r];
-            if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
-              const uint64_t gi = (uint64_t)(row * N + col0 + 32 * ni + 8 * (r >> 2) + 4 * h32 + (r & 3));
-              x = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(x, 0.f) * ea.scale;
-            }
-            if constexpr (EPI == NR_EPI_EXP) x = epi_exp(x);
-            if constexpr (EPI == NR_EPI_GELU) x = gelu_erf(x);
-            v[ni][r] = x;
-          }
-        if constexpr (EPI == NR_EPI_SOFTMAX64) {
-          // the wave's 64 columns are one softmax group: row r32's values sit in lanes l and l ^ 32
-          float mx = v[0][0];
-#pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, v[ni][r]);
-          mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-          float sum = 0.f;
-#pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              v[ni][r] = epi_exp(v[ni][r] - mx);
-              sum += v[ni][r];
-            }
-          sum += __shfl_xor(sum, 32, 64);
-          const float inv = 1.0f / sum;
-#pragma unroll
-          for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[ni][r] *= inv;
-        }
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          uint2 pk[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            pk[g] = uint2{pack_bf16x2(v[ni][4 * g], v[ni][4 * g + 1]), pack_bf16x2(v[ni][4 * g + 2], v[ni][4 * g + 3])};
-            if constexpr (EPI == NR_EPI_RELU) pk[g] = uint2{relu_bf16x2(pk[g].x), relu_bf16x2(pk[g].y)};
-          }
-#pragma unroll
-          for (int pp = 0; pp < 2; ++pp) {
-            const uint4 q = swap_pair32(pk[2 * pp], pk[2 * pp + 1]);
-            if (live) *reinterpret_cast<uint4*>(C + row * ldc + col0 + 32 * ni + 16 * pp + so) = q;
-          }
-        }
-        if constexpr (EPI == NR_EPI_RESADD) __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    } else {
     const int64_t row0 = (int64_t)m0 + wm * 128 + c16;  // + 16 mi
     const int64_t col0 = (int64_t)n0 + wn * 64;          // this wave's 64 columns
     const int qo = 16 * (q4 & 1) + 8 * (q4 >> 1);        // lane's 8 columns after swap_pair16
@@ -1386,7 +1180,6 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
         if constexpr (EPI == NR_EPI_RESADD) __builtin_amdgcn_sched_barrier(0);  // row groups in load order
       }
     }
-    }
     if (!more) break;
     if (wmu == 1) __builtin_amdgcn_s_barrier();  // re-skew
     lslot ^= 1;
@@ -1395,421 +1188,6 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     n0 = nn0;
   }
 #undef NR_PHASE_SYNC_MMA
-}
-
-// ---------------------------------------------------------------------------
-// 4-wave persistent variant: the same 256x256 block tile, LDS stage images,
-// swizzled LDS-DMA and cross-tile operand stream as gemm256t_kernel, but 4
-// waves (one per SIMD) of 128x128 each on v_mfma_f32_32x32x16_bf16 (4 x 4
-// accumulators of 32x32 = 256 accumulator registers, AGPR-resident).  Per K
-// step a wave reads 32 KiB of fragments (the whole workgroup 128 KiB instead of
-// the 8-wave layout's 192 KiB) and issues 64 MFMAs of 32 cycles, whose 24
-// free issue cycles each hold the ds_reads and DMAs of a single wave.  Phases
-// (row tile i of the wave's 128 rows, all four column tiles, K = 64):
-//   P0: read B (16 frags) + A tiles 0, 1; barrier; DMA B of step k+2; MMA tile 0
-//   P1: read A tile 2;                     DMA A rows of tiles 0, 1; MMA tile 1
-//   P2: read A tile 3;                                               MMA tile 2
-//   P3: barrier; DMA A rows of tiles 2, 3; MMA tile 3; vmcnt (step k+1 landed); barrier
-// Stage st is refilled for step k + 2 once every wave has read the region (the
-// barriers in P0 / P3 follow lgkmcnt(0)), and read again only after the vmcnt
-// + barrier that ends step k + 1.
-template <int EPI, bool LNF = false>
-__global__ __launch_bounds__(256, 1) void gemm256w4_kernel(int64_t M, int64_t N, int64_t K,
-                                                           const __bf16* __restrict__ A, int64_t lda,
-                                                           const __bf16* __restrict__ W, int64_t ldw,
-                                                           const float* __restrict__ bias, const __bf16* R,
-                                                           int64_t ldr, __bf16* C, int64_t ldc, EpiArgs ea, int ntn,
-                                                           int ntm, int n_tiles) {
-  constexpr int BK = 64;
-  // stages + 2 bias slots (tile parity; 4 waves x 128 floats) + LNF slots (u, c: 4 x 2 x 512 B; stats 256 x 8 B)
-  constexpr int kLn4 = 4 * 1024 + 256 * 8;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE + 2 * 4 * 512 + (LNF ? 2 * kLn4 : 0)];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nk = (int)(K / BK);  // >= 2 (host)
-
-  const int G = (int)gridDim.x;
-  int t, t_end, t_step;
-  if (G % 8 == 0) {
-    const int x = (int)blockIdx.x & 7, li = (int)blockIdx.x >> 3;
-    const int qq = n_tiles >> 3, rr = n_tiles & 7;
-    const int lo = x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq;
-    t = lo + li;
-    t_end = lo + qq + (x < rr ? 1 : 0);
-    t_step = G >> 3;
-  } else {
-    t = (int)blockIdx.x;
-    t_end = n_tiles;
-    t_step = G;
-  }
-  if (t >= t_end) return;
-  auto tile_base = [&](int tile, uint32_t& mb, uint32_t& nb) {
-    int mt, nt;
-    tile_of(tile, ntn, ntm, ea.group_m, mt, nt);
-    mb = (uint32_t)mt * G2BM;
-    nb = (uint32_t)nt * G2BN;
-  };
-  auto rsrc = [](const void* p, int64_t bytes) {
-    const uint64_t v = (uint64_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    const int n = __builtin_amdgcn_readfirstlane((int)(bytes > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)bytes));
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
-  };
-  const __amdgpu_buffer_rsrc_t rA = rsrc(A, M * lda * 2), rW = rsrc(W, N * ldw * 2);
-  // output / residual through buffer descriptors (host: < 4 GiB each): one 32-bit
-  // offset per row tile, the column steps in the instruction's immediate offset
-  const int64_t ccols = EPI == NR_EPI_GEGLU ? N / 2 : N;
-  const __amdgpu_buffer_rsrc_t rC = rsrc(C, ((M - 1) * ldc + ccols) * 2);
-  const __amdgpu_buffer_rsrc_t rR = rsrc(R, EPI == NR_EPI_RESADD ? ((M - 1) * ldr + N) * 2 : 0);
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  // DMA units.  A unit i = rows 32 i .. +31 of both 128-row halves: wave w owns
-  // rows 128 (w >> 1) + 32 i + 16 (w & 1) + 8 j + l / 8 (j = 0, 1).  B: wave w
-  // owns rows 64 w + 8 j + l / 8 (j = 0..7).  16-B chunk (l & 7) ^ ((row >> 1) & 7).
-  const uint32_t ldab = (uint32_t)lda * 2, ldwb = (uint32_t)ldw * 2, mlast = (uint32_t)(M - 1);
-  auto chunk = [&](int j) { return (uint32_t)(((lane & 7) ^ ((4 * j + (lane >> 4)) & 7)) * 16); };
-  const int qa = (wave >> 1) * 128 + (wave & 1) * 16;
-  // Per-lane DMA offsets: one base per chunk parity, the row steps (8 j, 32 i)
-  // ride in the scalar offset with the K offset (4 VGPRs instead of 16).  B rows
-  // never pass N; A rows past M (last M-tile only) are clamped to M - 1 per lane.
-  uint32_t oA[2], oB[2], amb = 0;
-  bool afull = true;
-  auto set_offA = [&](uint32_t mb) {
-    amb = mb;
-    afull = mb + (uint32_t)G2BM <= (uint32_t)M;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) oA[j] = (mb + (uint32_t)(qa + (lane >> 3))) * ldab + chunk(j);
-  };
-  auto set_offB = [&](uint32_t nb) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) oB[j] = (nb + (uint32_t)(64 * wave + (lane >> 3))) * ldwb + chunk(j);
-  };
-  auto dmaA = [&](int i, int stage, int kt) {
-    unsigned char* sa = smem + stage * G2_STAGE + (qa + 32 * i) * 128;
-    if (afull) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sa + 8 * j * 128), 16, oA[j],
-                                                 kt * (BK * 2) + (32 * i + 8 * j) * ldab, 0, 0);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint32_t o = min(amb + (uint32_t)(qa + 32 * i + 8 * j + (lane >> 3)), mlast) * ldab + chunk(j);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sa + 8 * j * 128), 16, o, kt * (BK * 2), 0, 0);
-      }
-    }
-  };
-  auto dmaB = [&](int stage, int kt) {
-    unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128 + 64 * wave * 128;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(sb + 8 * j * 128), 16, oB[j & 1],
-                                               kt * (BK * 2) + 8 * j * ldwb, 0, 0);
-  };
-  // this wave's 128 bias floats, slot = tile parity (the next tile's bias lands
-  // while this tile's epilogue still reads its own; added in the epilogue, so the
-  // accumulators start at zero)
-  unsigned char* bias_lds = smem + 2 * G2_STAGE + wave * 512;
-  const __amdgpu_buffer_rsrc_t rBias = rsrc(bias, N * 4);
-  auto dma_bias = [&](int slot, uint32_t nb) {
-    if (bias)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rBias, (lds_void*)(bias_lds + slot * 2048 + 256 * h), 4,
-                                                 (nb + (uint32_t)(wn * 128 + 64 * h + lane)) * 4, 0, 0, 0);
-  };
-  unsigned char* ln_lds = smem + 2 * G2_STAGE + 2 * 4 * 512;
-  const __amdgpu_buffer_rsrc_t rUC = rsrc(ea.ln_uc, LNF ? 2 * N * 4 : 0);
-  const __amdgpu_buffer_rsrc_t rST = rsrc(ea.ln_stats, LNF ? M * 8 : 0);
-  auto dma_ln = [&](int slot, uint32_t mb, uint32_t nb) {
-    if constexpr (LNF) {
-      unsigned char* base = ln_lds + slot * kLn4;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t cu = (nb + (uint32_t)(wn * 128 + 64 * h + lane)) * 4;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rUC, (lds_void*)(base + wave * 1024 + 256 * h), 4, cu, 0, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rUC, (lds_void*)(base + wave * 1024 + 512 + 256 * h), 4,
-                                                 cu + (uint32_t)N * 4, 0, 0, 0);
-        const uint32_t row = min(mb + (uint32_t)(64 * wave + 32 * h + (lane >> 1)), mlast);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rST, (lds_void*)(base + 4 * 1024 + wave * 512 + 256 * h), 4,
-                                                 row * 8 + (uint32_t)(lane & 1) * 4, 0, 0, 0);
-      }
-    }
-  };
-  int lslot = 0;
-
-  // 32x32x16 fragments: row lane & 31, 16-B chunk 2 s + lane / 32 of k slice s
-  const int r32 = lane & 31, h32 = lane >> 5;
-  const int sw32 = (r32 >> 1) & 7;
-  int cs[4];
-#pragma unroll
-  for (int s4 = 0; s4 < 4; ++s4) cs[s4] = ((2 * s4 + h32) ^ sw32) << 4;
-  const int abase = (wm * 128 + r32) * 128, bbase = G2BM * 128 + (wn * 128 + r32) * 128;
-  typedef f32x4 frag_t;
-  frag_t fa0[4], fa1[4], fb[4][4];
-  f32x16 acc[4][4];
-  auto readA = [&](int stage, int i, frag_t (&fa)[4]) {
-    const unsigned char* sp = smem + stage * G2_STAGE + abase + i * 32 * 128;
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) fa[s4] = *reinterpret_cast<const frag_t*>(sp + cs[s4]);
-  };
-  // P0's reads in MFMA order (k slice s: B of all four column tiles, then A of
-  // row tile 0), so the first MFMAs wait only for their own fragments
-  auto readP0 = [&](int stage) {
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        fb[j][s4] = *reinterpret_cast<const frag_t*>(smem + stage * G2_STAGE + bbase + j * 32 * 128 + cs[s4]);
-      fa0[s4] = *reinterpret_cast<const frag_t*>(smem + stage * G2_STAGE + abase + cs[s4]);
-    }
-  };
-  auto mma = [&](int i, const frag_t (&fa)[4]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, fb[j][s4]),
-                                                            __builtin_bit_cast(bf16x8, fa[s4]), acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {
-    const bool pf = kt + 2 < nk || more;
-    const bool edge = kt + 2 >= nk;  // this step's DMAs fetch the next tile's step kt + 2 - nk
-    const int kf = edge ? kt + 2 - nk : kt + 2;
-    // P0: fragments of row tile 0 and all of B; MFMAs start as their operands land
-    readP0(st);
-    readA(st, 1, fa1);
-    mma(0, fa0);
-    // P1: every wave has read B and A tiles 0, 1 of this stage -> refill them for step kt + 2
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    if (pf) {
-      if (kt + 2 == nk) {
-        set_offA(nm0);
-        set_offB(nn0);
-        dma_bias(lslot ^ 1, nn0);
-      }
-      dmaB(st, kf);
-      dmaA(0, st, kf);
-      dmaA(1, st, kf);
-    }
-    readA(st, 2, fa0);
-    mma(1, fa1);
-    // P2
-    readA(st, 3, fa1);
-    mma(2, fa0);
-    // P3: A tiles 2, 3 read by every wave -> refill them
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    if (pf) {
-      dmaA(2, st, kf);
-      dmaA(3, st, kf);
-      if (LNF && kt + 2 == nk) dma_ln(lslot ^ 1, nm0, nn0);
-    }
-    mma(3, fa1);
-    // step kt + 1 (issued during step kt - 1, or the prologue) has landed; this step's DMAs may fly
-    if (!pf) {
-      __builtin_amdgcn_s_waitcnt(kVmcnt0);
-    } else if (kt + 2 == nk) {
-      // 16 operand DMAs + the bias (and LN) DMAs of the next tile are this step's
-      if (LNF) {
-        if (bias) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
-      } else {
-        if (bias) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      }
-    } else {
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-  };
-
-  uint32_t m0, n0;
-  tile_base(t, m0, n0);
-  set_offA(m0);
-  set_offB(n0);
-  dma_ln(0, m0, n0);
-  dma_bias(0, n0);
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    dmaB(k, k);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dmaA(i, k, k);
-  }
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // step 0 (+ bias, LN) landed
-  __builtin_amdgcn_s_barrier();
-  int st = 0;
-  while (true) {
-    const int tn = t + t_step;
-    const bool more = tn < t_end;
-    uint32_t nm0 = 0, nn0 = 0;
-    if (more) tile_base(tn, nm0, nn0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    for (int kt = 0; kt < nk; ++kt) {
-      kstep(kt, st, more, nm0, nn0);
-      st ^= 1;
-    }
-    // pin the accumulators to AGPRs at the loop exit: the epilogue then reads
-    // them out one row tile at a time instead of copying all 256 to VGPRs
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[i][j]));
-    // ---------------- epilogue of tile (m0, n0): rows wm*128 + 32 i + r32, cols wn*128 + 32 j
-    // (tile coordinates made opaque here: otherwise the epilogue's addresses are
-    // hoisted into the K loop, where they hold ~100 VGPRs and force spills)
-    uint32_t em0 = m0, en0 = n0;
-    asm volatile("" : "+s"(em0), "+s"(en0));
-    const uint32_t row0 = em0 + (uint32_t)(wm * 128 + r32);
-    const uint32_t col0 = en0 + (uint32_t)(wn * 128);
-    const int so = 8 * h32;
-    const unsigned char* ln_base = ln_lds + lslot * kLn4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t row = min(row0 + (uint32_t)(32 * i), mlast);
-      const bool live = row0 + (uint32_t)(32 * i) < (uint32_t)M;
-      const uint32_t cof = (row * (uint32_t)ldc + (EPI == NR_EPI_GEGLU ? col0 / 2 : col0) + so) * 2;
-      // one row tile at a time (the scheduler would otherwise read all 256
-      // accumulators out up front and spill): a fence between row tiles
-      __builtin_amdgcn_sched_barrier(0);
-      f32x16 v[4];  // this row tile's values (the accumulators are only read)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = acc[i][j];
-      if (bias) {  // tile j's lane columns 32 j + 8 g + 4 h32 + (reg & 3)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias_lds + lslot * 2048 + (32 * j + 8 * g + 4 * h32) * 4);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[j][4 * g + r] += b4[r];
-          }
-      }
-      if constexpr (LNF) {
-        const float2 ms = *reinterpret_cast<const float2*>(ln_base + 4 * 1024 + (wm * 128 + r32 + 32 * i) * 8);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 u4 = *reinterpret_cast<const f32x4*>(ln_base + wave * 1024 + (32 * j + 8 * g + 4 * h32) * 4);
-            const f32x4 c4 = *reinterpret_cast<const f32x4*>(ln_base + wave * 1024 + 512 + (32 * j + 8 * g + 4 * h32) * 4);
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              v[j][4 * g + r] = fmaf(ms.y, fmaf(-ms.x, u4[r], v[j][4 * g + r]), c4[r]);
-          }
-      }
-      if constexpr (EPI == NR_EPI_GEGLU) {
-        // W rows interleaved in 32-row (a, g) blocks: tiles (0, 1) and (2, 3) are (a, g) pairs
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          uint2 pk[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            float o[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = v[2 * hh][4 * g + r] * gelu_erf(v[2 * hh + 1][4 * g + r]);
-            pk[g] = uint2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])};
-          }
-#pragma unroll
-          for (int pp = 0; pp < 2; ++pp) {
-            const uint4 v = swap_pair32(pk[2 * pp], pk[2 * pp + 1]);
-            if (live)
-              __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rC, cof + (32 * hh + 16 * pp) * 2, 0, 0);
-          }
-        }
-      } else {
-        if constexpr (EPI == NR_EPI_RESADD) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int pp = 0; pp < 2; ++pp) {
-              const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(
-                  rR, (row * (uint32_t)ldr + col0 + so) * 2 + (32 * j + 16 * pp) * 2, 0, 0);
-              const uint4 q = swap_pair32(uint2{rv.x, rv.y}, uint2{rv.z, rv.w});
-              const uint32_t w[2][2] = {{q.x, q.y}, {q.z, q.w}};
-#pragma unroll
-              for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                  const uint32_t u = w[h][r >> 1];
-                  v[j][4 * (2 * pp + h) + r] += (r & 1) ? bf16_hi(u) : bf16_lo(u);
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float x = v[j][r];
-            if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
-              const uint64_t gi = (uint64_t)row * N + col0 + 32 * j + 8 * (r >> 2) + 4 * h32 + (r & 3);
-              x = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(x, 0.f) * ea.scale;
-            }
-            if constexpr (EPI == NR_EPI_EXP) x = expf(x);
-            if constexpr (EPI == NR_EPI_GELU) x = gelu_erf(x);
-            v[j][r] = x;
-          }
-        if constexpr (EPI == NR_EPI_SOFTMAX64) {
-          // 64-column softmax groups = tile pairs (0, 1) and (2, 3); a row sits in lanes l and l ^ 32
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            float mx = v[2 * hh][0];
-#pragma unroll
-            for (int j = 2 * hh; j < 2 * hh + 2; ++j)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) mx = fmaxf(mx, v[j][r]);
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-            float sum = 0.f;
-#pragma unroll
-            for (int j = 2 * hh; j < 2 * hh + 2; ++j)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) {
-                v[j][r] = expf(v[j][r] - mx);
-                sum += v[j][r];
-              }
-            sum += __shfl_xor(sum, 32, 64);
-            const float inv = 1.0f / sum;
-#pragma unroll
-            for (int j = 2 * hh; j < 2 * hh + 2; ++j)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) v[j][r] *= inv;
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          uint2 pk[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            pk[g] = uint2{pack_bf16x2(v[j][4 * g], v[j][4 * g + 1]),
-                          pack_bf16x2(v[j][4 * g + 2], v[j][4 * g + 3])};
-            if constexpr (EPI == NR_EPI_RELU) pk[g] = uint2{relu_bf16x2(pk[g].x), relu_bf16x2(pk[g].y)};
-          }
-#pragma unroll
-          for (int pp = 0; pp < 2; ++pp) {
-            const uint4 q = swap_pair32(pk[2 * pp], pk[2 * pp + 1]);
-            if (live)
-              __builtin_amdgcn_raw_buffer_store_b128(u32x4{q.x, q.y, q.z, q.w}, rC, cof + (32 * j + 16 * pp) * 2, 0, 0);
-          }
-        }
-      }
-    }
-    if (!more) break;
-    lslot ^= 1;
-    t = tn;
-    m0 = nm0;
-    n0 = nn0;
-  }
 }
 
 // Workgroups of a persistent GEMM launch: the device's CU count rounded down
@@ -2089,186 +1467,7 @@ int gemm_dispatch_ex(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N,
   return launch_gemm_t<__bf16, __bf16>(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, ea, s);
 }
 
-// ---------------------------------------------------------------------------
-// Split-K tail of the bf16 transform GEMMs.  A persistent launch over M rows
-// runs ceil(tiles / CUs) rounds of 256x256 tiles; when the last round is only
-// partly filled (M = 72,023: ff2 / final.l3 / l5 4.4 rounds, S 2.2, ff1 35.25)
-// its CUs idle for a whole tile time.  Here the rows of the full rounds run as
-// usual and the rows past them run as `s` K-slices in one grouped launch
-// (f32 partials, gemm256p_group_kernel) that fills the CUs, followed by a
-// row-wise fixup that sums the slices and applies the same epilogue (bias,
-// LayerNorm fold, ReLU / exp / GEGLU / softmax64 / residual).  The sum runs
-// in f32 in a different order than one tile's K loop, so results agree with
-// the unsplit launch to bf16 rounding (tests/test_lnfold.py
-// `test_split_tail_matches_unsplit`).
-
-// One thread per 4 output columns; softmax64 groups are 16 consecutive threads.
-template <int EPI, bool LNF>
-__global__ __launch_bounds__(256) void tail_fixup_kernel(int64_t rows, int64_t N, int parts, const float* __restrict__ P,
-                                                         const float* __restrict__ bias,
-                                                         const float* __restrict__ stats,  // [rows] (mean, rstd)
-                                                         const float* __restrict__ uc,     // u [N] | c [N]
-                                                         const __bf16* R, int64_t ldr, __bf16* C, int64_t ldc) {
-  const int64_t ncols = EPI == NR_EPI_GEGLU ? N / 2 : N;
-  const int64_t quads = ncols / 4;
-  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t r = (int64_t)blockIdx.y;
-  if (r >= rows) return;
-  const bool act = q < quads;
-  const int64_t o = act ? 4 * q : 0;  // first output column
-  float2 ms = make_float2(0.f, 1.f);
-  if constexpr (LNF) ms = *reinterpret_cast<const float2*>(stats + 2 * r);
-  auto col_val = [&](int64_t c) {  // the epilogue's pre-activation value of input column c (4 of them)
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int p = 0; p < parts; ++p) acc += *reinterpret_cast<const f32x4*>(P + ((int64_t)p * rows + r) * N + c);
-    if (bias) acc += *reinterpret_cast<const f32x4*>(bias + c);
-    if constexpr (LNF) {
-      const f32x4 u = *reinterpret_cast<const f32x4*>(uc + c), cc = *reinterpret_cast<const f32x4*>(uc + N + c);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) acc[k] = fmaf(ms.y, fmaf(-ms.x, u[k], acc[k]), cc[k]);
-    }
-    return acc;
-  };
-  float v[4];
-  if constexpr (EPI == NR_EPI_GEGLU) {
-    // W rows interleaved in 32-row (a, g) blocks: output column o = 32 b + w -> a = 64 b + w, g = a + 32
-    const int64_t ca = 64 * (o / 32) + (o % 32);
-    const f32x4 a = col_val(ca), g = col_val(ca + 32);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = a[k] * gelu_erf(g[k]);
-  } else {
-    const f32x4 a = col_val(o);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float x = a[k];
-      if constexpr (EPI == NR_EPI_RELU) x = fmaxf(x, 0.f);
-      if constexpr (EPI == NR_EPI_EXP) x = expf(x);
-      if constexpr (EPI == NR_EPI_GELU) x = gelu_erf(x);
-      v[k] = x;
-    }
-    if constexpr (EPI == NR_EPI_SOFTMAX64) {
-      float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-#pragma unroll
-      for (int m = 8; m >= 1; m >>= 1) mx = fmaxf(mx, __shfl_xor(mx, m, 64));
-      float sum = 0.f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        v[k] = expf(v[k] - mx);
-        sum += v[k];
-      }
-#pragma unroll
-      for (int m = 8; m >= 1; m >>= 1) sum += __shfl_xor(sum, m, 64);
-      const float inv = 1.0f / sum;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] *= inv;
-    }
-    if constexpr (EPI == NR_EPI_RESADD) {
-      const uint2 rr = *reinterpret_cast<const uint2*>(R + r * ldr + o);
-      v[0] += bf16_lo(rr.x);
-      v[1] += bf16_hi(rr.x);
-      v[2] += bf16_lo(rr.y);
-      v[3] += bf16_hi(rr.y);
-    }
-  }
-  if (act) *reinterpret_cast<uint2*>(C + r * ldc + o) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-}
-
-// nr_set_split_tail; off by default: the split rows depend on M, so with it on a
-// row's bits depend on how the table is cut into chunks / rank shards (round-3
-// GPU run: the chunked one-rank RCCL transform differed from one launch), for
-// ~15 us per K = 4096 GEMM (profiles/round3/split_tail_ab.jsonl)
-static std::atomic<int> g_split_tail{0};
-
-// Scratch the split tail may need (f32 partials), for any M: at most #CUs tiles
-// of 256 x 256 f32 are in the tail's slices.
-int64_t split_tail_scratch_bytes() { return (int64_t)num_cus() * G2BM * G2BN * 4; }
-
-// bf16 -> bf16 GEMM over M rows with the split-K tail (see above); `lnf`:
-// LayerNorm folded (stats [M] pairs, uc [2N], no bias) as gemm_lnfold_dispatch.
-// Falls back to the single persistent launch when splitting does not pay
-// (K < 4096, no partial last round, fewer than 2 slices, or too little scratch).
-// K >= 4096 only: at K = 1024 a tile takes ~20 us, the idle part of the last
-// round is worth less than the slice launch + fixup + f32 partial traffic
-// (measured in round 3: latent S + ff1 split 26 us slower per transform).
-int gemm_split_tail_dispatch(int epi, bool lnf, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
-                             const void* W, int64_t ldw, const float* bias, const float* stats, const float* uc,
-                             const void* R, int64_t ldr, void* C, int64_t ldc, void* scratch, int64_t scratch_bytes,
-                             hipStream_t s) {
-  auto whole = [&](int64_t m, int64_t r0) -> int {
-    const char* a = (const char*)A + r0 * lda * 2;
-    char* c = (char*)C + r0 * ldc * 2;
-    const char* r = R ? (const char*)R + r0 * ldr * 2 : nullptr;
-    if (lnf) return gemm_lnfold_dispatch(epi, m, N, K, a, lda, W, ldw, stats + 2 * r0, uc, c, ldc, s);
-    return gemm_dispatch(NR_BF16, NR_BF16, epi, m, N, K, a, lda, W, ldw, bias, r, ldr, c, ldc, s);
-  };
-  const int ncu = num_cus();
-  const int64_t ntn = N / G2BN;
-  const int64_t ntm = (M + G2BM - 1) / G2BM;
-  if (!g_split_tail.load() || N % G2BN || K < 4096 || ntn > ncu || ncu % ntn) return whole(M, 0);
-  const int64_t per_round = ncu / ntn;                 // M-tiles per full round
-  const int64_t ntm_main = ntm / per_round * per_round;
-  const int64_t tail_tiles = (ntm - ntm_main) * ntn;
-  if (tail_tiles == 0) return whole(M, 0);
-  int parts = (int)(ncu / tail_tiles);
-  if (parts > NR_GEMM_MAX_GROUP) parts = NR_GEMM_MAX_GROUP;
-  while (parts > 1 && (K % (64 * parts) || K / parts < 128)) --parts;
-  const int64_t row0 = ntm_main * G2BM, rows = M - row0;
-  if (parts < 2 || !scratch || scratch_bytes < (int64_t)parts * rows * N * 4 || ((uintptr_t)scratch & 15))
-    return whole(M, 0);
-  int rc;
-  if (row0 > 0 && (rc = whole(row0, 0))) return rc;
-  // the tail rows as `parts` K-slices: out_p = A[row0:, k_p] . W[:, k_p]^T (f32, no bias)
-  GemmGroup g{};
-  const int64_t ks = K / parts;
-  int64_t tiles = 0;
-  for (int p = 0; p < parts; ++p) {
-    g.M[p] = rows; g.N[p] = N; g.K[p] = ks;
-    g.A[p] = (const __bf16*)A + row0 * lda + p * ks;
-    g.W[p] = (const __bf16*)W + p * ks;
-    g.C[p] = (float*)scratch + (int64_t)p * rows * N;
-    g.lda[p] = lda; g.ldw[p] = ldw; g.ldc[p] = N;
-    g.ntn[p] = (int)ntn;
-    tiles += ((rows + G2BM - 1) / G2BM) * ntn;
-    g.tile_end[p] = (int)tiles;
-  }
-  g.n = parts;
-  hipLaunchKernelGGL((gemm256p_group_kernel<__bf16, float, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);
-  NR_CHECK_LAUNCH("nr_gemm(split tail)");
-  const int64_t ncols = epi == NR_EPI_GEGLU ? N / 2 : N;
-  const dim3 grid((unsigned)((ncols / 4 + 255) / 256), (unsigned)rows);
-  const float* st = lnf ? stats + 2 * row0 : nullptr;
-  const __bf16* r = R ? (const __bf16*)R + row0 * ldr : nullptr;
-  __bf16* c = (__bf16*)C + row0 * ldc;
-  const float* P = (const float*)scratch;
-#define NR_FIX(E)                                                                                                 \
-  do {                                                                                                            \
-    if (lnf)                                                                                                      \
-      hipLaunchKernelGGL((tail_fixup_kernel<E, true>), grid, dim3(256), 0, s, rows, N, parts, P, nullptr, st, uc, \
-                         r, ldr, c, ldc);                                                                         \
-    else                                                                                                          \
-      hipLaunchKernelGGL((tail_fixup_kernel<E, false>), grid, dim3(256), 0, s, rows, N, parts, P, bias, st, uc,   \
-                         r, ldr, c, ldc);                                                                         \
-  } while (0)
-  switch (epi) {
-    case NR_EPI_NONE: NR_FIX(NR_EPI_NONE); break;
-    case NR_EPI_RELU: NR_FIX(NR_EPI_RELU); break;
-    case NR_EPI_EXP: NR_FIX(NR_EPI_EXP); break;
-    case NR_EPI_GEGLU: NR_FIX(NR_EPI_GEGLU); break;
-    case NR_EPI_RESADD: NR_FIX(NR_EPI_RESADD); break;
-    case NR_EPI_SOFTMAX64: NR_FIX(NR_EPI_SOFTMAX64); break;
-    default: set_error("nr_gemm(split tail): epilogue %d unsupported", epi); return NR_ERR_UNSUPPORTED;
-  }
-#undef NR_FIX
-  NR_CHECK_LAUNCH("nr_gemm(split tail fixup)");
-  return NR_OK;
-}
-
 }  // namespace nr
-
-extern "C" int nr_set_split_tail(int on) {
-  nr::g_split_tail.store(on ? 1 : 0);
-  return NR_OK;
-}
 
 extern "C" int nr_gemm_relu_dropout(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K,
                                     const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,

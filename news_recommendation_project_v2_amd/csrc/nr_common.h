@@ -24,6 +24,7 @@ void clear_error();
 // memory.  check_device_ptrs names the first offending argument of the
 // stringified list `names`; null pointers are skipped (nullable arguments).
 bool device_accessible(const void* p);
+void residency_flush();  // drop every thread's verified ranges (nr_residency_flush)
 int check_device_ptrs(const char* fn, const char* names, std::initializer_list<const void*> ptrs);
 
 // internal dispatchers (validate + launch, no error reset)
@@ -47,13 +48,6 @@ int row_stats_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int6
 // NR_EPI_GEGLU): C = epi(rstd_m * (A W^T - mean_m u_n) + c_n); stats [M] (mean, rstd), uc [2][N]
 int gemm_lnfold_dispatch(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W,
                          int64_t ldw, const float* stats, const float* uc, void* C, int64_t ldc, hipStream_t s);
-// bf16 GEMM whose last partial round of tiles runs as K-slices + a fixup (gemm.hip);
-// lnf: LayerNorm folded (stats / uc as gemm_lnfold_dispatch).  scratch: f32 partials.
-int64_t split_tail_scratch_bytes();
-int gemm_split_tail_dispatch(int epi, bool lnf, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
-                             const void* W, int64_t ldw, const float* bias, const float* stats, const float* uc,
-                             const void* R, int64_t ldr, void* C, int64_t ldc, void* scratch, int64_t scratch_bytes,
-                             hipStream_t s);
 int inv_norm_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps,
                       float* out, hipStream_t s);
 

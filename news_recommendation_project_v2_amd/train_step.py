@@ -320,7 +320,8 @@ class LatentAttentionTrainStep:
 
     def __init__(self, token_model, latent_model, dtype: torch.dtype = torch.float32, lr: float = 1e-6,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.01, max_norm: float = 0.5,
-                 dropout: float = 0.0, seed: int = 1234, device=None):
+                 seed: int = 1234, device=None):
+        # (no dropout argument: LatentAttentionModel has no dropout, latent_attention.py:77-171)
         if dtype not in (torch.float32, torch.bfloat16):
             raise NewsRecHIPError("latent-attention train step dtype must be float32 or bfloat16")
         layers = list(token_model.encoder.layer)

@@ -224,14 +224,38 @@ def per_news_tables_large(pooler: str, sd: dict, table: torch.Tensor, chunk: int
 _FASTPOOL = []
 
 
+def build_fastpool():
+    """Compile oracle/fastpool.c -> oracle/libfastpool.so (gcc -O3 -fopenmp) when
+    missing or built from other source text (sha256 sidecar).  Test
+    infrastructure: only the oracle's own full-size checker loads it, so it is
+    built here on first use, not by __graft_entry__.build()."""
+    import hashlib
+    import subprocess
+    from pathlib import Path
+    here = Path(__file__).resolve().parent
+    src, so, tag = here / "fastpool.c", here / "libfastpool.so", here / "libfastpool.so.hash"
+    h = hashlib.sha256(src.read_bytes()).hexdigest()[:16]
+    if so.is_file() and tag.is_file() and tag.read_text() == h:
+        return so
+    tmp = so.with_suffix(".so.tmp")
+    subprocess.run(["gcc", "-O3", "-fopenmp", "-fPIC", "-shared", str(src), "-o", str(tmp), "-lm"], check=True)
+    tmp.replace(so)
+    tag.write_text(h)
+    return so
+
+
 def _fastpool():
-    """oracle/libfastpool.so (built by __graft_entry__.build()), or None."""
+    """oracle/libfastpool.so (built on first use by build_fastpool), or None
+    when it cannot be built (no gcc): the torch reductions below then run."""
     if not _FASTPOOL:
         import ctypes
-        from pathlib import Path
-        so = Path(__file__).resolve().with_name("libfastpool.so")
+        import subprocess
+        try:
+            so = build_fastpool()
+        except (OSError, subprocess.CalledProcessError):
+            so = None
         lib = None
-        if so.is_file():
+        if so is not None:
             lib = ctypes.CDLL(str(so))
             v, i64 = ctypes.c_void_p, ctypes.c_int64
             lib.fp_pool.argtypes = [ctypes.c_int, v, i64, v, v, i64, v]

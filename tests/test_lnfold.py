@@ -83,50 +83,3 @@ def test_latent_lnfold_rejects_f32(gpu_device):
                                                 p(w["Wf_ln"]), p(w["ucf"]), p(w["W2"]), p(w["b2"]), p(out), p(ws),
                                                 ws.numel(), None)
     assert rc == -3, rc  # NR_ERR_UNSUPPORTED
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("pooler", ["latent", "final"])
-def test_split_tail_matches_unsplit(gpu_device, pooler):
-    """The bf16 transforms' split-K tail (rows past the last full round of
-    tiles run as K-slices + fixup: at M = 72,023 the K = 4096 GEMMs, latent ff2
-    and final.l3 / l5) against the same transform with the split off: rows
-    before the tail are bit-identical; in the tail rows a split GEMM's sums
-    differ from the unsplit one's only in f32 summation order, which moves a
-    bf16 output by at most one rounding step.  Latent: ff2 is the last GEMM, so
-    each tail value is within one bf16 ulp (2^-7 relative, + 2^-12 for the
-    residual's cancellation).  FinalAttention: x (l3) moves by an ulp, which
-    l4 and l5 carry into the exp logits (an element-wise bound of 2^-4 of the
-    row's rms logit failed on the box), so the logits are held by every tail
-    row's cosine with the unsplit row > 0.9999.  The split is opt-in (off by
-    default)."""
-    from news_recommendation_project_v2_amd import _lib, synthetic
-    from news_recommendation_project_v2_amd.engine import PoolScoreEngine
-    from news_recommendation_project_v2_amd.latent_attention import LatentAttentionModel
-    from news_recommendation_project_v2_amd.modeling_utils import FinalAttention
-    n = synthetic.SHAPES["mind_large_dev"][0]
-    m = LatentAttentionModel() if pooler == "latent" else FinalAttention(1024, 4096)
-    m.load_state_dict(W.latent_attention_state_dict(1234) if pooler == "latent" else W.final_attention_state_dict(1234))
-    m = m.to(gpu_device).eval()
-    table = W.news_table(1234, n, 1024, name="mind_large").to(gpu_device)
-    eng = PoolScoreEngine(m, dtype=torch.bfloat16, device=gpu_device).load_news(table)
-    lib = _lib.load()
-    try:
-        lib.nr_set_split_tail(0)
-        ref = eng.transform().clone()
-        lib.nr_set_split_tail(1)
-        got = eng.transform().clone()
-    finally:
-        lib.nr_set_split_tail(0)  # the library default
-    torch.cuda.synchronize()
-    head = 65536  # every split GEMM's full rounds cover at least these rows
-    assert torch.equal(got[:head], ref[:head])
-    g, r = got[head:].float(), ref[head:].float()
-    if pooler == "final":  # the exp(w) half: compare the logits
-        g, r = torch.cat([g[:, :1024], g[:, 1024:].log()], 1), torch.cat([r[:, :1024], r[:, 1024:].log()], 1)
-    # latent: ff2's own output; final: x, l3's own output (the logits by the row cosine below)
-    gx, rx = (g, r) if pooler == "latent" else (g[:, :1024], r[:, :1024])
-    tol = rx.abs() * 2.0 ** -7 + 2.0 ** -12
-    assert ((gx - rx).abs() <= tol).all(), float(((gx - rx).abs() - tol).max())
-    assert float(torch.nn.functional.cosine_similarity(g, r, dim=1).min()) > 0.9999  # 0.99998 measured (final)
-    assert not torch.equal(got, ref) or pooler == "final"  # the latent tail did take the split path

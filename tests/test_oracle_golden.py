@@ -110,7 +110,7 @@ def test_large_oracle_matches_reference(pooler, fast, monkeypatch):
     table = W.news_table(1234, int(g["n_news"]), 1024, name=str(g["table_name"]))
     if fast:
         if pool_ref._fastpool() is None:
-            pytest.skip("oracle/libfastpool.so not built (run __graft_entry__.build())")
+            pytest.skip("oracle/libfastpool.so could not be built (gcc -fopenmp)")
     else:
         monkeypatch.setattr(pool_ref, "_fastpool", lambda: None)
     s = pool_ref.cos_sim_scores_large(pooler, sd, g["hist_idx"], g["hist_len"], g["cand_idx"], g["cand_len"], table,

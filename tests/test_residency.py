@@ -91,3 +91,24 @@ def test_encoder_forward_refuses_host_weights(gpu_device):
     torch.cuda.synchronize()
     assert torch.isfinite(pooled).all()
     np.testing.assert_array_less(0.0, pooled.abs().sum(1).cpu().numpy())
+
+
+@pytest.mark.gpu
+def test_residency_flush_drops_freed_ranges(gpu_device):
+    """verified ranges are cached per thread; after torch returns a
+    segment to the driver (empty_cache) its address range is no longer device
+    memory.  nr_residency_flush (called by _lib.empty_cache) drops the cached
+    ranges, so the freed address is verified again and refused.  Only the
+    query entry is called with the stale pointer: nothing is launched on it."""
+    lib = _lib.load()
+    t = torch.empty(512 << 20, dtype=torch.uint8, device=gpu_device)  # its own 512 MiB segment
+    p = ctypes.c_void_p(t.data_ptr() + (256 << 20))
+    assert lib.nr_is_device_pointer(p) == 1
+    del t
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()  # the segment goes back to the driver; the range is still cached
+    assert lib.nr_is_device_pointer(p) == 1  # the stale verdict the flush exists for
+    _lib.empty_cache()  # empty_cache + nr_residency_flush
+    assert lib.nr_is_device_pointer(p) == 0
+    (torch.ones(4, device=gpu_device) * 2).sum().item()  # no HIP error left behind
+    assert lib.nr_is_device_pointer(ctypes.c_void_p(torch.ones(4, device=gpu_device).data_ptr())) == 1

@@ -81,8 +81,8 @@ def _calls(P):
 def test_every_entry_with_pointers_is_covered():
     """The table below names every header entry that takes a device pointer."""
     no_ptr = {"nr_version", "nr_build_hash", "nr_init", "nr_last_error", "nr_set_persistent_workgroups",
-              "nr_persistent_workgroups", "nr_set_split_tail", "nr_final_attn_workspace_bytes", "nr_latent_workspace_bytes",
-              "nr_encoder_workspace_bytes"}
+              "nr_persistent_workgroups", "nr_final_attn_workspace_bytes", "nr_latent_workspace_bytes",
+              "nr_encoder_workspace_bytes", "nr_residency_flush", "nr_is_device_pointer"}
     assert set(_calls(ctypes.c_void_p(256))) == set(_lib.SIGNATURES) - no_ptr
 
 
@@ -93,3 +93,10 @@ def test_host_pointers_refused_by_every_entry(lib, H):
         msg = lib.nr_last_error().decode()
         assert rc == -1, f"{name}: rc {rc} ({msg})"
         assert "not device memory" in msg, f"{name}: {msg}"
+
+
+def test_is_device_pointer_refuses_host_memory(lib, H):
+    _, P = H
+    assert lib.nr_is_device_pointer(P) == 0
+    assert lib.nr_is_device_pointer(None) == 0
+    assert lib.nr_residency_flush() == 0

@@ -10,6 +10,11 @@ that A/B ran (recorded in DESIGN.md §3.2 / profiles/round*/): adopted ones
 (quarters, dma2, fastexp) are in the source now, and patches written against
 an older main loop no longer apply (the script then stops at the failing
 assert instead of building a wrong library).
+
+The lab-only kernels (the MF32 32x32x16 branches of gemm256t_kernel and the
+4-wave gemm256w4_kernel, DESIGN.md §3.2b: measured, not adopted) are not in the
+product source: variants listed in OVERLAY first apply
+patches/lab_kernels.patch (a unified diff against csrc/gemm.hip) to the copy.
 """
 import subprocess
 import sys
@@ -475,14 +480,23 @@ __device__ __forceinline__ void gelu_erf2x2(f32x2v& g0, f32x2v& g1) {
 }
 
 
+# variants whose launch swaps need the lab kernels patched back into the copy
+OVERLAY = {"mf32": "lab_kernels.patch", "w4": "lab_kernels.patch"}
+
+
 def main():
     name = sys.argv[1]
+    build = OUT / "build"
+    build.mkdir(exist_ok=True)
     src = (CSRC / "gemm.hip").read_text()
+    if name in OVERLAY:
+        base = build / f"gemm_{name}_base.hip"
+        base.write_text(src)
+        subprocess.run(["patch", "-s", str(base), str(OUT / "patches" / OVERLAY[name])], check=True)
+        src = base.read_text()
     for old, new in VARIANTS[name]:
         assert src.count(old) == 1, old
         src = src.replace(old, new)
-    build = OUT / "build"
-    build.mkdir(exist_ok=True)
     (build / f"gemm_{name}.hip").write_text(src)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I", str(CSRC), "-c",
                     str(build / f"gemm_{name}.hip"), "-o", str(build / f"gemm_{name}.o")], check=True)
