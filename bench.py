@@ -193,6 +193,44 @@ def timed(step, steps: int, warmup: int, world: int, dev, host_reduce: bool):
     return dt
 
 
+def rank_parity(run: Run, n_check: int = 200, seed: int = 0) -> float:
+    """Max |score - float64 re-pool| over `n_check` sampled impressions of this
+    rank's range, re-pooled from the rank's own (all-gathered) table and
+    candidate rows in float64 (tests/test_gpu_parity.py
+    test_full_size_mind_large_properties): FinalAttention sum x p / (sum p +
+    1e-10), latent normalize(mean); cosine with the per-vector 1e-8 clamps."""
+    s, _ = run.step()
+    torch.cuda.synchronize()
+    imps, eng = run.imps, run.eng
+    if imps.n_imp == 0:
+        return 0.0
+    rng = np.random.default_rng(seed)
+    ho, co = imps.hist_off(), imps.cand_off()
+    dev = s.device
+    tab, cand = eng.hist_table, eng.cand_table
+    err = 0.0
+    for i in rng.choice(imps.n_imp, min(n_check, imps.n_imp), replace=False):
+        rows = tab[torch.as_tensor(imps.hist_idx[ho[i]:ho[i + 1]], dtype=torch.long, device=dev)].double()
+        if run.pooler == "final":
+            x, p = rows[:, :1024], rows[:, 1024:]
+            u = (x * p).sum(0) / (p.sum(0) + 1e-10)
+        else:
+            u = rows.mean(0)
+            u = u / u.norm().clamp_min(1e-12)
+        e = cand[torch.as_tensor(imps.cand_idx[co[i]:co[i + 1]], dtype=torch.long, device=dev)].double()
+        ref = (e @ u) / u.norm().clamp_min(1e-8) / e.norm(dim=1).clamp_min(1e-8)
+        err = max(err, float((s[co[i]:co[i + 1]].double() - ref).abs().max()))
+    return err
+
+
+def table_digest(t: torch.Tensor) -> int:
+    """Order-sensitive integer digest of a table's bytes (equal on every rank
+    iff the all-gathered tables agree, up to a 2^-63 collision chance)."""
+    v = t.contiguous().view(torch.int16).to(torch.int64).flatten()
+    w = torch.arange(1, v.numel() + 1, device=v.device, dtype=torch.int64) % 1_000_003
+    return int(((v * w).sum() % (2 ** 61 - 1)).item())
+
+
 def auc_of(run: Run) -> float:
     """Mean AUC over all impressions: dense ranks + per-impression metrics on the
     device (nr_dense_rank, nr_impression_metrics; == evaluation.score, tested)."""
@@ -505,20 +543,32 @@ def auc_gate_full(dev, poolers=("latent", "final"), dtype: str = "bf16") -> dict
         eng = PoolScoreEngine(make_model(pooler, dev), dtype=DTYPES[dtype], device=dev).load_news(table_d)
         eng.load_impressions(imps.hist_idx, imps.hist_len, imps.cand_idx, imps.cand_len)
         s, _ = eng.step()
-        g = evaluation.score_device(eng.rank(s), imps.labels, imps.cand_off())
+        r = eng.rank(s)
+        g = evaluation.score_device(r, imps.labels, imps.cand_off())
         diff = abs(g["auc"] - auc_ref)
         out[pooler] = {"cpu_ref_f32_auc": auc_ref, f"gpu_{dtype}_auc": g["auc"], "auc_abs_diff": diff,
                        "auc_equal_4dp": bool(diff < AUC_4DP),
                        "auc_rounded_4dp_equal": round(g["auc"], 4) == round(auc_ref, 4),
                        "max_abs_score_diff": float(np.abs(s.cpu().numpy() - ref).max()),
                        "cpu_ref_seconds": round(t_cpu, 1)}
-        log(f"[bench] AUC gate {pooler}: cpu f32 {auc_ref:.7f} gpu {dtype} {g['auc']:.7f} |d| {diff:.2e} "
+        # the same gate with clicks that follow the reference score (AUC ~ 0.8: ranking quality)
+        lab = synthetic.logistic_labels(ref, imps.cand_len)
+        a_ref = float(np.nanmean(data_ref.impression_aucs(ref, lab, imps.cand_len)))
+        a_gpu = evaluation.score_device(r, lab, imps.cand_off())["auc"]
+        out[pooler]["logistic_labels"] = {
+            "cpu_ref_f32_auc": a_ref, f"gpu_{dtype}_auc": a_gpu, "auc_abs_diff": abs(a_gpu - a_ref),
+            "auc_equal_4dp": bool(abs(a_gpu - a_ref) < AUC_4DP),
+            "auc_rounded_4dp_equal": round(a_gpu, 4) == round(a_ref, 4),
+            "labels": "y ~ Bernoulli(sigmoid(4 (s_ref - q90) / std)), synthetic.logistic_labels"}
+        log(f"[bench] AUC gate {pooler}: cpu f32 {auc_ref:.7f} gpu {dtype} {g['auc']:.7f} |d| {diff:.2e}; "
+            f"logistic labels cpu {a_ref:.7f} gpu {a_gpu:.7f} |d| {abs(a_gpu - a_ref):.2e} "
             f"(CPU reference {t_cpu:.1f}s)")
-        del eng, s, ref
+        del eng, s, r, ref
         _lib.empty_cache()
     return {"impressions": imps.n_imp, "candidates": imps.n_cand, "by_pooler": out,
-            "auc_equal_4dp": all(v["auc_equal_4dp"] for v in out.values()),
-            "criterion": f"|AUC_gpu - AUC_cpu_ref| < {AUC_4DP}"}
+            "auc_equal_4dp": all(v["auc_equal_4dp"] and v["logistic_labels"]["auc_equal_4dp"] for v in out.values()),
+            "criterion": f"|AUC_gpu - AUC_cpu_ref| < {AUC_4DP} for both label sets (random i.i.d. clicks and "
+                         f"logistic-of-reference-score clicks)"}
 
 
 def load_traffic(pooler: str, dtype: str):
@@ -672,6 +722,63 @@ def main():
         extra["allgather_GBs_in_per_gpu"] = round(gb_in / (g_ms * 1e-3) / 1e9, 1) if g_ms > 0 else None
         extra["transform_chunks"] = head.tab.chunks
 
+    dist_info = None
+    if world > 1:
+        # what actually ran: world size / backend as initialised, RCCL version, the ranks
+        # that joined, per-rank float64 parity of 200 sampled impressions, table identity
+        red = "cpu" if host_reduce else dev
+        err = rank_parity(head)
+        ok_t = torch.tensor([1 if err <= 2e-5 else 0, 1], dtype=torch.int64, device=red)
+        dist.all_reduce(ok_t)  # [ranks with parity ok, ranks]
+        err_t = torch.tensor([err], dtype=torch.float64, device=red)
+        dist.all_reduce(err_t, op=dist.ReduceOp.MAX)
+        dg = table_digest(head.tab.full)
+        dmin = torch.tensor([dg], dtype=torch.int64, device=red)
+        dmax = dmin.clone()
+        dist.all_reduce(dmin, op=dist.ReduceOp.MIN)
+        dist.all_reduce(dmax, op=dist.ReduceOp.MAX)
+        try:
+            rv = ".".join(map(str, torch.cuda.nccl.version())) if dist.get_backend() == "nccl" else None
+        except Exception:  # noqa: BLE001
+            rv = None
+        dist_info = {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "rccl_version": rv,
+                     "rccl_ranks": int(ok_t[1].item()) if dist.get_backend() == "nccl" else 0,
+                     "parity_ok": bool(int(ok_t[0].item()) == world), "parity_ranks_ok": int(ok_t[0].item()),
+                     "parity_max_abs_err": float(err_t.item()),
+                     "parity_check": "200 sampled impressions per rank vs a float64 re-pool of the rank's own "
+                                     "all-gathered table, |err| <= 2e-5",
+                     "table_identical_on_all_ranks": bool(int(dmin.item()) == int(dmax.item()))}
+        log(f"[bench] ranks: {json.dumps(dist_info)}")
+
+    if world > 1 and not args.no_extra and args.backend == "nccl":
+        # the same all-gather through the library's own RCCL communicator (nr_comm_init /
+        # nr_allgather): its step time and its table against torch's bit for bit
+        from news_recommendation_project_v2_amd.distributed import NrComm
+        comm = None
+        try:
+            ref_table = head.tab.full.clone()
+            comm = NrComm(rank, world)
+            r = Run(args.pooler, args.dtype, imps, table, dev, rank, world)
+            r.tab = ShardedTable(r.eng, rank, world, comm=comm)
+            r.tab.timing = True
+            d = timed(r.step, max(3, args.steps // 2), 2, world, dev, host_reduce) / max(3, args.steps // 2)
+            r.tab.build()
+            torch.cuda.synchronize()
+            t_ms, g_ms = r.tab.last_ms()
+            same = torch.tensor([int(torch.equal(r.tab.full, ref_table))], device=dev)
+            dist.all_reduce(same, op=dist.ReduceOp.MIN)
+            extra["nr_allgather"] = {"ms_per_step": round(d * 1e3, 3), "value": round(total_cand / d, 1),
+                                     "allgather_ms": round(float(g_ms), 3),
+                                     "table_bit_identical_to_torch": bool(same.item())}
+            r.tab.timing = False
+            del r, ref_table
+        except Exception as e:  # noqa: BLE001  (an extra: report, never fail the headline)
+            extra["nr_allgather"] = {"error": repr(e)[:300]}
+        finally:
+            if comm is not None:
+                comm.close()
+            _lib.empty_cache()
+
     if world > 1 and not args.no_extra:
         # the opt-in overlapped build (2 chunks, each chunk's all-gather beside the next
         # chunk's transform): its step time, and its table against the default's bit for bit
@@ -701,6 +808,11 @@ def main():
         key = "weak_scaling" if args.scaling == "strong" else "strong_scaling"
         extra[key] = {"value": round(int(c.item()) / d, 1), "ms_per_step": round(d * 1e3, 3),
                       "impressions_per_gpu_rank0": other.n_imp}
+        other_parity = rank_parity(r)
+        pt = torch.tensor([other_parity], dtype=torch.float64, device="cpu" if host_reduce else dev)
+        dist.all_reduce(pt, op=dist.ReduceOp.MAX)
+        extra[key]["parity_max_abs_err"] = float(pt.item())
+        extra[key]["parity_ok"] = bool(float(pt.item()) <= 2e-5)
         del r, other
         _lib.empty_cache()
 
@@ -812,6 +924,13 @@ def main():
                          "frac_vs_gather_ceiling": round(achieved / GATHER_CEILING_GBS, 4),
                          "traffic": load_traffic(args.pooler, args.dtype) if world == 1 else None,
                          "algorithmic_bytes_per_launch": bytes_ps, "avg_launch_ms": round(stages[2], 4)},
+            # both scaling readings at the top level: configs[3] is ONE MIND-large eval
+            # partitioned over the ranks (strong); weak = a full set per rank
+            "configs3_value": (round(value, 1) if world == 1 or args.scaling == "strong" else
+                               extra.get("strong_scaling", {}).get("value")),
+            "weak_scaling_value": (round(value, 1) if world == 1 or args.scaling == "weak" else
+                                   extra.get("weak_scaling", {}).get("value")),
+            "distributed": dist_info,
             "cpu_baseline": cpu,
             # the north star's AUC clause on the headline workload itself (configs[2] size)
             "auc_parity": gate,

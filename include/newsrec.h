@@ -72,7 +72,7 @@ extern "C" {
 int nr_version(void);
 
 /* Hash of the sources the library was built from (16 hex digits: sha256 of
- * csrc/{capi,gemm,pool_score,rowops,rank,encoder,train,metrics}.hip,
+ * csrc/{capi,gemm,pool_score,rowops,rank,encoder,train,metrics,comm}.hip,
  * csrc/nr_common.h and this header, concatenated in that order); the Python
  * loader refuses a library whose hash differs from the tree it sits in. */
 const char* nr_build_hash(void);
@@ -446,6 +446,29 @@ int nr_sumsq(int64_t n, const float* x, float* out, void* stream);
 int nr_adamw(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf16, int64_t step, float lr,
              float beta1, float beta2, float eps, float weight_decay, float max_norm, const float* sumsq,
              void* stream);
+
+/*
+ * ---- RCCL communicator of the multi-GPU eval (SURVEY §8(b) nr_allgather,
+ * §8(e)): one process per GPU; every rank transforms a row shard of the
+ * per-news table and ONE all-gather over xGMI gives each GPU the whole table.
+ * The reference has no distributed code: this is the exchange
+ * step the north star adds.  RCCL is resolved at run time (the process's
+ * librccl.so.1, e.g. the one torch mapped); without it the entries return
+ * NR_ERR_UNSUPPORTED.
+ *   rank 0: nr_comm_unique_id(id); the host sends the 128 id bytes to every
+ *   rank (any channel: torch.distributed broadcast, a file, MPI ...);
+ *   every rank: nr_init(device); nr_comm_init(&c, id, nranks, rank)
+ *   (collective: blocks until all nranks have called it).
+ * nr_allgather: recv[r * bytes_per_rank ..] = rank r's send, async on `stream`;
+ * in place when send == recv + rank * bytes_per_rank.
+ */
+#define NR_COMM_ID_BYTES 128
+typedef struct nr_comm* nr_comm_t;
+int nr_rccl_version(void); /* RCCL's NCCL_VERSION_CODE, 0 when RCCL is absent */
+int nr_comm_unique_id(unsigned char* id);
+int nr_comm_init(nr_comm_t* comm, const unsigned char* id, int nranks, int rank);
+int nr_comm_destroy(nr_comm_t comm);
+int nr_allgather(nr_comm_t comm, const void* send, void* recv, int64_t bytes_per_rank, void* stream);
 
 /*
  * ---- Whole title-encoder forward (get_embeddings, data_model_helper.py:45-84:

@@ -18,7 +18,7 @@ CSRC = Path(__file__).resolve().with_name("csrc")
 INCLUDE = Path(__file__).resolve().parent.parent / "include"
 # translation units of libnewsrec_hip.so, in link order (also the hash order)
 HIP_SOURCES = ("capi.hip", "gemm.hip", "pool_score.hip", "rowops.hip", "rank.hip", "encoder.hip", "train.hip",
-               "metrics.hip")
+               "metrics.hip", "comm.hip")
 
 
 def hip_source_files() -> list:
@@ -76,6 +76,11 @@ SIGNATURES = {
     "nr_init": (_i, [_i]),
     "nr_last_error": (ctypes.c_char_p, []),
     "nr_residency_flush": (_i, []),
+    "nr_rccl_version": (_i, []),
+    "nr_comm_unique_id": (_i, [_p]),
+    "nr_comm_init": (_i, [_p, _p, _i, _i]),
+    "nr_comm_destroy": (_i, [_p]),
+    "nr_allgather": (_i, [_p, _p, _p, _l, _p]),
     "nr_is_device_pointer": (_i, [_p]),
     "nr_set_persistent_workgroups": (_i, [_i]),
     "nr_persistent_workgroups": (_i, []),

@@ -49,6 +49,49 @@ def partition_by_cost(hist_len: np.ndarray, cand_len: np.ndarray, world: int, ta
     return np.maximum.accumulate(b).astype(np.int64)
 
 
+class NrComm:
+    """The library's own RCCL communicator (include/newsrec.h nr_comm_*,
+    SURVEY §8(b) nr_allgather): rank 0 draws the 128-byte unique id
+    (nr_comm_unique_id), the host broadcasts it over the torch.distributed
+    group, and every rank joins (nr_comm_init, collective).  ``allgather``
+    issues ncclAllGather on the current torch stream."""
+
+    def __init__(self, rank: int, world: int, group=None):
+        import ctypes
+        from . import _lib
+        self._lib = _lib.load()
+        self.rank, self.world = rank, world
+        idb = (ctypes.c_ubyte * 128)()
+        if rank == 0:
+            _lib.check(self._lib.nr_comm_unique_id(idb), "nr_comm_unique_id")
+        dev = torch.device("cuda", torch.cuda.current_device())
+        staged = _host_staged(group)
+        t_id = torch.tensor(bytes(idb), dtype=torch.uint8, device="cpu" if staged else dev)
+        dist.broadcast(t_id, src=0, group=group)
+        idb = (ctypes.c_ubyte * 128)(*t_id.cpu().tolist())
+        self._lib.nr_init(dev.index)
+        self._h = ctypes.c_void_p()
+        _lib.check(self._lib.nr_comm_init(ctypes.byref(self._h), idb, world, rank), "nr_comm_init")
+
+    def allgather(self, send: torch.Tensor, recv: torch.Tensor) -> None:
+        from . import _lib
+        nb = send.numel() * send.element_size()
+        assert recv.numel() * recv.element_size() == nb * self.world and send.is_contiguous() and recv.is_contiguous()
+        _lib.check(self._lib.nr_allgather(self._h, send.data_ptr(), recv.data_ptr(), nb,
+                                          torch.cuda.current_stream().cuda_stream), "nr_allgather")
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.nr_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # best effort; call close() explicitly before the process group goes
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 # the shard's transform is cut in two (rows permitting) so that the all-gather of
 # the first half runs on the communicator's stream while the second half is
 # transformed.  Measured price of the cut alone (tools/chunk_probe.py, latent
@@ -83,8 +126,12 @@ class ShardedTable:
     for RCCL's stream at the end of the call, so the second interval is the
     all-gather); ``last_ms()`` reads them after a sync."""
 
-    def __init__(self, engine: PoolScoreEngine, rank: int, world: int, group=None, chunks=1, timing: bool = False):
+    def __init__(self, engine: PoolScoreEngine, rank: int, world: int, group=None, chunks=1, timing: bool = False,
+                 comm: Optional[NrComm] = None):
         self.eng, self.rank, self.world, self.group = engine, rank, world, group
+        # comm: run the all-gather through the library's own RCCL communicator
+        # (nr_allgather) instead of torch.distributed's (one chunk only)
+        self.comm = comm
         n = engine.hist_src.shape[0]
         self.rows = shard_rows(n, world)
         width = 2048 if engine.pooler == "final" else 1024
@@ -107,7 +154,9 @@ class ShardedTable:
         self.local = self.full[rank * self.rows:(rank + 1) * self.rows] if in_place else \
             torch.empty((self.rows, width), dtype=engine.dtype, device=engine.device)
         if chunks is None or chunks == "auto":
-            chunks = 2 if world > 1 and self.rows >= 2 * CHUNK_MIN_ROWS else 1
+            chunks = 2 if world > 1 and self.rows >= 2 * CHUNK_MIN_ROWS and comm is None else 1
+        if comm is not None and chunks != 1:
+            raise ValueError("ShardedTable: the nr_allgather path gathers the shard in one piece (chunks=1)")
         self.chunks = max(1, min(int(chunks), self.rows))
         self.bounds = [round(c * self.rows / self.chunks) for c in range(self.chunks + 1)]
         self.timing = bool(timing) and self.full.is_cuda
@@ -143,7 +192,10 @@ class ShardedTable:
             self._mark(0)
             self.eng.transform(rows=slice(self.lo, self.lo + self.rows), out=self.local, src=self.src)
             self._mark(1)
-            dist.all_gather_into_tensor(self.full.view(torch.uint8), self.local.view(torch.uint8), group=self.group)
+            if self.comm is not None:
+                self.comm.allgather(self.local.view(torch.uint8), self.full.view(torch.uint8))
+            else:
+                dist.all_gather_into_tensor(self.full.view(torch.uint8), self.local.view(torch.uint8), group=self.group)
             self._mark(2)
             return
         reserve = self.full.is_cuda and self.chunks > 1
@@ -169,7 +221,7 @@ class ShardedTable:
         self._mark(2)
 
     def build(self) -> torch.Tensor:
-        if self.world > 1 and not (_host_staged(self.group) and self.local.is_cuda):
+        if self.comm is not None or (self.world > 1 and not (_host_staged(self.group) and self.local.is_cuda)):
             self._overlapped()
             self.eng.hist_table = self.full
             return self.full

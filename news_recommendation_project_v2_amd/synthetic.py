@@ -123,3 +123,24 @@ def to_behaviors(imps: Impressions, with_labels: bool = True, news_prefix: str =
     hist = [" ".join(hist_tok[ho[i]:ho[i + 1]]) if ho[i + 1] > ho[i] else None for i in range(imps.n_imp)]
     impr = [" ".join(cand_tok[co[i]:co[i + 1]]) for i in range(imps.n_imp)]
     return hist, impr
+
+
+def logistic_labels(ref_scores, cand_len, seed: int = 1, slope: float = 4.0) -> np.ndarray:
+    """Clicks that follow a reference score (so an AUC measures ranking quality,
+    not noise around 0.5): y ~ Bernoulli(sigmoid(slope * z)), z = (s - q90(s)) /
+    std(s) over all candidates (the recipe of tests/test_gpu_parity.py
+    test_gpu_f32_and_bf16_vs_oracle_auc).  An impression left with one class gets
+    one candidate flipped, chosen uniformly (not by score), so every impression
+    has both classes and a defined AUC, as the MIND-shaped random labels do.
+    Returns int64 [C]."""
+    s = np.asarray(ref_scores, dtype=np.float64)
+    lens = np.asarray(cand_len, dtype=np.int64)
+    rng = np.random.default_rng(seed)
+    z = (s - np.quantile(s, 0.9)) / (s.std() + 1e-12)
+    y = (rng.random(len(s)) < 1.0 / (1.0 + np.exp(-slope * z))).astype(np.int64)
+    off = np.concatenate([[0], np.cumsum(lens)])
+    pos = np.add.reduceat(y, off[:-1]) if len(lens) else np.zeros(0, np.int64)
+    one_class = np.nonzero((pos == 0) | (pos == lens))[0]
+    pick = off[one_class] + (rng.random(len(one_class)) * lens[one_class]).astype(np.int64)
+    y[pick] = 1 - y[pick]
+    return y

@@ -64,7 +64,7 @@ def final_attention_train(sd, emb, mask, seeds, p, slot_rows):
     return (x * w).sum(dim=1)
 
 
-def _loss(P, tok_last, hist_groups, pos, neg, p, seeds, ln_eps, margin):
+def _loss(P, tok_last, hist_groups, pos, neg, p, seeds, ln_eps, margin, pooler="final"):
     E = F.layer_norm(tok_last.float(), (tok_last.shape[1],), P["ln.weight"], P["ln.bias"], ln_eps)
     B = len(hist_groups)
     L = max(len(h) for h in hist_groups)
@@ -78,7 +78,12 @@ def _loss(P, tok_last, hist_groups, pos, neg, p, seeds, ln_eps, margin):
         slot_rows[b, :len(h)] = np.arange(r, r + len(h))
         r += len(h)
     second = E[idx] * mask.unsqueeze(-1)
-    out = final_attention_train(P, second, mask, seeds, p, slot_rows)
+    if pooler == "latent":  # LatentAttentionModel in FinalAttention's slot (no dropout in that module)
+        from oracle import pool_ref
+        out = pool_ref.latent_attention_forward({k[7:]: v for k, v in P.items() if k.startswith("latent.")},
+                                                second, mask)
+    else:
+        out = final_attention_train(P, second, mask, seeds, p, slot_rows)
     pn = torch.as_tensor(np.concatenate([pos, neg]).astype(np.int64))
     res = F.cosine_similarity(out.repeat((2, 1)), E[pn])
     return torch.nn.MarginRankingLoss(margin)(*torch.chunk(res, 2), torch.tensor([1.0]))
@@ -124,3 +129,25 @@ def train_epoch(params: dict, batches, *, lr=1e-6, max_norm=0.5, weight_decay=0.
         tot += float(loss) * n
         cnt += n
     return tot / cnt, {k: v.detach().clone() for k, v in P.items()}
+
+
+def train_steps(params: dict, batches, *, pooler="final", lr=1e-6, max_norm=0.5, weight_decay=0.01, ln_eps=1e-12,
+                margin=2.0):
+    """The train_one_epoch loop (trainer.py:1044-1069: zero_grad, forward, loss,
+    backward, clip_grad_norm_, AdamW.step with ONE persistent optimizer) over
+    `batches` = list of (tok_last, hist_groups, pos, neg), dropout off, with
+    FinalAttention (params "ln.*", "linear*") or the latent pooler (params
+    "ln.*", "latent.<LatentAttentionModel name>").  Returns (per-step losses,
+    per-step clipped-grad total norms, params after)."""
+    P = _leaf(params)
+    plist = list(P.values())
+    opt = torch.optim.AdamW(plist, lr=lr, weight_decay=weight_decay)
+    losses, norms = [], []
+    for tok_last, groups, pos, neg in batches:
+        opt.zero_grad()
+        loss = _loss(P, tok_last, groups, pos, neg, 0.0, (0, 0, 0), ln_eps, margin, pooler)
+        loss.backward()
+        norms.append(float(torch.nn.utils.clip_grad_norm_(plist, max_norm=max_norm)))
+        opt.step()
+        losses.append(float(loss.detach()))
+    return losses, norms, {k: v.detach().clone() for k, v in P.items()}

@@ -82,7 +82,9 @@ def test_every_entry_with_pointers_is_covered():
     """The table below names every header entry that takes a device pointer."""
     no_ptr = {"nr_version", "nr_build_hash", "nr_init", "nr_last_error", "nr_set_persistent_workgroups",
               "nr_persistent_workgroups", "nr_final_attn_workspace_bytes", "nr_latent_workspace_bytes",
-              "nr_encoder_workspace_bytes", "nr_residency_flush", "nr_is_device_pointer"}
+              "nr_encoder_workspace_bytes", "nr_residency_flush", "nr_is_device_pointer",
+              # communicator handles (tests/test_comm.py)
+              "nr_rccl_version", "nr_comm_unique_id", "nr_comm_init", "nr_comm_destroy", "nr_allgather"}
     assert set(_calls(ctypes.c_void_p(256))) == set(_lib.SIGNATURES) - no_ptr
 
 

@@ -1,0 +1,145 @@
+"""Config 5 in bf16 (BASELINE configs[4]: "bf16 MFMA backward") held to the f32
+ORACLE over many steps, not to the HIP f32 path.
+
+Both config-5 engines (FinalAttentionTrainStep, LatentAttentionTrainStep) run
+22 bf16 steps -- two epochs of the reference trainer's golden batching
+(tests/golden/train_step.npz: FinalAttentionTrainDataset, batch 8, 11 batches)
+-- with ONE persistent AdamW, as train_one_epoch does (trainer.py:1030-1117).
+oracle/train_ref.train_steps runs the same 22 steps in f32 torch autograd on
+the CPU (FinalAttention: pinned to the reference's own step and epoch golden in
+test_train.py; latent: torch autograd of the reference module's forward,
+pool_ref.latent_attention_forward, pinned to the reference golden).
+
+Bounds, at the reference's lr = 1e-6 and at a 100x lr (1e-4)
+that makes the parameters actually move, so bf16 drift accumulates:
+  per-step loss    |l_bf16 - l_oracle| <= LOSS_REL * |l_oracle| at every step
+  update           per parameter tensor, d = p_22 - p_0 (the trained change):
+                   cos(d_bf16, d_oracle) >= UPD_COS and
+                   ||d_bf16 - d_oracle|| <= UPD_REL * ||d_oracle||
+  trained model    (lr 1e-6) eval AUC of the bf16-trained pooler (HIP eval
+                   path, bf16 and f32) vs the oracle-trained pooler (oracle eval)
+                   on 20,000 held-out impressions over 4,096 held-out news,
+                   clicks ~ logistic of the oracle score: equal to 4 decimal
+                   places (|dAUC| < 5e-5)
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from news_recommendation_project_v2_amd import weights as W
+
+STEPS_EPOCHS = 2
+LOSS_REL = {1e-6: 5e-3, 1e-4: 1e-2}
+UPD_COS = {1e-6: 0.95, 1e-4: 0.95}
+UPD_REL = {1e-6: 0.35, 1e-4: 0.35}
+AUC_4DP = 5e-5
+
+
+def _params(pooler):
+    tok = W.token_attn_state_dict(1234)
+    p = {"ln.weight": tok["encoder.layer.0.g_mlp_layernorm.weight"].clone(),
+         "ln.bias": tok["encoder.layer.0.g_mlp_layernorm.bias"].clone()}
+    if pooler == "final":
+        p.update({k: v.clone() for k, v in W.final_attention_state_dict(1234).items()})
+    else:
+        p.update({f"latent.{k}": v.clone() for k, v in W.latent_attention_state_dict(1234, ln_random=True).items()})
+    return p
+
+
+def _engine(pooler, dev, lr):
+    from news_recommendation_project_v2_amd.latent_attention import LatentAttentionModel
+    from news_recommendation_project_v2_amd.modeling_utils import FinalAttention, get_token_attn_model
+    from news_recommendation_project_v2_amd.train_step import FinalAttentionTrainStep, LatentAttentionTrainStep
+    tm = get_token_attn_model()
+    tm.load_state_dict(W.token_attn_state_dict(1234))
+    if pooler == "final":
+        fa = FinalAttention(1024, 4096)
+        fa.load_state_dict(W.final_attention_state_dict(1234))
+        return FinalAttentionTrainStep(tm, fa.to(dev), dtype=torch.bfloat16, lr=lr, dropout=0.0, device=dev)
+    lm = LatentAttentionModel()
+    lm.load_state_dict(W.latent_attention_state_dict(1234, ln_random=True))
+    return LatentAttentionTrainStep(tm, lm.to(dev).train(), dtype=torch.bfloat16, lr=lr, device=dev)
+
+
+def _cos(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a @ b) / (a.norm() * b.norm() + 1e-300))
+
+
+def _scores_gpu(pooler, sd, E, imps, dev, dtype):
+    from news_recommendation_project_v2_amd.engine import PoolScoreEngine
+    from news_recommendation_project_v2_amd.latent_attention import LatentAttentionModel
+    from news_recommendation_project_v2_amd.modeling_utils import FinalAttention
+    m = FinalAttention(1024, 4096) if pooler == "final" else LatentAttentionModel()
+    m.load_state_dict(sd)  # a fresh module: no cached fold of the pre-training weights
+    eng = PoolScoreEngine(m.to(dev).eval(), dtype=dtype, device=dev).load_news(E)
+    eng.load_impressions(imps.hist_idx, imps.hist_len, imps.cand_idx, imps.cand_len)
+    s, _ = eng.step()
+    return eng, s
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("lr", [1e-6, 1e-4])
+@pytest.mark.parametrize("pooler", ["final", "latent"])
+def test_bf16_training_tracks_f32_oracle(gpu_device, tmp_path, pooler, lr):
+    import torch.nn.functional as F
+    from test_train import _dataset, _device_batch, _oracle_batch, _setup
+    from news_recommendation_project_v2_amd import evaluation, synthetic
+    from oracle import data_ref, pool_ref, train_ref
+    torch.set_num_threads(min(16, os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS") or 16)))
+    g, states, labels = _setup()
+    ds = _dataset(g, labels)
+    ranges = ds.batches() * STEPS_EPOCHS
+    assert len(ranges) >= 20
+    dev_batches = {r: _device_batch(ds, states, r[0], r[1], gpu_device, tmp_path) for r in ds.batches()}
+    eng = _engine(pooler, gpu_device, lr)
+    p0 = {k: v.detach().cpu().clone() for k, v in eng.views.items()}
+    losses = [float(eng.step(dev_batches[r])) for r in ranges]
+    torch.cuda.synchronize()
+    p_gpu = {k: v.detach().cpu().clone() for k, v in eng.views.items()}
+
+    obatches = [_oracle_batch(ds, states, lo, hi)[:4] for lo, hi in ranges]
+    ref_losses, _, p_ref = train_ref.train_steps(_params(pooler), obatches, pooler=pooler, lr=lr)
+    assert set(p_ref) == set(p_gpu)
+
+    rel = [abs(a - b) / abs(b) for a, b in zip(losses, ref_losses)]
+    print(f"\n[bf16 drift] {pooler} lr={lr:g}: steps {len(losses)}, loss rel err max {max(rel):.2e} "
+          f"(first {rel[0]:.2e}, last {rel[-1]:.2e}); loss {ref_losses[0]:.5f} -> {ref_losses[-1]:.5f}")
+    assert max(rel) <= LOSS_REL[lr], (pooler, lr, rel)
+    worst_cos, worst_rel = 1.0, 0.0
+    for k in p_ref:
+        d_ref = p_ref[k] - p0[k]
+        d_gpu = p_gpu[k] - p0[k]
+        c = _cos(d_gpu, d_ref)
+        r = float((d_gpu - d_ref).double().norm() / (d_ref.double().norm() + 1e-300))
+        worst_cos, worst_rel = min(worst_cos, c), max(worst_rel, r)
+        assert c >= UPD_COS[lr] and r <= UPD_REL[lr], (pooler, lr, k, c, r)
+    print(f"[bf16 drift] {pooler} lr={lr:g}: update cosine min {worst_cos:.4f}, update rel err max {worst_rel:.3f}")
+    if lr != 1e-6:
+        return
+
+    # the trained poolers on held-out impressions, clicks ~ logistic of the oracle score
+    n_news, n_imp = 4096, 20000
+    tok = torch.stack([W.normal_tensor(97, f"heldout_tok_{i}", (1024,)) * 2.0 + 0.3 for i in range(n_news)]).half()
+    imps = synthetic.mind_impressions(n_news, n_imp, seed=21)
+    E_ref = F.layer_norm(tok.float(), (1024,), p_ref["ln.weight"], p_ref["ln.bias"], 1e-12)
+    strip = (lambda d: {k: v for k, v in d.items() if not k.startswith("ln.")}) if pooler == "final" else \
+        (lambda d: {k[7:]: v for k, v in d.items() if k.startswith("latent.")})
+    ref = pool_ref.cos_sim_scores_per_news(pooler, strip(p_ref), imps.hist_idx, imps.hist_len, imps.cand_idx,
+                                           imps.cand_len, E_ref).numpy()
+    lab = synthetic.logistic_labels(ref, imps.cand_len)
+    auc_ref = float(np.nanmean(data_ref.impression_aucs(ref, lab, imps.cand_len)))
+    from news_recommendation_project_v2_amd import ops
+    E_gpu = ops.gather_layernorm(tok.to(gpu_device), None, eng.views["ln.weight"].view(1, 1024),
+                                 eng.views["ln.bias"].view(1, 1024), 1e-12)
+    sd_gpu = {k: v.to(gpu_device) for k, v in strip(p_gpu).items()}
+    for dt in (torch.bfloat16, torch.float32):
+        e, s = _scores_gpu(pooler, sd_gpu, E_gpu, imps, gpu_device, dt)
+        auc = evaluation.score_device(e.rank(s), lab, imps.cand_off())["auc"]
+        print(f"[bf16 drift] {pooler}: held-out AUC oracle-trained (oracle eval) {auc_ref:.6f}, bf16-trained "
+              f"({'bf16' if dt == torch.bfloat16 else 'f32'} HIP eval) {auc:.6f}, |d| {abs(auc - auc_ref):.2e}")
+        assert auc_ref > 0.7
+        assert abs(auc - auc_ref) < AUC_4DP, (pooler, dt, auc, auc_ref)
