@@ -72,7 +72,7 @@ extern "C" {
 int nr_version(void);
 
 /* Hash of the sources the library was built from (16 hex digits: sha256 of
- * csrc/{capi,gemm,pool_score,rowops,rank,encoder,train,metrics,comm}.hip,
+ * csrc/{capi,gemm,pool_score,rowops,rank,encoder,train,metrics,comm,latent_train}.hip,
  * csrc/nr_common.h and this header, concatenated in that order); the Python
  * loader refuses a library whose hash differs from the tree it sits in. */
 const char* nr_build_hash(void);
@@ -446,6 +446,59 @@ int nr_sumsq(int64_t n, const float* x, float* out, void* stream);
 int nr_adamw(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf16, int64_t step, float lr,
              float beta1, float beta2, float eps, float weight_decay, float max_norm, const float* sumsq,
              void* stream);
+
+/*
+ * ---- Config-5 step with the latent pooler (BASELINE configs[4]: token encoder
+ * + LatentAttentionModel, bf16 MFMA backward), forward + backward of one batch
+ * as ONE call: the body of train_one_epoch (trainer.py:1044-1066) with
+ * LatentAttentionModel (latent_attention.py:134-171) in FinalAttention's slot.
+ *   E     = LN_tok(tok_last)                      (g_mlp_layernorm, eps 1e-12)
+ *   fold  KV = LN_c(latents) Wkv^T; A_h = K_h Wq_h / sqrt(512); Bt_h^T = V_h Wo_h^T
+ *   per history slot: X = LN_q(E[hist]); P = softmax64(X A^T); H1 = P Bt^T + E[hist]
+ *                     G = LN_f(H1) W1^T + b1; Z = GEGLU(G)
+ *   per batch row:    m = mean(Z) W2^T + b2 + mean(H1)   (= mean(H): the last
+ *                     linear layer commutes with the history mean)
+ *                     u = normalize(m); loss = MarginRankingLoss(2)(cos(u, E[pos]), cos(u, E[neg]))
+ * and the exact backward of all of it; gradients are written into the f32
+ * grad buffers (caller-zeroed: some are accumulated with atomics).  dtype
+ * NR_F32: exact-f32 MFMA GEMMs and f32 activations; NR_BF16: bf16 operands and
+ * activations, f32 accumulation, statistics and parameter gradients.
+ * Weights are passed in `dtype` (the bf16 mirror for NR_BF16), LayerNorm
+ * parameters, biases and latents in f32.  hist_idx: [Hs] indices into the U
+ * rows, hist_off [B+1] CSR offsets, pos / neg [B].  users (nullable, f32
+ * [B][1024]): the normalized pooled users.  ws: nr_latent_train_workspace_bytes.
+ */
+typedef struct nr_latent_train_args {
+  int dtype;
+  int tok_dtype;  /* NR_F32 / NR_BF16 / NR_F16 */
+  int64_t B, U, Hs;
+  const void* tok_last; /* [U][1024] last valid token state per unique news */
+  const int32_t* hist_idx;
+  const int64_t* hist_off;
+  const int32_t* pos;
+  const int32_t* neg;
+  float margin;
+  /* parameters (f32 unless noted) */
+  const float *tok_g, *tok_b; /* token LayerNorm (g_mlp_layernorm) */
+  const float* latents;       /* [64][1024] */
+  const float *nq_g, *nq_b;   /* cross_attend_blocks.0.norm */
+  const float *nc_g, *nc_b;   /* cross_attend_blocks.0.norm_context */
+  const void *Wq, *Wkv, *Wo;  /* `dtype`: to_q [4096][1024], to_kv [8192][1024], to_out [1024][4096] */
+  const float *nf_g, *nf_b;   /* cross_attend_blocks.1.norm */
+  const void* W1;             /* `dtype`: net.0.weight [8192][1024] */
+  const float* b1;            /* [8192] */
+  const void* W2;             /* `dtype`: net.2.weight [1024][4096] */
+  const float* b2;            /* [1024] */
+  /* gradients (f32, same shapes, caller-zeroed) */
+  float *g_tok_g, *g_tok_b, *g_latents, *g_nq_g, *g_nq_b, *g_nc_g, *g_nc_b, *g_Wq, *g_Wkv, *g_Wo;
+  float *g_nf_g, *g_nf_b, *g_W1, *g_b1, *g_W2, *g_b2;
+  /* outputs */
+  float* loss;  /* device scalar (set, not accumulated) */
+  float* users; /* nullable [B][1024] */
+} nr_latent_train_args;
+
+int64_t nr_latent_train_workspace_bytes(int dtype, int64_t B, int64_t U, int64_t Hs);
+int nr_latent_train_step(const nr_latent_train_args* args, void* ws, int64_t ws_bytes, void* stream);
 
 /*
  * ---- RCCL communicator of the multi-GPU eval (SURVEY §8(b) nr_allgather,

@@ -18,7 +18,7 @@ CSRC = Path(__file__).resolve().with_name("csrc")
 INCLUDE = Path(__file__).resolve().parent.parent / "include"
 # translation units of libnewsrec_hip.so, in link order (also the hash order)
 HIP_SOURCES = ("capi.hip", "gemm.hip", "pool_score.hip", "rowops.hip", "rank.hip", "encoder.hip", "train.hip",
-               "metrics.hip", "comm.hip")
+               "metrics.hip", "comm.hip", "latent_train.hip")
 
 
 def hip_source_files() -> list:
@@ -77,6 +77,8 @@ SIGNATURES = {
     "nr_last_error": (ctypes.c_char_p, []),
     "nr_residency_flush": (_i, []),
     "nr_rccl_version": (_i, []),
+    "nr_latent_train_workspace_bytes": (_l, [_i, _l, _l, _l]),
+    "nr_latent_train_step": (_i, [_p, _p, _l, _p]),
     "nr_comm_unique_id": (_i, [_p]),
     "nr_comm_init": (_i, [_p, _p, _i, _i]),
     "nr_comm_destroy": (_i, [_p]),
@@ -129,6 +131,21 @@ class EncoderLayer(ctypes.Structure):
     """struct nr_encoder_layer (include/newsrec.h): device pointers of one layer."""
     _fields_ = [(n, ctypes.c_void_p) for n in ("wqkv", "bqkv", "wo", "bo", "ln1_g", "ln1_b", "w1", "b1", "w2", "b2",
                                              "ln2_g", "ln2_b")]
+
+
+LATENT_TRAIN_PARAMS = ("tok_g", "tok_b", "latents", "nq_g", "nq_b", "nc_g", "nc_b", "Wq", "Wkv", "Wo", "nf_g", "nf_b",
+                       "W1", "b1", "W2", "b2")
+LATENT_TRAIN_GRADS = ("g_tok_g", "g_tok_b", "g_latents", "g_nq_g", "g_nq_b", "g_nc_g", "g_nc_b", "g_Wq", "g_Wkv",
+                      "g_Wo", "g_nf_g", "g_nf_b", "g_W1", "g_b1", "g_W2", "g_b2")
+
+
+class LatentTrainArgs(ctypes.Structure):
+    """struct nr_latent_train_args (include/newsrec.h)."""
+    _fields_ = ([("dtype", ctypes.c_int), ("tok_dtype", ctypes.c_int), ("B", ctypes.c_int64), ("U", ctypes.c_int64),
+                 ("Hs", ctypes.c_int64)]
+                + [(n, ctypes.c_void_p) for n in ("tok_last", "hist_idx", "hist_off", "pos", "neg")]
+                + [("margin", ctypes.c_float)]
+                + [(n, ctypes.c_void_p) for n in LATENT_TRAIN_PARAMS + LATENT_TRAIN_GRADS + ("loss", "users")])
 
 
 class NewsRecHIPError(RuntimeError):

@@ -363,6 +363,7 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) {
               float v = acc[mi][ni][r] + b16[ni];
+              if constexpr (EPI == NR_EPI_NONE) v *= ea.scale;
               if constexpr (EPI == NR_EPI_RELU) v = fmaxf(v, 0.f);
               if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
                 const uint64_t gi = (uint64_t)((m0 + wm * 128 + pass * 64 + lr) * N + wcol + 16 * ni + c16);
@@ -386,6 +387,7 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
           slab[lr * COLS + cl] = (acc[mi][0][reg] + ba) * gelu_erf(acc[mi][1][reg] + bg);
         } else {
           float v0 = acc[mi][0][reg] + ba, v1 = acc[mi][1][reg] + bg;
+          if constexpr (EPI == NR_EPI_NONE) { v0 *= ea.scale; v1 *= ea.scale; }
           if constexpr (EPI == NR_EPI_RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
           if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
             const uint64_t gi = (uint64_t)((m0 + wm * 128 + pass * 64 + lr) * N + wcol + cl);
@@ -700,21 +702,27 @@ __global__ __launch_bounds__(512, 2) void gemm256p_kernel(int64_t M, int64_t N, 
                                    ldw, bias, R, ldr, C, ldc, ea);
 }
 
-// Grouped launch of up to NR_GEMM_MAX_GROUP independent problems with one
-// dtype / epilogue (no bias, no residual): one grid over all problems' tiles,
-// so small problems (the config-5 weight-grad GEMMs, 64 tiles each) fill the
-// 256 CUs together instead of one after another.  tile_end[p] = prefix sum of
-// the problems' tile counts; tiles are remapped XCD-aware over the whole grid,
-// so one problem's N tiles of an A panel stay on one XCD.
+// Grouped launch of up to kGroupMax independent problems with one dtype pair
+// and no bias / residual: one grid over all problems' tiles, so small
+// problems (the config-5 weight-grad GEMMs, 64 tiles each) fill the 256 CUs
+// together instead of one after another.  A problem may be a strided batch
+// (`batch` instances at A + b sA, W + b sW, C + b sC: the 8 heads of the latent
+// K/V fold, or the K-slices of a split-K GEMM) and carries a scale alpha
+// (C = alpha A W^T).  tile_end[p] = prefix sum of the problems' tile counts
+// (tiles x batch); tiles are remapped XCD-aware over the whole grid, so one
+// problem's N tiles of an A panel stay on one XCD.
 struct GemmGroup {
   int n;
-  int tile_end[NR_GEMM_MAX_GROUP];
-  int ntn[NR_GEMM_MAX_GROUP];
-  int64_t M[NR_GEMM_MAX_GROUP], N[NR_GEMM_MAX_GROUP], K[NR_GEMM_MAX_GROUP];
-  const void* A[NR_GEMM_MAX_GROUP];
-  const void* W[NR_GEMM_MAX_GROUP];
-  void* C[NR_GEMM_MAX_GROUP];
-  int64_t lda[NR_GEMM_MAX_GROUP], ldw[NR_GEMM_MAX_GROUP], ldc[NR_GEMM_MAX_GROUP];
+  int tile_end[kGroupMax];
+  int ntn[kGroupMax];
+  int tpb[kGroupMax];  // tiles per batch instance
+  float alpha[kGroupMax];
+  int64_t M[kGroupMax], N[kGroupMax], K[kGroupMax];
+  const void* A[kGroupMax];
+  const void* W[kGroupMax];
+  void* C[kGroupMax];
+  int64_t lda[kGroupMax], ldw[kGroupMax], ldc[kGroupMax];
+  int64_t sA[kGroupMax], sW[kGroupMax], sC[kGroupMax];
 };
 
 template <typename TI, typename TO, bool MF16>
@@ -724,10 +732,59 @@ __global__ __launch_bounds__(512, 2) void gemm256p_group_kernel(GemmGroup g) {
   int p = 0;
   while (p + 1 < g.n && t >= g.tile_end[p]) ++p;
   const int local = t - (p ? g.tile_end[p - 1] : 0);
+  const int b = local / g.tpb[p], lt = local - b * g.tpb[p];
   const int nx = g.ntn[p];
-  gemm256p_body<TI, NR_EPI_NONE, TO, MF16>(smem, (int64_t)(local / nx) * G2BM, (int64_t)(local % nx) * G2BN, g.M[p],
-                                           g.N[p], g.K[p], (const TI*)g.A[p], g.lda[p], (const TI*)g.W[p], g.ldw[p],
-                                           nullptr, nullptr, 0, (TO*)g.C[p], g.ldc[p], EpiArgs{0, 0, 1.f});
+  gemm256p_body<TI, NR_EPI_NONE, TO, MF16>(smem, (int64_t)(lt / nx) * G2BM, (int64_t)(lt % nx) * G2BN, g.M[p],
+                                           g.N[p], g.K[p], (const TI*)g.A[p] + b * g.sA[p], g.lda[p],
+                                           (const TI*)g.W[p] + b * g.sW[p], g.ldw[p], nullptr, nullptr, 0,
+                                           (TO*)g.C[p] + b * g.sC[p], g.ldc[p], EpiArgs{0, 0, g.alpha[p]});
+}
+
+int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, int n, hipStream_t s) {
+  NR_CHECK_ARG(dtype_in == NR_BF16 || dtype_in == NR_F32, "gemm_group: bad dtype_in %d", dtype_in);
+  NR_CHECK_ARG(dtype_out == NR_F32 || dtype_out == NR_BF16, "gemm_group: bad dtype_out %d", dtype_out);
+  NR_CHECK_ARG(n >= 0 && n <= kGroupMax, "gemm_group: n=%d outside [0, %d]", n, kGroupMax);
+  GemmGroup g{};
+  g.n = 0;
+  int64_t tiles = 0;
+  const int64_t bk = dtype_in == NR_F32 ? 32 : 64, e16 = dtype_in == NR_F32 ? 4 : 8;
+  const int64_t vo = dtype_out == NR_F32 ? 4 : 8;
+  for (int i = 0; i < n; ++i) {
+    const GemmProblem& q = probs[i];
+    NR_CHECK_ARG(q.M >= 0 && q.N > 0 && q.K > 0 && q.N % G2BN == 0 && q.K % bk == 0 && q.batch >= 0,
+                 "gemm_group: problem %d bad shape M=%lld N=%lld K=%lld (need N %% 256, K %% 64 bf16 / 32 f32)", i,
+                 (long long)q.M, (long long)q.N, (long long)q.K);
+    if (q.M == 0 || q.batch == 0) continue;
+    NR_CHECK_ARG(q.A && q.W && q.C, "gemm_group: problem %d null operand", i);
+    NR_CHECK_ARG(q.lda >= q.K && q.ldw >= q.K && q.lda % e16 == 0 && q.ldw % e16 == 0 && q.ldc >= q.N &&
+                     q.ldc % vo == 0 && ((uintptr_t)q.A & 15) == 0 && ((uintptr_t)q.W & 15) == 0 &&
+                     ((uintptr_t)q.C & 15) == 0 && q.sA % e16 == 0 && q.sW % e16 == 0 && q.sC % vo == 0,
+                 "gemm_group: problem %d operands must be 16-byte aligned with 16-byte row / batch strides", i);
+    const int j = g.n++;
+    g.M[j] = q.M; g.N[j] = q.N; g.K[j] = q.K;
+    g.A[j] = q.A; g.W[j] = q.W; g.C[j] = q.C;
+    g.lda[j] = q.lda; g.ldw[j] = q.ldw; g.ldc[j] = q.ldc;
+    g.sA[j] = q.sA; g.sW[j] = q.sW; g.sC[j] = q.sC;
+    g.alpha[j] = q.alpha;
+    g.ntn[j] = (int)(q.N / G2BN);
+    const int64_t tpb = ((q.M + G2BM - 1) / G2BM) * g.ntn[j];
+    NR_CHECK_ARG(tpb <= 0x7fffffff, "gemm_group: too many tiles");
+    g.tpb[j] = (int)tpb;
+    tiles += tpb * q.batch;
+    NR_CHECK_ARG(tiles <= 0x7fffffff, "gemm_group: too many tiles");
+    g.tile_end[j] = (int)tiles;
+  }
+  if (g.n == 0) return NR_OK;
+  if (dtype_in == NR_F32 && dtype_out == NR_F32)
+    hipLaunchKernelGGL((gemm256p_group_kernel<float, float, false>), dim3((unsigned)tiles), dim3(512), 0, s, g);
+  else if (dtype_in == NR_F32)
+    hipLaunchKernelGGL((gemm256p_group_kernel<float, __bf16, false>), dim3((unsigned)tiles), dim3(512), 0, s, g);
+  else if (dtype_out == NR_F32)
+    hipLaunchKernelGGL((gemm256p_group_kernel<__bf16, float, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm256p_group_kernel<__bf16, __bf16, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);
+  NR_CHECK_LAUNCH("gemm_group");
+  return NR_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -1503,46 +1560,12 @@ extern "C" int nr_gemm_grouped(int dtype_in, int dtype_out, int n, const int64_t
                                const int64_t* K, const void* const* A, const int64_t* lda, const void* const* W,
                                const int64_t* ldw, void* const* C, const int64_t* ldc, void* stream) {
   nr::clear_error();
-  NR_CHECK_ARG(dtype_in == NR_BF16 || dtype_in == NR_F32, "nr_gemm_grouped: bad dtype_in %d", dtype_in);
-  NR_CHECK_ARG(dtype_out == NR_F32 || dtype_out == NR_BF16, "nr_gemm_grouped: bad dtype_out %d", dtype_out);
   NR_CHECK_ARG(n >= 1 && n <= NR_GEMM_MAX_GROUP, "nr_gemm_grouped: n=%d outside [1, %d]", n, NR_GEMM_MAX_GROUP);
   NR_CHECK_ARG(M && N && K && A && lda && W && ldw && C && ldc, "nr_gemm_grouped: null array");
-  nr::GemmGroup g{};
-  g.n = 0;
-  int64_t tiles = 0;
-  const int64_t vo = dtype_out == NR_F32 ? 4 : 8;
+  nr::GemmProblem p[NR_GEMM_MAX_GROUP];
   for (int i = 0; i < n; ++i) {
-    const int64_t bk = dtype_in == NR_F32 ? 32 : 64, e16 = dtype_in == NR_F32 ? 4 : 8;
-    NR_CHECK_ARG(M[i] >= 0 && N[i] > 0 && K[i] > 0 && N[i] % nr::G2BN == 0 && K[i] % bk == 0,
-                 "nr_gemm_grouped: problem %d bad shape M=%lld N=%lld K=%lld (need N %% 256, K %% 64 bf16 / 32 f32)", i,
-                 (long long)M[i], (long long)N[i], (long long)K[i]);
-    if (M[i] == 0) continue;  // empty problem: no operand is read (torch gives a null data pointer)
-    NR_CHECK_ARG(A[i] && W[i] && C[i], "nr_gemm_grouped: problem %d null operand", i);
-    NR_CHECK_DEVICE("nr_gemm_grouped", A[i], W[i], C[i]);
-    NR_CHECK_ARG(lda[i] >= K[i] && ldw[i] >= K[i] && lda[i] % e16 == 0 && ldw[i] % e16 == 0 && ldc[i] >= N[i] &&
-                     ldc[i] % vo == 0 && ((uintptr_t)A[i] & 15) == 0 && ((uintptr_t)W[i] & 15) == 0 &&
-                     ((uintptr_t)C[i] & 15) == 0,
-                 "nr_gemm_grouped: problem %d operands must be 16-byte aligned with 16-byte row strides", i);
-    const int j = g.n++;
-    g.M[j] = M[i]; g.N[j] = N[i]; g.K[j] = K[i];
-    g.A[j] = A[i]; g.W[j] = W[i]; g.C[j] = C[i];
-    g.lda[j] = lda[i]; g.ldw[j] = ldw[i]; g.ldc[j] = ldc[i];
-    g.ntn[j] = (int)(N[i] / nr::G2BN);
-    tiles += ((M[i] + nr::G2BM - 1) / nr::G2BM) * g.ntn[j];
-    NR_CHECK_ARG(tiles <= 0x7fffffff, "nr_gemm_grouped: too many tiles");
-    g.tile_end[j] = (int)tiles;
+    if (M[i] > 0) NR_CHECK_DEVICE("nr_gemm_grouped", A[i], W[i], C[i]);
+    p[i] = nr::GemmProblem{M[i], N[i], K[i], A[i], lda[i], 0, W[i], ldw[i], 0, C[i], ldc[i], 0, 1, 1.0f};
   }
-  if (g.n == 0) return NR_OK;
-  hipStream_t s = (hipStream_t)stream;
-  if (dtype_in == NR_F32 && dtype_out == NR_F32)
-    hipLaunchKernelGGL((nr::gemm256p_group_kernel<float, float, false>), dim3((unsigned)tiles), dim3(512), 0, s, g);
-  else if (dtype_in == NR_F32)
-    hipLaunchKernelGGL((nr::gemm256p_group_kernel<float, __bf16, false>), dim3((unsigned)tiles), dim3(512), 0, s, g);
-  else if (dtype_out == NR_F32)
-    hipLaunchKernelGGL((nr::gemm256p_group_kernel<__bf16, float, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);
-  else
-    hipLaunchKernelGGL((nr::gemm256p_group_kernel<__bf16, __bf16, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);
-  NR_CHECK_LAUNCH("nr_gemm_grouped");
-  return NR_OK;
+  return nr::gemm_group_dispatch(dtype_in, dtype_out, p, n, (hipStream_t)stream);
 }
-

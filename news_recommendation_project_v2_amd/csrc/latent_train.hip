@@ -1,0 +1,909 @@
+// Config-5 training step with the latent pooler (BASELINE configs[4]: "bf16
+// MFMA backward for encoder + latent attention"), forward and backward of one
+// batch as one C call (nr_latent_train_step, include/newsrec.h).  The math is
+// the reference trainer's loop body (trainer.py:1044-1066) with
+// LatentAttentionModel (latent_attention.py:134-171) in FinalAttention's slot:
+//
+//   E  = g_mlp_LN(last token)                        token model (attention.py:193)
+//   fold (weights only, once per step; the reference rebuilds K/V per batch row,
+//   latent_attention.py:161-162):
+//        KV = LN_c(latents) Wkv^T;  A_h = K_h Wq_h / sqrt(512);  BtT_h = V_h Wo_h^T
+//   per history slot (packed valid rows, CSR order, zero rows up to Hp = pad64(Hs)):
+//        S = E[hist];  X = LN_q(S);  P = softmax64(X A^T);  H1 = P Bt^T + S
+//        G = LN_f(H1) W1^T + b1;  Z = a * gelu(g), (a, g) = G.chunk(2)
+//   per batch row b (h_b slots):
+//        m_b = mean(Z) W2^T + b2 + mean(H1)  ==  mean(Z W2^T + b2 + H1) = mean(H)
+//        u_b = normalize(m_b);  loss = mean(max(0, 2 - cos(u, E[pos]) + cos(u, E[neg])))
+// The last linear layer commutes with the history mean, so its forward GEMM,
+// its data-grad GEMM and its weight-grad GEMM run over B rows instead of Hs
+// slots (exact up to f32 summation order; the reference computes H per padded
+// slot).  Backward:
+//   dm (normalize backward) -> dZ_b = (dm_b / h_b) W2 (per row, broadcast to its
+//   slots) -> dG = GEGLU' -> dY = dG W1 -> dH1 = LN_f'(dY) + dm_b / h_b ->
+//   dP = dH1 Bt -> dS = softmax64'(P, dP) -> dX = dS A -> dE[hist] += LN_q'(dX) + dH1
+//   weight grads: W1 = dG^T Y, W2 = dm^T mean(Z), A = dS^T X, Bt = dH1^T P (one
+//   grouped launch), then the fold backward (Wq, Wkv, Wo, latents, norm_context)
+//   as two grouped launches of the 8 heads, and the LN parameter grads.
+// GEMMs: nr's MFMA kernels (gemm.hip: persistent bf16, grouped strided batches);
+// everything else here is HBM-bound row work (one wave per row, 16-B lanes).
+#include "nr_common.h"
+
+namespace nr {
+namespace lt {
+
+constexpr int D = 1024, F = 4096, S = 512, NL = 64, HEADS = 8, DH = 512;
+
+template <typename T>
+__device__ __forceinline__ void ld4(const T* p, float v[4]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    v[0] = bf16_lo(u.x); v[1] = bf16_hi(u.x); v[2] = bf16_lo(u.y); v[3] = bf16_hi(u.y);
+  }
+}
+
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{a, b}, b2));
+}
+
+template <typename T>
+__device__ __forceinline__ void st4(T* p, const float v[4]) {
+  if constexpr (sizeof(T) == 4) *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
+  else *reinterpret_cast<uint2*>(p) = uint2{pk2(v[0], v[1]), pk2(v[2], v[3])};
+}
+
+template <typename T>
+__device__ __forceinline__ void st4z(T* p) {
+  const float z[4] = {0.f, 0.f, 0.f, 0.f};
+  st4<T>(p, z);
+}
+
+__device__ __forceinline__ float gelu_x(float g) { return 0.5f * g * (1.0f + erff(g * 0.70710678118654752440f)); }
+
+// ------------------------------------------------------------------ forward rows
+// S = E[idx[row]], X = LN_q(S) (eps 1e-5); idx < 0 (padding): both rows zero.
+// One wave per row, lane columns 256 j + 4 lane .. +3.
+template <typename TA>
+__global__ __launch_bounds__(256) void gather_ln_kernel(int64_t n, int64_t nvalid, const float* __restrict__ E, int64_t lde,
+                                                        const int32_t* __restrict__ idx, const float* __restrict__ g,
+                                                        const float* __restrict__ b, float eps, TA* __restrict__ Sx,
+                                                        TA* __restrict__ X) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (int64_t)gridDim.x * 4) {
+    const int32_t r = row < nvalid ? idx[row] : -1;
+    if (r < 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        st4z<TA>(Sx + row * D + j * 256 + lane * 4);
+        st4z<TA>(X + row * D + j * 256 + lane * 4);
+      }
+      continue;
+    }
+    float v[4][4];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ld4<float>(E + (int64_t)r * lde + j * 256 + lane * 4, v[j]);
+      s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+    }
+    const float mean = wave_sum(s) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { const float d = v[j][t] - mean; q = fmaf(d, d, q); }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = j * 256 + lane * 4;
+      float o[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t] = (v[j][t] - mean) * rstd * g[c + t] + b[c + t];
+      st4<TA>(Sx + row * D + c, v[j]);
+      st4<TA>(X + row * D + c, o);
+    }
+  }
+}
+
+// Z = a * gelu(g), (a | g) = the two halves of G's 2F columns (GEGLU,
+// latent_attention.py:24-27, exact erf).  4 columns per thread.
+template <typename TA>
+__global__ __launch_bounds__(256) void geglu_fwd_kernel(int64_t rows, const TA* __restrict__ G, TA* __restrict__ Z) {
+  const int64_t total = rows * (F / 4);
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+    const int64_t r = q / (F / 4), c = (q % (F / 4)) * 4;
+    float a[4], g[4], o[4];
+    ld4<TA>(G + r * 2 * F + c, a);
+    ld4<TA>(G + r * 2 * F + F + c, g);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[t] = a[t] * gelu_x(g[t]);
+    st4<TA>(Z + r * F + c, o);
+  }
+}
+
+// Per batch row b: zbar_b = mean of Z over its slots (TA, the m GEMM's A
+// operand), h1bar_b = mean of H1 (f32), and row_seg[slot] = b.  Block =
+// (row b, 512-column chunk: chunks 0..7 of Z, 8..9 of H1); the 4 waves stride
+// the segment's rows, 8 columns per lane, fixed-order LDS fold.  Rows b in
+// [B, Bp) of zbar are zero; the last block marks the padding slots -1.
+template <typename TA>
+__global__ __launch_bounds__(256) void segmean_kernel(int64_t B, int64_t Bp, const int64_t* __restrict__ off,
+                                                      int64_t n_rows, const TA* __restrict__ Z,
+                                                      const TA* __restrict__ H1, TA* __restrict__ zbar,
+                                                      float* __restrict__ h1bar, int32_t* __restrict__ row_seg) {
+  __shared__ float part[4][512];
+  const int64_t b = blockIdx.x;
+  const int y = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (b >= Bp) {  // the padding slots
+    if (y == 0)
+      for (int64_t r = off[B] + threadIdx.x; r < n_rows; r += 256) row_seg[r] = -1;
+    return;
+  }
+  const bool zpart = y < 8;
+  const int64_t ld = zpart ? F : D;
+  const int c0 = (zpart ? y : y - 8) * 512 + lane * 8;
+  if (b >= B) {
+    if (zpart && wave == 0) {
+      st4z<TA>(zbar + b * F + c0);
+      st4z<TA>(zbar + b * F + c0 + 4);
+    }
+    return;
+  }
+  const int64_t r0 = off[b], r1 = off[b + 1];
+  if (y == 0)
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) row_seg[r] = (int32_t)b;
+  const TA* src = zpart ? Z : H1;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t r = r0 + wave; r < r1; r += 4) {
+    float v[4], w[4];
+    ld4<TA>(src + r * ld + c0, v);
+    ld4<TA>(src + r * ld + c0 + 4, w);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { acc[t] += v[t]; acc[4 + t] += w[t]; }
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) part[wave][lane * 8 + t] = acc[t];
+  __syncthreads();
+  if (wave != 0) return;
+  const float inv = 1.0f / (float)(r1 - r0);  // an empty row gives NaN, as the reference's s / d
+  float o[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int c = lane * 8 + t;
+    o[t] = ((part[0][c] + part[1][c]) + (part[2][c] + part[3][c])) * inv;
+  }
+  if (zpart) {
+    st4<TA>(zbar + b * F + c0, o);
+    st4<TA>(zbar + b * F + c0 + 4, o + 4);
+  } else {
+    st4<float>(h1bar + b * D + c0, o);
+    st4<float>(h1bar + b * D + c0 + 4, o + 4);
+  }
+}
+
+// Per batch row (one wave): m = sum_s parts[s][b] + b2 + h1bar[b];
+// u = m / max(|m|, 1e-12) (F.normalize, latent_attention.py:170);
+// F.cosine_similarity(u, E[pos]) / (u, E[neg]) with the per-vector 1e-8 clamp,
+// MarginRankingLoss(margin) mean over B (trainer.py:1058-1066); backward:
+// du as nr_cosine_margin, dm = (du - u (u . du)) / |m| (normalize backward;
+// du / 1e-12 below the clamp).  Writes users = u, dmA = dm, dmc = dm / h_b
+// (rows b in [B, Bp): zero), gb2 += dm, dE[pos / neg] += their cosine grads.
+template <typename TA>
+__global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int nparts, const float* __restrict__ parts,
+                                                   const float* __restrict__ b2, const float* __restrict__ h1bar,
+                                                   const int64_t* __restrict__ off, const float* __restrict__ E,
+                                                   int64_t lde, const int32_t* __restrict__ pos,
+                                                   const int32_t* __restrict__ neg, float margin,
+                                                   float* __restrict__ loss, float* __restrict__ users,
+                                                   TA* __restrict__ dmA, TA* __restrict__ dmc, float* __restrict__ dE,
+                                                   float* __restrict__ gb2) {
+  constexpr float EPS = 1e-8f, NEPS = 1e-12f;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= Bp) return;
+  if (b >= B) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      st4z<TA>(dmA + b * D + j * 256 + lane * 4);
+      st4z<TA>(dmc + b * D + j * 256 + lane * 4);
+    }
+    return;
+  }
+  float m[4][4], ep[4][4], en[4][4];
+  float mm = 0.f;
+  const float* pr = E + (int64_t)pos[b] * lde;
+  const float* nr_ = E + (int64_t)neg[b] * lde;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = j * 256 + lane * 4;
+    float t4[4];
+    ld4<float>(h1bar + b * D + c, m[j]);
+    ld4<float>(b2 + c, t4);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) m[j][t] += t4[t];
+    for (int s = 0; s < nparts; ++s) {
+      ld4<float>(parts + ((int64_t)s * Bp + b) * D + c, t4);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) m[j][t] += t4[t];
+    }
+    ld4<float>(pr + c, ep[j]);
+    ld4<float>(nr_ + c, en[j]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) mm = fmaf(m[j][t], m[j][t], mm);
+  }
+  const float nm = sqrtf(wave_sum(mm));
+  const float den = fmaxf(nm, NEPS);
+  float uu = 0.f, pp = 0.f, nn = 0.f, up = 0.f, un = 0.f;
+  float u[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      u[j][t] = m[j][t] / den;
+      uu = fmaf(u[j][t], u[j][t], uu);
+      pp = fmaf(ep[j][t], ep[j][t], pp);
+      nn = fmaf(en[j][t], en[j][t], nn);
+      up = fmaf(u[j][t], ep[j][t], up);
+      un = fmaf(u[j][t], en[j][t], un);
+    }
+  uu = wave_sum(uu); pp = wave_sum(pp); nn = wave_sum(nn); up = wave_sum(up); un = wave_sum(un);
+  const float nu = sqrtf(uu), np_ = sqrtf(pp), nq = sqrtf(nn);
+  const float iu = 1.0f / fmaxf(nu, EPS), ip = 1.0f / fmaxf(np_, EPS), iq = 1.0f / fmaxf(nq, EPS);
+  const float sp = up * iu * ip, sn = un * iu * iq;
+  const float v = margin - (sp - sn);
+  const float act = v >= 0.f ? 1.0f : 0.0f;
+  const float gsp = -act / (float)B, gsn = act / (float)B;
+  if (lane == 0) atomicAdd(loss, fmaxf(v, 0.f) / (float)B);
+  const float cu = nu > EPS ? 1.f : 0.f, cp = np_ > EPS ? 1.f : 0.f, cq = nq > EPS ? 1.f : 0.f;
+  float* dp = dE + (int64_t)pos[b] * lde;
+  float* dn = dE + (int64_t)neg[b] * lde;
+  float g[4][4];
+  float ug = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = j * 256 + lane * 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float uh = u[j][t] * iu, ph = ep[j][t] * ip, qh = en[j][t] * iq;
+      g[j][t] = gsp * (ph - cu * sp * uh) * iu + gsn * (qh - cu * sn * uh) * iu;
+      ug = fmaf(u[j][t], g[j][t], ug);
+      atomicAdd(dp + c + t, gsp * (uh - cp * sp * ph) * ip);
+      atomicAdd(dn + c + t, gsn * (uh - cq * sn * qh) * iq);
+    }
+  }
+  ug = wave_sum(ug);
+  const float icnt = 1.0f / (float)(off[b + 1] - off[b]);
+  const bool live = nm > NEPS;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = j * 256 + lane * 4;
+    float dm[4], dc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      dm[t] = (live ? g[j][t] - u[j][t] * ug : g[j][t]) / den;
+      dc[t] = dm[t] * icnt;
+      atomicAdd(gb2 + c + t, dm[t]);
+    }
+    if (users) st4<float>(users + b * D + c, u[j]);
+    st4<TA>(dmA + b * D + c, dm);
+    st4<TA>(dmc + b * D + c, dc);
+  }
+}
+
+// ------------------------------------------------------------------ backward rows
+// dG = (dz gelu(g), dz a gelu'(g)) with dz = dZseg[row_seg[row]] (the per-row
+// dZ of the mean trick, f32), padding slots zero; gb1 += column sums (one
+// atomic per column per block).  Block = (rows_per_block rows, 1024 a-columns),
+// 4 columns per thread.
+template <typename TA>
+__global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t rows, int rpb, const TA* __restrict__ G,
+                                                        const float* __restrict__ dZ, const int32_t* __restrict__ row_seg,
+                                                        TA* __restrict__ dG, float* __restrict__ gb1) {
+  const int c = (int)blockIdx.y * 1024 + threadIdx.x * 4;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
+  float sa[4] = {0.f, 0.f, 0.f, 0.f}, sg[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t r = r0; r < r1; ++r) {
+    const int32_t s = row_seg[r];
+    if (s < 0) {
+      st4z<TA>(dG + r * 2 * F + c);
+      st4z<TA>(dG + r * 2 * F + F + c);
+      continue;
+    }
+    float a[4], g[4], d[4], da[4], dg[4];
+    ld4<TA>(G + r * 2 * F + c, a);
+    ld4<TA>(G + r * 2 * F + F + c, g);
+    ld4<float>(dZ + (int64_t)s * F + c, d);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float cdf = 0.5f * (1.0f + erff(g[t] * 0.70710678118654752440f));
+      const float pdf = 0.39894228040143267794f * expf(-0.5f * g[t] * g[t]);
+      da[t] = d[t] * g[t] * cdf;
+      dg[t] = d[t] * a[t] * (cdf + g[t] * pdf);
+      sa[t] += da[t];
+      sg[t] += dg[t];
+    }
+    st4<TA>(dG + r * 2 * F + c, da);
+    st4<TA>(dG + r * 2 * F + F + c, dg);
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    atomicAdd(gb1 + c + t, sa[t]);
+    atomicAdd(gb1 + F + c + t, sg[t]);
+  }
+}
+
+// LayerNorm input gradient (stats recomputed from x with the forward's
+// arithmetic) plus a residual gradient, and the LN parameter grads:
+//   dx = rstd (dxh - mean(dxh) - xhat mean(dxh xhat)) + res,  dxh = dy gamma
+//   dgamma += dy xhat, dbeta += dy (per-lane registers, one atomic per column per block)
+// MODE 0 (LN_f of H1): res = dmc[row_seg[row]] (the broadcast dH of the mean),
+//   dx -> out rows (TA); padding slots (row_seg < 0) -> zero rows.
+// MODE 1 (LN_q of S):  res = dH1 row (TA); dx scattered into dE[idx[row]]
+//   (f32 atomics: the gradient of the history gather), idx < 0 skipped.
+template <typename TA, int MODE>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, const TA* __restrict__ x, const float* __restrict__ gamma,
+                                                     float eps, const TA* __restrict__ dy, const TA* __restrict__ res,
+                                                     const int32_t* __restrict__ sel, TA* __restrict__ out,
+                                                     float* __restrict__ dE, int64_t lde, float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta) {
+  __shared__ float sg[4][D], sb[4][D];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float ag[4][4], ab[4][4], gm[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    ld4<float>(gamma + j * 256 + lane * 4, gm[j]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { ag[j][t] = 0.f; ab[j][t] = 0.f; }
+  }
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < n; row += (int64_t)gridDim.x * 4) {
+    const int32_t s = row < nvalid ? sel[row] : -1;
+    if (s < 0) {
+      if constexpr (MODE == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) st4z<TA>(out + row * D + j * 256 + lane * 4);
+      }
+      continue;
+    }
+    float v[4][4], g[4][4];
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ld4<TA>(x + row * D + j * 256 + lane * 4, v[j]);
+      sum += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+    }
+    const float mean = wave_sum(sum) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { const float d = v[j][t] - mean; q = fmaf(d, d, q); }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float d4[4];
+      ld4<TA>(dy + row * D + j * 256 + lane * 4, d4);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        v[j][t] = (v[j][t] - mean) * rstd;  // xhat
+        ag[j][t] = fmaf(d4[t], v[j][t], ag[j][t]);
+        ab[j][t] += d4[t];
+        g[j][t] = d4[t] * gm[j][t];  // dxhat
+        s1 += g[j][t];
+        s2 = fmaf(g[j][t], v[j][t], s2);
+      }
+    }
+    const float m1 = wave_sum(s1) / (float)D, m2 = wave_sum(s2) / (float)D;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = j * 256 + lane * 4;
+      float r4[4], o[4];
+      ld4<TA>(res + (MODE == 0 ? (int64_t)s : row) * D + c, r4);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t] = rstd * (g[j][t] - m1 - v[j][t] * m2) + r4[t];
+      if constexpr (MODE == 0) {
+        st4<TA>(out + row * D + c, o);
+      } else {
+        float* d = dE + (int64_t)s * lde + c;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) atomicAdd(d + t, o[t]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sg[wave][j * 256 + lane * 4 + t] = ag[j][t];
+      sb[wave][j * 256 + lane * 4 + t] = ab[j][t];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    atomicAdd(dgamma + c, (sg[0][c] + sg[1][c]) + (sg[2][c] + sg[3][c]));
+    atomicAdd(dbeta + c, (sb[0][c] + sb[1][c]) + (sb[2][c] + sb[3][c]));
+  }
+}
+
+// dS = P (dP - sum_group P dP) over the 8 groups of 64 columns (one head's
+// latents, SDPA's softmax backward).  One wave per (row, group).
+template <typename TA>
+__global__ __launch_bounds__(256) void softmax64_bwd_kernel(int64_t rows, const TA* __restrict__ P,
+                                                            const TA* __restrict__ dP, TA* __restrict__ dS) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ng = rows * HEADS;
+  for (int64_t gi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); gi < ng; gi += (int64_t)gridDim.x * 4) {
+    const int64_t i = gi * 64 + lane;  // rows x 512 = groups x 64
+    const float p = (float)P[i], d = (float)dP[i];
+    const float dot = wave_sum(p * d);
+    dS[i] = (TA)(p * (d - dot));
+  }
+}
+
+// Backward of the latents' LayerNorm (norm_context, 64 rows) with dy = the sum
+// of `ns` split-K partials [ns][64][1024]: dlatents (written), dgamma / dbeta
+// (one block: plain accumulation into the caller-zeroed grads).
+__global__ __launch_bounds__(256) void lnc_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                      float eps, int ns, const float* __restrict__ parts,
+                                                      float* __restrict__ dx, float* __restrict__ dgamma,
+                                                      float* __restrict__ dbeta) {
+  __shared__ float sg[4][D], sb[4][D];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float ag[4][4], ab[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { ag[j][t] = 0.f; ab[j][t] = 0.f; }
+  for (int row = wave; row < NL; row += 4) {
+    float v[4][4], g[4][4], dy[4][4];
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = j * 256 + lane * 4;
+      ld4<float>(x + row * D + c, v[j]);
+      sum += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) dy[j][t] = 0.f;
+      for (int s = 0; s < ns; ++s) {
+        float p4[4];
+        ld4<float>(parts + ((int64_t)s * NL + row) * D + c, p4);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) dy[j][t] += p4[t];
+      }
+    }
+    const float mean = wave_sum(sum) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { const float d = v[j][t] - mean; q = fmaf(d, d, q); }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gm[4];
+      ld4<float>(gamma + j * 256 + lane * 4, gm);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        v[j][t] = (v[j][t] - mean) * rstd;
+        ag[j][t] = fmaf(dy[j][t], v[j][t], ag[j][t]);
+        ab[j][t] += dy[j][t];
+        g[j][t] = dy[j][t] * gm[t];
+        s1 += g[j][t];
+        s2 = fmaf(g[j][t], v[j][t], s2);
+      }
+    }
+    const float m1 = wave_sum(s1) / (float)D, m2 = wave_sum(s2) / (float)D;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float o[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t] = rstd * (g[j][t] - m1 - v[j][t] * m2);
+      st4<float>(dx + row * D + j * 256 + lane * 4, o);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sg[wave][j * 256 + lane * 4 + t] = ag[j][t];
+      sb[wave][j * 256 + lane * 4 + t] = ab[j][t];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    dgamma[c] += (sg[0][c] + sg[1][c]) + (sg[2][c] + sg[3][c]);
+    dbeta[c] += (sb[0][c] + sb[1][c]) + (sb[2][c] + sb[3][c]);
+  }
+}
+
+// ------------------------------------------------------------------ batched transposes
+// Up to kTMax matrices per launch (the step's weight transposes, the weight-grad
+// operands, the fold's operands): dst = src^T (transpose = 1) or dst = src
+// (a dtype conversion), 64 x 64 tiles through a float LDS tile.
+constexpr int kTMax = 8;
+struct TBatch {
+  int n;
+  int tile_end[kTMax], tiles_x[kTMax], transpose[kTMax];
+  const void* src[kTMax];
+  void* dst[kTMax];
+  int64_t rows[kTMax], cols[kTMax], lds[kTMax], ldd[kTMax];
+};
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void transpose_batched_kernel(TBatch tb) {
+  __shared__ float tile[64][65];
+  const int t = (int)blockIdx.x;
+  int p = 0;
+  while (p + 1 < tb.n && t >= tb.tile_end[p]) ++p;
+  const int local = t - (p ? tb.tile_end[p - 1] : 0);
+  const int64_t r0 = (int64_t)(local / tb.tiles_x[p]) * 64, c0 = (int64_t)(local % tb.tiles_x[p]) * 64;
+  const TI* src = (const TI*)tb.src[p];
+  TO* dst = (TO*)tb.dst[p];
+  const int64_t rows = tb.rows[p], cols = tb.cols[p], lds = tb.lds[p], ldd = tb.ldd[p];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  if (!tb.transpose[p]) {
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+      const int64_t r = r0 + ty + 4 * k, c = c0 + tx;
+      if (r < rows && c < cols) dst[r * ldd + c] = (TO)(float)src[r * lds + c];
+    }
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int rr = ty + 4 * k;
+    const int64_t r = r0 + rr, c = c0 + tx;
+    tile[rr][tx] = (r < rows && c < cols) ? (float)src[r * lds + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int cc = ty + 4 * k;
+    const int64_t c = c0 + cc, r = r0 + tx;
+    if (c < cols && r < rows) dst[c * ldd + r] = (TO)tile[tx][cc];
+  }
+}
+
+// 16-bit -> 16-bit transposes with 16-B global accesses (train.hip's
+// transpose16_kernel, batched): rows / cols / strides multiples of 8.
+__global__ __launch_bounds__(256) void transpose16_batched_kernel(TBatch tb) {
+  constexpr int P = 66;
+  __shared__ uint16_t tile[64 * P];
+  const int t = (int)blockIdx.x;
+  int p = 0;
+  while (p + 1 < tb.n && t >= tb.tile_end[p]) ++p;
+  const int local = t - (p ? tb.tile_end[p - 1] : 0);
+  const int64_t r0 = (int64_t)(local / tb.tiles_x[p]) * 64, c0 = (int64_t)(local % tb.tiles_x[p]) * 64;
+  const uint16_t* src = (const uint16_t*)tb.src[p];
+  uint16_t* dst = (uint16_t*)tb.dst[p];
+  const int64_t rows = tb.rows[p], cols = tb.cols[p], lds = tb.lds[p], ldd = tb.ldd[p];
+  const int th = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int rr = (th >> 3) + 32 * k, ch = th & 7;
+    const int64_t r = r0 + rr, c = c0 + 8 * ch;
+    uint4 u = make_uint4(0, 0, 0, 0);
+    if (r < rows && c < cols) u = *reinterpret_cast<const uint4*>(src + r * lds + c);
+    uint32_t* d = reinterpret_cast<uint32_t*>(tile + rr * P + 8 * ch);
+    d[0] = u.x; d[1] = u.y; d[2] = u.z; d[3] = u.w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int oc = (th >> 3) + 32 * k, rc = th & 7;
+    const int64_t c = c0 + oc, r = r0 + 8 * rc;
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      w[j] = (uint32_t)tile[(8 * rc + 2 * j) * P + oc] | ((uint32_t)tile[(8 * rc + 2 * j + 1) * P + oc] << 16);
+    if (c < cols && r < rows) *reinterpret_cast<uint4*>(dst + c * ldd + r) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+struct TList {
+  TBatch b{};
+  int tiles = 0;
+  bool all16 = true;
+  void add(const void* src, int64_t lds, void* dst, int64_t ldd, int64_t rows, int64_t cols, bool tr) {
+    const int i = b.n++;
+    b.src[i] = src; b.dst[i] = dst; b.rows[i] = rows; b.cols[i] = cols; b.lds[i] = lds; b.ldd[i] = ldd;
+    b.transpose[i] = tr ? 1 : 0;
+    b.tiles_x[i] = (int)((cols + 63) / 64);
+    tiles += (int)(((rows + 63) / 64) * b.tiles_x[i]);
+    b.tile_end[i] = tiles;
+    all16 = all16 && tr && rows % 8 == 0 && cols % 8 == 0 && lds % 8 == 0 && ldd % 8 == 0;
+  }
+};
+
+// TI -> TO batched transposes / conversions; 16-bit to 16-bit transposes on the 16-B kernel
+template <typename TI, typename TO>
+int launch_tlist(const TList& l, hipStream_t s) {
+  if (l.b.n == 0) return NR_OK;
+  if (sizeof(TI) == 2 && sizeof(TO) == 2 && l.all16)
+    hipLaunchKernelGGL(transpose16_batched_kernel, dim3((unsigned)l.tiles), dim3(256), 0, s, l.b);
+  else
+    hipLaunchKernelGGL((transpose_batched_kernel<TI, TO>), dim3((unsigned)l.tiles), dim3(256), 0, s, l.b);
+  NR_CHECK_LAUNCH("nr_latent_train_step (transposes)");
+  return NR_OK;
+}
+
+static int64_t pad64(int64_t n) { return n < 64 ? 64 : (n + 63) / 64 * 64; }
+static int64_t al(int64_t b) { return (b + 255) / 256 * 256; }
+
+// Workspace layout (byte offsets), shared by the size query and the step.
+struct Layout {
+  int64_t Hp, Bp, es;
+  int64_t E, Sx, X, P, H1, Y, G, Z, zbar, h1bar, row_seg, hparts, dmA, dmc, dZ, dG, dY, dH1, dP, dS, dX, dE;
+  int64_t dGT, YT, dH1T, PT, dST, XT, dmT, zbarT;
+  int64_t WqT, W1T, W2T, WoT, WkvT, latn, latnT, KV, KVT, A, AT, BtT, Bt;
+  int64_t gA, gBt, gA16, gAT16, gBt16, gBtT16, dKV, dKV16, dKVT16, dlat;
+  int64_t total;
+};
+constexpr int kHParts = 16;  // split-K slices of the m GEMM (K = 4096 -> 256)
+constexpr int kLatParts = 32;  // split-K slices of dlatents' GEMM (K = 8192 -> 256)
+
+static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs) {
+  Layout L{};
+  L.Hp = pad64(Hs);
+  L.Bp = pad64(B);
+  L.es = dtype == NR_F32 ? 4 : 2;
+  const int64_t Hp = L.Hp, Bp = L.Bp, es = L.es;
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) { const int64_t r = o; o += al(bytes); return r; };
+  L.E = take(U * D * 4);
+  L.Sx = take(Hp * D * es); L.X = take(Hp * D * es); L.P = take(Hp * S * es); L.H1 = take(Hp * D * es);
+  L.Y = take(Hp * D * es); L.G = take(Hp * 2 * F * es); L.Z = take(Hp * F * es);
+  L.zbar = take(Bp * F * es); L.h1bar = take(Bp * D * 4); L.row_seg = take(Hp * 4);
+  L.hparts = take((int64_t)kHParts * Bp * D * 4);
+  L.dmA = take(Bp * D * es); L.dmc = take(Bp * D * es); L.dZ = take(Bp * F * 4);
+  L.dG = take(Hp * 2 * F * es); L.dY = take(Hp * D * es); L.dH1 = take(Hp * D * es);
+  L.dP = take(Hp * S * es); L.dS = take(Hp * S * es); L.dX = take(Hp * D * es); L.dE = take(U * D * 4);
+  L.dGT = take(2 * F * Hp * es); L.YT = take(D * Hp * es); L.dH1T = take(D * Hp * es); L.PT = take(S * Hp * es);
+  L.dST = take(S * Hp * es); L.XT = take(D * Hp * es); L.dmT = take(D * Bp * es); L.zbarT = take(F * Bp * es);
+  L.WqT = take(D * F * es); L.W1T = take(D * 2 * F * es); L.W2T = take(F * D * es); L.WoT = take(F * D * es);
+  L.WkvT = take(D * 2 * F * es);
+  L.latn = take(NL * D * es); L.latnT = take(D * NL * es); L.KV = take(NL * 2 * F * es); L.KVT = take(2 * F * NL * es);
+  L.A = take(S * D * es); L.AT = take(D * S * es); L.BtT = take(S * D * es); L.Bt = take(D * S * es);
+  L.gA = take(S * D * 4); L.gBt = take(D * S * 4);
+  L.gA16 = take(S * D * es); L.gAT16 = take(D * S * es); L.gBt16 = take(D * S * es); L.gBtT16 = take(S * D * es);
+  L.dKV = take(NL * 2 * F * 4); L.dKV16 = take(NL * 2 * F * es); L.dKVT16 = take(2 * F * NL * es);
+  L.dlat = take((int64_t)kLatParts * NL * D * 4);
+  L.total = o;
+  return L;
+}
+
+static int grid_rows(int64_t rows, int cap = 1024) {
+  const int64_t g = (rows + 3) / 4;
+  return (int)(g < cap ? (g > 0 ? g : 1) : cap);
+}
+
+template <typename TA>
+int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
+  const int dt = a.dtype;
+  const Layout L = layout(dt, a.B, a.U, a.Hs);
+  const int64_t B = a.B, U = a.U, Hp = L.Hp, Bp = L.Bp;
+  auto P_ = [&](int64_t off) { return (void*)(ws + off); };
+  float* E = (float*)P_(L.E);
+  TA *Sx = (TA*)P_(L.Sx), *X = (TA*)P_(L.X), *Pm = (TA*)P_(L.P), *H1 = (TA*)P_(L.H1), *Y = (TA*)P_(L.Y);
+  TA *G = (TA*)P_(L.G), *Z = (TA*)P_(L.Z), *zbar = (TA*)P_(L.zbar);
+  float* h1bar = (float*)P_(L.h1bar);
+  int32_t* row_seg = (int32_t*)P_(L.row_seg);
+  float* hparts = (float*)P_(L.hparts);
+  TA *dmA = (TA*)P_(L.dmA), *dmc = (TA*)P_(L.dmc);
+  float* dZ = (float*)P_(L.dZ);
+  TA *dG = (TA*)P_(L.dG), *dY = (TA*)P_(L.dY), *dH1 = (TA*)P_(L.dH1), *dP = (TA*)P_(L.dP), *dS = (TA*)P_(L.dS);
+  TA* dX = (TA*)P_(L.dX);
+  float* dE = (float*)P_(L.dE);
+  TA *dGT = (TA*)P_(L.dGT), *YT = (TA*)P_(L.YT), *dH1T = (TA*)P_(L.dH1T), *PT = (TA*)P_(L.PT), *dST = (TA*)P_(L.dST);
+  TA *XT = (TA*)P_(L.XT), *dmT = (TA*)P_(L.dmT), *zbarT = (TA*)P_(L.zbarT);
+  TA *WqT = (TA*)P_(L.WqT), *W1T = (TA*)P_(L.W1T), *W2T = (TA*)P_(L.W2T), *WoT = (TA*)P_(L.WoT),
+     *WkvT = (TA*)P_(L.WkvT);
+  TA *latn = (TA*)P_(L.latn), *latnT = (TA*)P_(L.latnT), *KV = (TA*)P_(L.KV), *KVT = (TA*)P_(L.KVT);
+  TA *Am = (TA*)P_(L.A), *AT = (TA*)P_(L.AT), *BtT = (TA*)P_(L.BtT), *Bt = (TA*)P_(L.Bt);
+  float *gA = (float*)P_(L.gA), *gBt = (float*)P_(L.gBt);
+  TA *gA16 = (TA*)P_(L.gA16), *gAT16 = (TA*)P_(L.gAT16), *gBt16 = (TA*)P_(L.gBt16), *gBtT16 = (TA*)P_(L.gBtT16);
+  float* dKV = (float*)P_(L.dKV);
+  TA *dKV16 = (TA*)P_(L.dKV16), *dKVT16 = (TA*)P_(L.dKVT16);
+  float* dlat = (float*)P_(L.dlat);
+  const TA *Wq = (const TA*)a.Wq, *Wkv = (const TA*)a.Wkv, *Wo = (const TA*)a.Wo, *W1 = (const TA*)a.W1,
+           *W2 = (const TA*)a.W2;
+  const float scale = 1.0f / sqrtf((float)DH);  // SDPA default scale (latent_attention.py:72)
+  int rc;
+#define NR_LT_CHECK(name) NR_CHECK_LAUNCH("nr_latent_train_step (" name ")")
+
+  // ---- weight transposes (the data-grad GEMMs' W operands) and zeroed accumulators
+  {
+    TList t;
+    t.add(Wq, D, WqT, F, F, D, true);          // [4096, 1024] -> [1024, 4096]
+    t.add(W1, D, W1T, 2 * F, 2 * F, D, true);  // [8192, 1024] -> [1024, 8192]
+    t.add(W2, F, W2T, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
+    t.add(Wo, F, WoT, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
+    t.add(Wkv, D, WkvT, 2 * F, 2 * F, D, true);
+    if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
+  }
+  if (hipMemsetAsync(dE, 0, U * D * 4, st) != hipSuccess || hipMemsetAsync(a.loss, 0, 4, st) != hipSuccess) {
+    set_error("nr_latent_train_step: hipMemsetAsync failed");
+    return NR_ERR_HIP;
+  }
+  // ---- E = token LN of the last tokens (f32)
+  {
+    const float* gs = a.tok_g;
+    const float* bs = a.tok_b;
+    if ((rc = gather_ln_dispatch(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1, gs, bs, 1e-12f, E, D, st))) return rc;
+  }
+  // ---- fold: latn = LN_c(latents); KV = latn Wkv^T; A_h = s K_h Wq_h; BtT_h = V_h Wo_h^T
+  if ((rc = layernorm_dispatch(NR_F32, dt, NL, D, a.latents, D, a.nc_g, a.nc_b, 1e-5f, latn, D, st))) return rc;
+  if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, NL, 2 * F, D, latn, D, Wkv, D, nullptr, nullptr, 0, KV, 2 * F, st)))
+    return rc;
+  {
+    GemmProblem p[2] = {
+        {NL, D, DH, KV, 2 * F, DH, WqT, F, DH, Am, D, (int64_t)NL * D, HEADS, scale},
+        {NL, D, DH, KV + F, 2 * F, DH, Wo, F, DH, BtT, D, (int64_t)NL * D, HEADS, 1.0f},
+    };
+    if ((rc = gemm_group_dispatch(dt, dt, p, 2, st))) return rc;
+  }
+  {
+    TList t;
+    t.add(Am, D, AT, S, S, D, true);        // A [512, 1024] -> AT [1024, 512]
+    t.add(BtT, D, Bt, S, S, D, true);       // BtT [512, 1024] -> Bt [1024, 512]
+    t.add(latn, D, latnT, NL, NL, D, true); // [64, 1024] -> [1024, 64]
+    t.add(KV, 2 * F, KVT, NL, NL, 2 * F, true);  // [64, 8192] -> [8192, 64]
+    if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
+  }
+  // ---- per-slot forward
+  hipLaunchKernelGGL((gather_ln_kernel<TA>), dim3(grid_rows(Hp)), dim3(256), 0, st, Hp, a.Hs, E, (int64_t)D, a.hist_idx,
+                     a.nq_g, a.nq_b, 1e-5f, Sx, X);
+  NR_LT_CHECK("gather_ln");
+  if ((rc = gemm_dispatch(dt, dt, NR_EPI_SOFTMAX64, Hp, S, D, X, D, Am, D, nullptr, nullptr, 0, Pm, S, st))) return rc;
+  if ((rc = gemm_dispatch(dt, dt, NR_EPI_RESADD, Hp, D, S, Pm, S, Bt, S, nullptr, Sx, D, H1, D, st))) return rc;
+  if ((rc = layernorm_dispatch(dt, dt, Hp, D, H1, D, a.nf_g, a.nf_b, 1e-5f, Y, D, st))) return rc;
+  if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, 2 * F, D, Y, D, W1, D, a.b1, nullptr, 0, G, 2 * F, st))) return rc;
+  {
+    const int64_t q = Hp * (F / 4);
+    const int64_t g = (q + 255) / 256;
+    hipLaunchKernelGGL((geglu_fwd_kernel<TA>), dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, Hp, G, Z);
+    NR_LT_CHECK("geglu_fwd");
+  }
+  // ---- per batch row: means, m = zbar W2^T (split-K) + b2 + h1bar, loss
+  hipLaunchKernelGGL((segmean_kernel<TA>), dim3((unsigned)(Bp + 1), 10), dim3(256), 0, st, B, Bp, a.hist_off, Hp, Z,
+                     H1, zbar, h1bar, row_seg);
+  NR_LT_CHECK("segmean");
+  {
+    const int64_t ks = F / kHParts;
+    GemmProblem p = {Bp, D, ks, zbar, F, ks, W2, F, ks, hparts, D, Bp * D, kHParts, 1.0f};
+    if ((rc = gemm_group_dispatch(dt, NR_F32, &p, 1, st))) return rc;
+  }
+  hipLaunchKernelGGL((head_kernel<TA>), dim3((unsigned)((Bp + 3) / 4)), dim3(256), 0, st, B, Bp, kHParts, hparts,
+                     a.b2, h1bar, a.hist_off, E, (int64_t)D, a.pos, a.neg, a.margin, a.loss, a.users, dmA, dmc, dE,
+                     a.g_b2);
+  NR_LT_CHECK("head");
+  // ---- backward
+  // dZ_b = (dm_b / h_b) W2  (f32 [Bp, 4096]): C = dmc . W2T^T
+  if ((rc = gemm_dispatch(dt, NR_F32, NR_EPI_NONE, Bp, F, D, dmc, D, W2T, D, nullptr, nullptr, 0, dZ, F, st))) return rc;
+  {
+    const int rpb = 64;
+    hipLaunchKernelGGL((geglu_bwd_kernel<TA>), dim3((unsigned)((Hp + rpb - 1) / rpb), F / 1024), dim3(256), 0, st, Hp,
+                       rpb, G, dZ, row_seg, dG, a.g_b1);
+    NR_LT_CHECK("geglu_bwd");
+  }
+  if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, 2 * F, dG, 2 * F, W1T, 2 * F, nullptr, nullptr, 0, dY, D, st)))
+    return rc;
+  hipLaunchKernelGGL((ln_bwd_kernel<TA, 0>), dim3(grid_rows(Hp, 256)), dim3(256), 0, st, Hp, Hp, H1, a.nf_g, 1e-5f, dY, dmc,
+                     row_seg, dH1, nullptr, (int64_t)0, a.g_nf_g, a.g_nf_b);
+  NR_LT_CHECK("ln_f_bwd");
+  if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, S, D, dH1, D, BtT, D, nullptr, nullptr, 0, dP, S, st))) return rc;
+  {
+    const int64_t g = (Hp * HEADS + 3) / 4;
+    hipLaunchKernelGGL((softmax64_bwd_kernel<TA>), dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, Hp, Pm,
+                       dP, dS);
+    NR_LT_CHECK("softmax64_bwd");
+  }
+  if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, S, dS, S, AT, S, nullptr, nullptr, 0, dX, D, st))) return rc;
+  hipLaunchKernelGGL((ln_bwd_kernel<TA, 1>), dim3(grid_rows(Hp, 256)), dim3(256), 0, st, Hp, a.Hs, Sx, a.nq_g, 1e-5f, dX, dH1,
+                     a.hist_idx, nullptr, dE, (int64_t)D, a.g_nq_g, a.g_nq_b);
+  NR_LT_CHECK("ln_q_bwd");
+  // token LayerNorm parameter grads from dE (history scatter + cosine grads)
+  if ((rc = nr_ln_param_grad(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1e-12f, dE, D, a.g_tok_g, a.g_tok_b, st)))
+    return rc;
+  // ---- weight grads: W1 = dG^T Y, W2 = dm^T zbar, A = dS^T X, Bt = dH1^T P (K = Hp / Bp)
+  {
+    TList t;
+    t.add(dG, 2 * F, dGT, Hp, Hp, 2 * F, true);
+    t.add(Y, D, YT, Hp, Hp, D, true);
+    t.add(dH1, D, dH1T, Hp, Hp, D, true);
+    t.add(Pm, S, PT, Hp, Hp, S, true);
+    t.add(dS, S, dST, Hp, Hp, S, true);
+    t.add(X, D, XT, Hp, Hp, D, true);
+    t.add(dmA, D, dmT, Bp, Bp, D, true);
+    t.add(zbar, F, zbarT, Bp, Bp, F, true);
+    if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
+  }
+  {
+    GemmProblem p[4] = {
+        {2 * F, D, Hp, dGT, Hp, 0, YT, Hp, 0, a.g_W1, D, 0, 1, 1.0f},
+        {D, F, Bp, dmT, Bp, 0, zbarT, Bp, 0, a.g_W2, F, 0, 1, 1.0f},
+        {S, D, Hp, dST, Hp, 0, XT, Hp, 0, gA, D, 0, 1, 1.0f},
+        {D, S, Hp, dH1T, Hp, 0, PT, Hp, 0, gBt, S, 0, 1, 1.0f},
+    };
+    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 4, st))) return rc;
+  }
+  // ---- fold backward
+  {
+    TList t;
+    t.add(gA, D, gA16, D, S, D, false);
+    t.add(gA, D, gAT16, S, S, D, true);
+    t.add(gBt, S, gBt16, S, D, S, false);
+    t.add(gBt, S, gBtT16, D, D, S, true);
+    if ((rc = launch_tlist<float, TA>(t, st))) return rc;
+  }
+  {
+    // per head h: dWq_h = s K_h^T gA_h; dK_h = s gA_h Wq_h^T... as C = A W^T problems over the 8 heads
+    GemmProblem p[4] = {
+        // dWq_h [512, 1024] = s K_h^T gA_h: A = KT rows h*512 [512, 64], W = gAT cols h*64 [1024, 64]
+        {DH, D, NL, KVT, NL, (int64_t)DH * NL, gAT16, S, NL, a.g_Wq, D, (int64_t)DH * D, HEADS, scale},
+        // dK_h [64, 512] = s gA_h Wq_h: A = gA rows h*64 [64, 1024], W = Wq rows h*512 [512, 1024]
+        {NL, DH, D, gA16, D, (int64_t)NL * D, Wq, D, (int64_t)DH * D, dKV, 2 * F, DH, HEADS, scale},
+        // dV_h [64, 512] = gBtT_h Wo_h: A = gBtT rows h*64 [64, 1024], W = WoT rows h*512 [512, 1024]
+        {NL, DH, D, gBtT16, D, (int64_t)NL * D, WoT, D, (int64_t)DH * D, dKV + F, 2 * F, DH, HEADS, 1.0f},
+        // dWo_h [1024, 512] = gBt_h V_h: A = gBt cols h*64 [1024, 64], W = VT rows h*512 [512, 64]
+        {D, DH, NL, gBt16, S, NL, KVT + (int64_t)F * NL, NL, (int64_t)DH * NL, a.g_Wo, F, DH, HEADS, 1.0f},
+    };
+    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 4, st))) return rc;
+  }
+  {
+    TList t;
+    t.add(dKV, 2 * F, dKV16, 2 * F, NL, 2 * F, false);
+    t.add(dKV, 2 * F, dKVT16, NL, NL, 2 * F, true);
+    if ((rc = launch_tlist<float, TA>(t, st))) return rc;
+  }
+  {
+    const int64_t ks = 2 * F / kLatParts;
+    GemmProblem p[2] = {
+        // gWkv [8192, 1024] = dKV^T latn: A = dKVT [8192, 64], W = latnT [1024, 64]
+        {2 * F, D, NL, dKVT16, NL, 0, latnT, NL, 0, a.g_Wkv, D, 0, 1, 1.0f},
+        // dlatn [64, 1024] = dKV Wkv, split-K: A = dKV16 cols, W = WkvT cols
+        {NL, D, ks, dKV16, 2 * F, ks, WkvT, 2 * F, ks, dlat, D, (int64_t)NL * D, kLatParts, 1.0f},
+    };
+    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, st))) return rc;
+  }
+  hipLaunchKernelGGL(lnc_bwd_kernel, dim3(1), dim3(256), 0, st, a.latents, a.nc_g, 1e-5f, kLatParts, dlat, a.g_latents,
+                     a.g_nc_g, a.g_nc_b);
+  NR_LT_CHECK("ln_c_bwd");
+#undef NR_LT_CHECK
+  return NR_OK;
+}
+
+}  // namespace lt
+}  // namespace nr
+
+extern "C" int64_t nr_latent_train_workspace_bytes(int dtype, int64_t B, int64_t U, int64_t Hs) {
+  if ((dtype != NR_F32 && dtype != NR_BF16) || B < 0 || U < 0 || Hs < 0) return -1;
+  return nr::lt::layout(dtype, B, U, Hs).total;
+}
+
+extern "C" int nr_latent_train_step(const nr_latent_train_args* args, void* ws, int64_t ws_bytes, void* stream) {
+  nr::clear_error();
+  NR_CHECK_ARG(args, "nr_latent_train_step: null args");
+  const nr_latent_train_args& a = *args;
+  NR_CHECK_ARG(a.dtype == NR_F32 || a.dtype == NR_BF16, "nr_latent_train_step: dtype must be NR_F32 or NR_BF16");
+  NR_CHECK_ARG(a.tok_dtype == NR_F32 || a.tok_dtype == NR_BF16 || a.tok_dtype == NR_F16,
+               "nr_latent_train_step: bad tok_dtype");
+  NR_CHECK_ARG(a.B >= 1 && a.U >= 1 && a.Hs >= 1, "nr_latent_train_step: empty batch (B=%lld U=%lld Hs=%lld)",
+               (long long)a.B, (long long)a.U, (long long)a.Hs);
+  NR_CHECK_ARG(a.Hs <= (1ll << 31) - 64 && a.U <= (1ll << 31), "nr_latent_train_step: batch too large");
+  NR_CHECK_DEVICE("nr_latent_train_step", a.tok_last, a.hist_idx, a.hist_off, a.pos, a.neg, a.tok_g, a.tok_b,
+                  a.latents, a.nq_g, a.nq_b, a.nc_g, a.nc_b, a.Wq, a.Wkv, a.Wo, a.nf_g, a.nf_b, a.W1, a.b1, a.W2, a.b2);
+  NR_CHECK_DEVICE("nr_latent_train_step", a.g_tok_g, a.g_tok_b, a.g_latents, a.g_nq_g, a.g_nq_b, a.g_nc_g, a.g_nc_b,
+                  a.g_Wq, a.g_Wkv, a.g_Wo, a.g_nf_g, a.g_nf_b, a.g_W1, a.g_b1, a.g_W2, a.g_b2, a.loss, a.users, ws);
+  NR_CHECK_ARG(a.tok_last && a.hist_idx && a.hist_off && a.pos && a.neg && a.loss && ws,
+               "nr_latent_train_step: null pointer");
+  const int64_t need = nr::lt::layout(a.dtype, a.B, a.U, a.Hs).total;
+  NR_CHECK_ARG(ws_bytes >= need, "nr_latent_train_step: workspace too small (%lld < %lld)", (long long)ws_bytes,
+               (long long)need);
+  NR_CHECK_ARG(((uintptr_t)ws & 255) == 0, "nr_latent_train_step: workspace must be 256-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  return a.dtype == NR_F32 ? nr::lt::step<float>(a, (char*)ws, s) : nr::lt::step<__bf16>(a, (char*)ws, s);
+}

@@ -40,6 +40,8 @@ int layernorm_dispatch(int dti, int dto, int64_t rows, int64_t dim, const void* 
                        hipStream_t s);
 int softmax64_dispatch(int64_t rows, int64_t groups, const float* x, int64_t ldx, int dto, void* y,
                        int64_t ldy, hipStream_t s);
+int gather_ln_dispatch(int dti, int64_t n, int64_t dim, const void* x, int64_t ldx, const int64_t* row_idx,
+                       int n_ln, const float* g, const float* b, float eps, float* y, int64_t ldy, hipStream_t s);
 int pool_rows_dispatch(int pooler, int dtype, const void* table, int64_t ld, const int64_t* off, int64_t n_seg,
                        float* users, hipStream_t s);
 int row_stats_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps, float* out,
@@ -48,6 +50,21 @@ int row_stats_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int6
 // NR_EPI_GEGLU): C = epi(rstd_m * (A W^T - mean_m u_n) + c_n); stats [M] (mean, rstd), uc [2][N]
 int gemm_lnfold_dispatch(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W,
                          int64_t ldw, const float* stats, const float* uc, void* C, int64_t ldc, hipStream_t s);
+// One problem of a grouped GEMM launch (gemm.hip gemm_group_dispatch): C = alpha A W^T,
+// no bias; `batch` instances at A + b sA, W + b sW, C + b sC (element strides).
+struct GemmProblem {
+  int64_t M, N, K;
+  const void* A;
+  int64_t lda, sA;
+  const void* W;
+  int64_t ldw, sW;
+  void* C;
+  int64_t ldc, sC;
+  int batch;
+  float alpha;
+};
+constexpr int kGroupMax = 16;
+int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, int n, hipStream_t s);
 int inv_norm_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps,
                       float* out, hipStream_t s);
 

@@ -33,6 +33,7 @@ gradient because MyLayer discards them, attention.py:193).
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 from typing import Optional
 
@@ -300,23 +301,23 @@ class FinalAttentionTrainStep:
 class LatentAttentionTrainStep:
     """Config-5 step with ``LatentAttentionModel`` in the pooler slot (BASELINE
     configs[4]: "backward for encoder + latent attention"; the reference
-    trainer's loop, trainer.py:1044-1069, with the latent pooler): GEMMs on f32
-    operands (exact-f32 MFMA) or bf16 operands (bf16 MFMA, f32 accumulate and f32
-    activations / residual stream / LN, softmax and GEGLU kernels).
+    trainer's loop, trainer.py:1044-1069, with the latent pooler) as ONE library
+    call per batch (``nr_latent_train_step``, csrc/latent_train.hip):
 
-      E     = g_mlp_LN(last token of each unique news)      nr_gather_layernorm
-      S     = E[hist]                                        nr_gather_rows
-      H     = per-item latent hiddens of S                   latent_attention._LatentItemFn (HIP fwd + bwd)
-      users = normalize(segment mean of H)                   nr_pool_score (mean pass), latent_attention.py:166-170
-      loss  = MarginRankingLoss(2)(cos(users, E[pos]), cos(users, E[neg]))   nr_cosine_margin
-      dE   += scatter(dS); token LN grads                    nr_scatter_add_rows, nr_ln_param_grad
-      clip_grad_norm_(0.5) + AdamW                           nr_sumsq, nr_adamw
+      E     = g_mlp_LN(last token of each unique news)
+      fold  K/V of the 64 latents into A (scores) and Bt (output) once per step
+      per history slot: X = LN_q(E[hist]); P = softmax64(X Aᵀ); H1 = P Btᵀ + E[hist];
+                        Z = GEGLU(LN_f(H1) W1ᵀ + b1)
+      per batch row:    m = mean(Z) W2ᵀ + b2 + mean(H1)  (the last linear layer commutes
+                        with the history mean: its three GEMMs run over B rows, not slots)
+      users = normalize(m); loss = MarginRankingLoss(2)(cos(users, E[pos]), cos(users, E[neg]))
+      backward of all of it; clip_grad_norm_(0.5) + AdamW   nr_sumsq, nr_adamw
 
-    The latent block's backward runs through torch autograd over
-    ``_LatentItemFn`` (its per-item GEMM / LayerNorm / softmax / GEGLU backward
-    are HIP kernels) and the 64-latent weight fold; the parameters are views of
-    one flat f32 buffer (as in FinalAttentionTrainStep), so ``state_dict()``
-    stays current and AdamW is one launch."""
+    dtype float32: exact-f32 MFMA GEMMs and f32 activations (the parity mode);
+    bfloat16: bf16 operands and activations with f32 accumulation, statistics
+    and gradients, weights read from a bf16 mirror AdamW rewrites.  The
+    parameters are views of one flat f32 buffer (as in FinalAttentionTrainStep),
+    so ``state_dict()`` stays current and AdamW is one launch."""
 
     def __init__(self, token_model, latent_model, dtype: torch.dtype = torch.float32, lr: float = 1e-6,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.01, max_norm: float = 0.5,
@@ -334,70 +335,92 @@ class LatentAttentionTrainStep:
         self.step_count = 0
         self.ln = layers[0].g_mlp_layernorm
         self.ln_eps = float(self.ln.eps)
+        if abs(self.ln_eps - 1e-12) > 1e-18:
+            raise NewsRecHIPError("the token LayerNorm of MyLayer has eps 1e-12 (attention.py:155)")
         self.model = latent_model
         lat = list(latent_model.named_parameters())
         self.names = ["ln.weight", "ln.bias"] + [f"latent.{n}" for n, _ in lat]
         params = [self.ln.weight, self.ln.bias] + [p for _, p in lat]
         offs, o = [], 0
-        for p in params:
+        for prm in params:
             offs.append(o)
-            o += (p.numel() + 63) // 64 * 64
+            o += (prm.numel() + 63) // 64 * 64
         dev = self.device
+        self.n_flat = o
         self.flat = torch.zeros(o, dtype=torch.float32, device=dev)
         self.grad = torch.zeros_like(self.flat)
         self.m = torch.zeros_like(self.flat)
         self.v = torch.zeros_like(self.flat)
-        self.views, self.gviews = {}, {}
-        self._lat_params = []
+        self.flat16 = torch.zeros(o, dtype=torch.bfloat16, device=dev) if dtype == torch.bfloat16 else None
+        self.views, self.gviews, self.cviews = {}, {}, {}
         with torch.no_grad():
             for name, prm, off in zip(self.names, params, offs):
                 n = prm.numel()
                 view = self.flat[off:off + n].view(prm.shape)
                 view.copy_(prm.detach().to(dev, torch.float32))
-                prm.data = view
+                prm.data = view  # the modules now read the master weights
                 self.views[name] = view
                 self.gviews[name] = self.grad[off:off + n].view(prm.shape)
-                if name.startswith("latent."):
-                    self._lat_params.append((name, prm))
+                self.cviews[name] = self.flat16[off:off + n].view(prm.shape) if self.flat16 is not None else view
+            if self.flat16 is not None:
+                self.flat16.copy_(self.flat)
         self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._ws = None
+        self._users = None
+        b = "latent.cross_attend_blocks."
+        self._pmap = {"tok_g": "ln.weight", "tok_b": "ln.bias", "latents": "latent.latents",
+                      "nq_g": b + "0.norm.weight", "nq_b": b + "0.norm.bias",
+                      "nc_g": b + "0.norm_context.weight", "nc_b": b + "0.norm_context.bias",
+                      "Wq": b + "0.fn.to_q.weight", "Wkv": b + "0.fn.to_kv.weight", "Wo": b + "0.fn.to_out.weight",
+                      "nf_g": b + "1.norm.weight", "nf_b": b + "1.norm.bias",
+                      "W1": b + "1.fn.net.0.weight", "b1": b + "1.fn.net.0.bias",
+                      "W2": b + "1.fn.net.2.weight", "b2": b + "1.fn.net.2.bias"}
+        if set(self._pmap.values()) != set(self.names):
+            raise NewsRecHIPError(f"unexpected LatentAttentionModel parameters: {sorted(self.names)}")
 
     def forward_backward(self, batch: TrainBatch):
         """Loss (device scalar) and gradients into ``self.grad`` (zeroed first).
-        Returns (loss, users, E) for inspection."""
-        from .latent_attention import segment_mean
-        U, B = batch.tok_last.shape[0], batch.B
+        Returns (loss, users, None): users = the normalized pooled users [B, D]."""
+        from . import _lib
+        U, B, Hs = batch.tok_last.shape[0], batch.B, batch.hist_idx.numel()
+        lib = _lib.load()
+        dt = _lib.NR_BF16 if self.dtype == torch.bfloat16 else _lib.NR_F32
+        need = int(lib.nr_latent_train_workspace_bytes(dt, B, U, Hs))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        if self._users is None or self._users.shape[0] < B:
+            self._users = torch.empty((B, D), dtype=torch.float32, device=self.device)
+        tok = batch.tok_last.contiguous()
+        tdt = {torch.float32: _lib.NR_F32, torch.bfloat16: _lib.NR_BF16, torch.float16: _lib.NR_F16}[tok.dtype]
+        hi, ho = batch.hist_idx.to(torch.int32).contiguous(), batch.hist_off.to(torch.int64).contiguous()
+        pos, neg = batch.pos.to(torch.int32).contiguous(), batch.neg.to(torch.int32).contiguous()
+        a = _lib.LatentTrainArgs()
+        a.dtype, a.tok_dtype, a.B, a.U, a.Hs, a.margin = dt, tdt, B, U, Hs, MARGIN
+        a.tok_last, a.hist_idx, a.hist_off, a.pos, a.neg = (tok.data_ptr(), hi.data_ptr(), ho.data_ptr(), pos.data_ptr(),
+                                                            neg.data_ptr())
+        for f, name in self._pmap.items():
+            src = self.cviews[name] if f in ("Wq", "Wkv", "Wo", "W1", "W2") else self.views[name]
+            setattr(a, f, src.data_ptr())
+            setattr(a, "g_" + f, self.gviews[name].data_ptr())
+        a.loss, a.users = self.loss.data_ptr(), self._users.data_ptr()
         self.grad.zero_()
-        self.loss.zero_()
-        E = ops.gather_layernorm(batch.tok_last, None, self.views["ln.weight"].view(1, D),
-                                 self.views["ln.bias"].view(1, D), self.ln_eps)
-        S = ops.gather_rows(E, batch.hist_idx, out_dtype=torch.float32).requires_grad_(True)
-        for name, p in self._lat_params:
-            p.grad = self.gviews[name]  # autograd accumulates in place into the (zeroed) flat grad slices
-        with torch.enable_grad():
-            u = segment_mean(self.model._train_items(S, mm_dtype=self.dtype), batch.hist_off)
-            u = torch.nn.functional.normalize(u, p=2, dim=-1)
-        users = u.detach().contiguous()
-        du = torch.empty((B, D), dtype=torch.float32, device=self.device)
-        dE = torch.zeros((U, D), dtype=torch.float32, device=self.device)
-        ops.cosine_margin(users, E, batch.pos, batch.neg, MARGIN, self.loss, du, dE)
-        u.backward(du)
-        ops.scatter_add_rows(S.grad, batch.hist_idx, dE)
-        ops.ln_param_grad(batch.tok_last, None, self.ln_eps, dE, self.gviews["ln.weight"], self.gviews["ln.bias"])
-        for name, p in self._lat_params:
-            g = self.gviews[name]
-            if p.grad is not None and p.grad.data_ptr() != g.data_ptr():
-                g.copy_(p.grad)  # autograd replaced the slice instead of accumulating into it
-            p.grad = None
-        return self.loss, users, E
+        _lib.check(lib.nr_latent_train_step(ctypes.byref(a), self._ws.data_ptr(), self._ws.numel(),
+                                            torch.cuda.current_stream(self.device).cuda_stream),
+                   "nr_latent_train_step")
+        self._keep = (tok, hi, ho, pos, neg)  # alive until the stream has run the step
+        return self.loss, self._users[:B], None
 
     def optimizer_step(self) -> None:
-        """clip_grad_norm_(max_norm) + AdamW, one launch each (trainer.py:1067-1069)."""
+        """clip_grad_norm_(max_norm) + AdamW, one launch each (trainer.py:1067-1069);
+        the bf16 mode's weight mirror is rewritten by the same AdamW launch."""
         self.step_count += 1
         self.sumsq.zero_()
         ops.sumsq(self.grad, self.sumsq)
         ops.adamw(self.flat, self.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps, self.wd,
-                  self.max_norm, self.sumsq if self.max_norm > 0 else None, None)
+                  self.max_norm, self.sumsq if self.max_norm > 0 else None, self.flat16)
+        if hasattr(self.model, "_hip_cache"):
+            self.model._hip_cache = {}  # the eval path's folded weights are stale now
 
     def step(self, batch: TrainBatch) -> torch.Tensor:
         loss, _, _ = self.forward_backward(batch)
@@ -408,8 +431,17 @@ class LatentAttentionTrainStep:
     def grad_dict(self) -> dict:
         return dict(self.gviews)
 
-    def flops_per_step(self, Hs: int) -> float:
-        """MFMA FLOPs of the per-item GEMMs (forward + data-grad + weight-grad)."""
+    def flops_per_step(self, Hs: int, B: int = 256) -> float:
+        """MFMA FLOPs the step executes (forward, data-grad and weight-grad GEMMs,
+        the fold and its backward; the last layer's GEMMs over B rows)."""
+        Hp, Bp = _pad64(Hs), _pad64(B)
+        slot = 2.0 * Hp * (D * 512 + 512 * D + D * 8192)          # P, H1, G
+        row = 2.0 * Bp * 4096 * D                                  # m = mean(Z) W2^T
+        fold = 2.0 * 64 * D * 8192 + 2 * (2.0 * 8 * 64 * 512 * D)  # KV, A, Bt^T
+        return 3.0 * (slot + row + fold)
+
+    def model_flops_per_step(self, Hs: int) -> float:
+        """The reference formulation's GEMM FLOPs (every linear layer per history
+        slot, K/V once): what rounds 1-3 reported as this step's gemm_tflops."""
         Hp = _pad64(Hs)
-        fwd = 2.0 * Hp * (D * 512 + 512 * D + D * 8192 + 4096 * D)
-        return 3.0 * fwd
+        return 3.0 * 2.0 * Hp * (D * 512 + 512 * D + D * 8192 + 4096 * D)

@@ -84,7 +84,9 @@ def test_every_entry_with_pointers_is_covered():
               "nr_persistent_workgroups", "nr_final_attn_workspace_bytes", "nr_latent_workspace_bytes",
               "nr_encoder_workspace_bytes", "nr_residency_flush", "nr_is_device_pointer",
               # communicator handles (tests/test_comm.py)
-              "nr_rccl_version", "nr_comm_unique_id", "nr_comm_init", "nr_comm_destroy", "nr_allgather"}
+              "nr_rccl_version", "nr_comm_unique_id", "nr_comm_init", "nr_comm_destroy", "nr_allgather",
+              # one struct of pointers (test_latent_train_step_refuses_host_pointers below)
+              "nr_latent_train_workspace_bytes", "nr_latent_train_step"}
     assert set(_calls(ctypes.c_void_p(256))) == set(_lib.SIGNATURES) - no_ptr
 
 
@@ -102,3 +104,21 @@ def test_is_device_pointer_refuses_host_memory(lib, H):
     assert lib.nr_is_device_pointer(P) == 0
     assert lib.nr_is_device_pointer(None) == 0
     assert lib.nr_residency_flush() == 0
+
+
+def test_latent_train_step_refuses_host_pointers(lib, H):
+    """nr_latent_train_step takes its pointers in a struct: each of them is
+    checked before any launch (host buffer here -> NR_ERR_INVALID)."""
+    _, P = H
+    a = _lib.LatentTrainArgs()
+    a.dtype, a.tok_dtype, a.B, a.U, a.Hs, a.margin = _lib.NR_BF16, _lib.NR_F16, 4, 8, 16, 2.0
+    for f, _ in a._fields_:
+        if f not in ("dtype", "tok_dtype", "B", "U", "Hs", "margin"):
+            setattr(a, f, P.value)
+    rc = lib.nr_latent_train_step(ctypes.byref(a), P, 1 << 24, None)
+    assert rc == -1 and "not device memory" in lib.nr_last_error().decode()
+    a.B = 0
+    assert lib.nr_latent_train_step(ctypes.byref(a), P, 1 << 24, None) == -1
+    assert "empty batch" in lib.nr_last_error().decode()
+    assert lib.nr_latent_train_workspace_bytes(_lib.NR_BF16, 256, 8000, 8310) > 0
+    assert lib.nr_latent_train_workspace_bytes(7, 1, 1, 1) == -1

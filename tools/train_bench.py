@@ -6,7 +6,7 @@ Synthetic MIND-shaped batch: B training rows (one history group + one
 positive + one negative each), history lengths ~ clip(geometric(1/33), 1, 600),
 ids uniform over the news of the batch's impressions, token states N(0, 1)
 last rows (only the last valid token reaches the token model).  Times
-FinalAttentionTrainStep.step (forward, backward, clip, AdamW) with HIP events
+FinalAttentionTrainStep.step / LatentAttentionTrainStep.step (forward, backward, clip, AdamW) with HIP events
 and prints one JSON line: rows/s, ms/step, MFMA TFLOP/s of the GEMMs.
 """
 from __future__ import annotations
@@ -75,7 +75,10 @@ def main():
     print(json.dumps({"metric": "config-5 training rows/s (fwd+bwd+clip+AdamW)", "dtype": args.dtype,
                       "batch_rows": args.batch, "history_slots": Hs, "unique_news": U, "ms_per_step": round(ms, 3),
                       "rows_per_s": round(args.batch / ms * 1e3, 1), "slots_per_s": round(Hs / ms * 1e3, 1),
-                      "gemm_tflops": round(fl / ms / 1e9, 1), "loss_first": float(losses[0]),
+                      "gemm_tflops": round(fl / ms / 1e9, 1),
+                      "model_tflops_equiv": (round(eng.model_flops_per_step(Hs) / ms / 1e9, 1)
+                                             if hasattr(eng, "model_flops_per_step") else None),
+                      "loss_first": float(losses[0]),
                       "loss_last": float(losses[-1])}), flush=True)
 
 
