@@ -459,8 +459,11 @@ int nr_adamw(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf
  *   per batch row:    m = mean(Z) W2^T + b2 + mean(H1)   (= mean(H): the last
  *                     linear layer commutes with the history mean)
  *                     u = normalize(m); loss = MarginRankingLoss(2)(cos(u, E[pos]), cos(u, E[neg]))
- * and the exact backward of all of it; gradients are written into the f32
- * grad buffers (caller-zeroed: some are accumulated with atomics).  dtype
+ * and the exact backward of all of it; every gradient is written into its f32
+ * grad buffer (the step zeroes the ones it accumulates itself).  The weight
+ * grads of W1 / W2 run on an internal second stream beside the data-grad
+ * chain, joined back to `stream` (event wait) before the call returns, so the
+ * step stays ordered on `stream` and graph-capturable.  dtype
  * NR_F32: exact-f32 MFMA GEMMs and f32 activations; NR_BF16: bf16 operands and
  * activations, f32 accumulation, statistics and parameter gradients.
  * Weights are passed in `dtype` (the bf16 mirror for NR_BF16), LayerNorm
@@ -489,7 +492,7 @@ typedef struct nr_latent_train_args {
   const float* b1;            /* [8192] */
   const void* W2;             /* `dtype`: net.2.weight [1024][4096] */
   const float* b2;            /* [1024] */
-  /* gradients (f32, same shapes, caller-zeroed) */
+  /* gradients (f32, same shapes; fully written by the step) */
   float *g_tok_g, *g_tok_b, *g_latents, *g_nq_g, *g_nq_b, *g_nc_g, *g_nc_b, *g_Wq, *g_Wkv, *g_Wo;
   float *g_nf_g, *g_nf_b, *g_W1, *g_b1, *g_W2, *g_b2;
   /* outputs */

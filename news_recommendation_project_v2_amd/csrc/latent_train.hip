@@ -64,14 +64,58 @@ __device__ __forceinline__ void st4z(T* p) {
 
 __device__ __forceinline__ float gelu_x(float g) { return 0.5f * g * (1.0f + erff(g * 0.70710678118654752440f)); }
 
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float v[8]) {
+  if constexpr (sizeof(T) == 4) {
+    ld4<float>(p, v);
+    ld4<float>(p + 4, v + 4);
+  } else {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    v[0] = bf16_lo(u.x); v[1] = bf16_hi(u.x); v[2] = bf16_lo(u.y); v[3] = bf16_hi(u.y);
+    v[4] = bf16_lo(u.z); v[5] = bf16_hi(u.z); v[6] = bf16_lo(u.w); v[7] = bf16_hi(u.w);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float v[8]) {
+  if constexpr (sizeof(T) == 4) {
+    st4<float>(p, v);
+    st4<float>(p + 4, v + 4);
+  } else {
+    *reinterpret_cast<uint4*>(p) = uint4{pk2(v[0], v[1]), pk2(v[2], v[3]), pk2(v[4], v[5]), pk2(v[6], v[7])};
+  }
+}
+
+// sum of v over the 256 threads of the block (4 waves), returned to every thread
+__device__ __forceinline__ float block_sum(float v, float* scratch /* [4] */) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (scratch[0] + scratch[1]) + (scratch[2] + scratch[3]);
+}
+
+// ------------------------------------------------------------------ small helpers
+// zero up to 16 f32 ranges in one launch (the step's accumulated gradients)
+struct ZList {
+  int n;
+  float* p[16];
+  int64_t len[16];
+};
+__global__ __launch_bounds__(256) void zero_kernel(ZList z) {
+  for (int i = 0; i < z.n; ++i)
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < z.len[i]; k += (int64_t)gridDim.x * 256)
+      z.p[i][k] = 0.f;
+}
+
 // ------------------------------------------------------------------ forward rows
-// S = E[idx[row]], X = LN_q(S) (eps 1e-5); idx < 0 (padding): both rows zero.
-// One wave per row, lane columns 256 j + 4 lane .. +3.
+// S = E[idx[row]], X = LN_q(S) (eps 1e-5); idx < 0 or row >= nvalid
+// (padding): both rows zero.  One wave per row, lane columns 256 j + 4 lane .. +3.
 template <typename TA>
-__global__ __launch_bounds__(256) void gather_ln_kernel(int64_t n, int64_t nvalid, const float* __restrict__ E, int64_t lde,
-                                                        const int32_t* __restrict__ idx, const float* __restrict__ g,
-                                                        const float* __restrict__ b, float eps, TA* __restrict__ Sx,
-                                                        TA* __restrict__ X) {
+__global__ __launch_bounds__(256) void gather_ln_kernel(int64_t n, int64_t nvalid, const float* __restrict__ E,
+                                                        int64_t lde, const int32_t* __restrict__ idx,
+                                                        const float* __restrict__ g, const float* __restrict__ b,
+                                                        float eps, TA* __restrict__ Sx, TA* __restrict__ X) {
   const int lane = threadIdx.x & 63;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += (int64_t)gridDim.x * 4) {
     const int32_t r = row < nvalid ? idx[row] : -1;
@@ -110,26 +154,27 @@ __global__ __launch_bounds__(256) void gather_ln_kernel(int64_t n, int64_t nvali
 }
 
 // Z = a * gelu(g), (a | g) = the two halves of G's 2F columns (GEGLU,
-// latent_attention.py:24-27, exact erf).  4 columns per thread.
+// latent_attention.py:24-27, exact erf).  8 columns (16 B of bf16) per thread.
 template <typename TA>
 __global__ __launch_bounds__(256) void geglu_fwd_kernel(int64_t rows, const TA* __restrict__ G, TA* __restrict__ Z) {
-  const int64_t total = rows * (F / 4);
+  const int64_t total = rows * (F / 8);
   for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
-    const int64_t r = q / (F / 4), c = (q % (F / 4)) * 4;
-    float a[4], g[4], o[4];
-    ld4<TA>(G + r * 2 * F + c, a);
-    ld4<TA>(G + r * 2 * F + F + c, g);
+    const int64_t r = q / (F / 8), c = (q % (F / 8)) * 8;
+    float a[8], g[8], o[8];
+    ld8<TA>(G + r * 2 * F + c, a);
+    ld8<TA>(G + r * 2 * F + F + c, g);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) o[t] = a[t] * gelu_x(g[t]);
-    st4<TA>(Z + r * F + c, o);
+    for (int t = 0; t < 8; ++t) o[t] = a[t] * gelu_x(g[t]);
+    st8<TA>(Z + r * F + c, o);
   }
 }
 
 // Per batch row b: zbar_b = mean of Z over its slots (TA, the m GEMM's A
 // operand), h1bar_b = mean of H1 (f32), and row_seg[slot] = b.  Block =
 // (row b, 512-column chunk: chunks 0..7 of Z, 8..9 of H1); the 4 waves stride
-// the segment's rows, 8 columns per lane, fixed-order LDS fold.  Rows b in
-// [B, Bp) of zbar are zero; the last block marks the padding slots -1.
+// the segment's rows (two rows in flight), 8 columns per lane, fixed-order LDS
+// fold.  Rows b in [B, Bp) of zbar are zero; the last block marks the padding
+// slots -1.
 template <typename TA>
 __global__ __launch_bounds__(256) void segmean_kernel(int64_t B, int64_t Bp, const int64_t* __restrict__ off,
                                                       int64_t n_rows, const TA* __restrict__ Z,
@@ -148,8 +193,8 @@ __global__ __launch_bounds__(256) void segmean_kernel(int64_t B, int64_t Bp, con
   const int c0 = (zpart ? y : y - 8) * 512 + lane * 8;
   if (b >= B) {
     if (zpart && wave == 0) {
-      st4z<TA>(zbar + b * F + c0);
-      st4z<TA>(zbar + b * F + c0 + 4);
+      const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      st8<TA>(zbar + b * F + c0, z);
     }
     return;
   }
@@ -158,12 +203,19 @@ __global__ __launch_bounds__(256) void segmean_kernel(int64_t B, int64_t Bp, con
     for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) row_seg[r] = (int32_t)b;
   const TA* src = zpart ? Z : H1;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int64_t r = r0 + wave; r < r1; r += 4) {
-    float v[4], w[4];
-    ld4<TA>(src + r * ld + c0, v);
-    ld4<TA>(src + r * ld + c0 + 4, w);
+  int64_t r = r0 + wave;
+  for (; r + 4 < r1; r += 8) {
+    float v[8], w[8];
+    ld8<TA>(src + r * ld + c0, v);
+    ld8<TA>(src + (r + 4) * ld + c0, w);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) { acc[t] += v[t]; acc[4 + t] += w[t]; }
+    for (int t = 0; t < 8; ++t) acc[t] += v[t] + w[t];
+  }
+  if (r < r1) {
+    float v[8];
+    ld8<TA>(src + r * ld + c0, v);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] += v[t];
   }
 #pragma unroll
   for (int t = 0; t < 8; ++t) part[wave][lane * 8 + t] = acc[t];
@@ -176,22 +228,18 @@ __global__ __launch_bounds__(256) void segmean_kernel(int64_t B, int64_t Bp, con
     const int c = lane * 8 + t;
     o[t] = ((part[0][c] + part[1][c]) + (part[2][c] + part[3][c])) * inv;
   }
-  if (zpart) {
-    st4<TA>(zbar + b * F + c0, o);
-    st4<TA>(zbar + b * F + c0 + 4, o + 4);
-  } else {
-    st4<float>(h1bar + b * D + c0, o);
-    st4<float>(h1bar + b * D + c0 + 4, o + 4);
-  }
+  if (zpart) st8<TA>(zbar + b * F + c0, o);
+  else st8<float>(h1bar + b * D + c0, o);
 }
 
-// Per batch row (one wave): m = sum_s parts[s][b] + b2 + h1bar[b];
-// u = m / max(|m|, 1e-12) (F.normalize, latent_attention.py:170);
-// F.cosine_similarity(u, E[pos]) / (u, E[neg]) with the per-vector 1e-8 clamp,
-// MarginRankingLoss(margin) mean over B (trainer.py:1058-1066); backward:
-// du as nr_cosine_margin, dm = (du - u (u . du)) / |m| (normalize backward;
-// du / 1e-12 below the clamp).  Writes users = u, dmA = dm, dmc = dm / h_b
-// (rows b in [B, Bp): zero), gb2 += dm, dE[pos / neg] += their cosine grads.
+// One block per batch row b (256 threads, columns tid + 256 j):
+// m = sum_s parts[s][b] + b2 + h1bar[b]; u = m / max(|m|, 1e-12) (F.normalize,
+// latent_attention.py:170); F.cosine_similarity(u, E[pos]) / (u, E[neg]) with
+// the per-vector 1e-8 clamp and MarginRankingLoss(margin), mean over B
+// (trainer.py:1058-1066); backward: du as nr_cosine_margin, dm = (du - u (u .
+// du)) / |m| (normalize backward; du / 1e-12 below the clamp).  Writes users = u,
+// dmA = dm, dmc = dm / h_b (rows b in [B, Bp): zero), gb2 += dm, dE[pos / neg]
+// += their cosine grads (lane-contiguous atomics: 256 B per wave instruction).
 template <typename TA>
 __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int nparts, const float* __restrict__ parts,
                                                    const float* __restrict__ b2, const float* __restrict__ h1bar,
@@ -202,138 +250,147 @@ __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int np
                                                    TA* __restrict__ dmA, TA* __restrict__ dmc, float* __restrict__ dE,
                                                    float* __restrict__ gb2) {
   constexpr float EPS = 1e-8f, NEPS = 1e-12f;
-  const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= Bp) return;
+  __shared__ float red[4];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
   if (b >= B) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      st4z<TA>(dmA + b * D + j * 256 + lane * 4);
-      st4z<TA>(dmc + b * D + j * 256 + lane * 4);
+      dmA[b * D + j * 256 + tid] = (TA)0.f;
+      dmc[b * D + j * 256 + tid] = (TA)0.f;
     }
     return;
   }
-  float m[4][4], ep[4][4], en[4][4];
-  float mm = 0.f;
+  float m[4], ep[4], en[4];
   const float* pr = E + (int64_t)pos[b] * lde;
   const float* nr_ = E + (int64_t)neg[b] * lde;
+  float mm = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = j * 256 + lane * 4;
-    float t4[4];
-    ld4<float>(h1bar + b * D + c, m[j]);
-    ld4<float>(b2 + c, t4);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) m[j][t] += t4[t];
-    for (int s = 0; s < nparts; ++s) {
-      ld4<float>(parts + ((int64_t)s * Bp + b) * D + c, t4);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) m[j][t] += t4[t];
-    }
-    ld4<float>(pr + c, ep[j]);
-    ld4<float>(nr_ + c, en[j]);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) mm = fmaf(m[j][t], m[j][t], mm);
+    const int c = j * 256 + tid;
+    float v = h1bar[b * D + c] + b2[c];
+    for (int s = 0; s < nparts; ++s) v += parts[((int64_t)s * Bp + b) * D + c];
+    m[j] = v;
+    ep[j] = pr[c];
+    en[j] = nr_[c];
+    mm = fmaf(v, v, mm);
   }
-  const float nm = sqrtf(wave_sum(mm));
+  const float nm = sqrtf(block_sum(mm, red));
   const float den = fmaxf(nm, NEPS);
+  float u[4];
   float uu = 0.f, pp = 0.f, nn = 0.f, up = 0.f, un = 0.f;
-  float u[4][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      u[j][t] = m[j][t] / den;
-      uu = fmaf(u[j][t], u[j][t], uu);
-      pp = fmaf(ep[j][t], ep[j][t], pp);
-      nn = fmaf(en[j][t], en[j][t], nn);
-      up = fmaf(u[j][t], ep[j][t], up);
-      un = fmaf(u[j][t], en[j][t], un);
-    }
-  uu = wave_sum(uu); pp = wave_sum(pp); nn = wave_sum(nn); up = wave_sum(up); un = wave_sum(un);
+  for (int j = 0; j < 4; ++j) {
+    u[j] = m[j] / den;
+    uu = fmaf(u[j], u[j], uu);
+    pp = fmaf(ep[j], ep[j], pp);
+    nn = fmaf(en[j], en[j], nn);
+    up = fmaf(u[j], ep[j], up);
+    un = fmaf(u[j], en[j], un);
+  }
+  uu = block_sum(uu, red); pp = block_sum(pp, red); nn = block_sum(nn, red);
+  up = block_sum(up, red); un = block_sum(un, red);
   const float nu = sqrtf(uu), np_ = sqrtf(pp), nq = sqrtf(nn);
   const float iu = 1.0f / fmaxf(nu, EPS), ip = 1.0f / fmaxf(np_, EPS), iq = 1.0f / fmaxf(nq, EPS);
   const float sp = up * iu * ip, sn = un * iu * iq;
   const float v = margin - (sp - sn);
   const float act = v >= 0.f ? 1.0f : 0.0f;
   const float gsp = -act / (float)B, gsn = act / (float)B;
-  if (lane == 0) atomicAdd(loss, fmaxf(v, 0.f) / (float)B);
+  if (tid == 0) atomicAdd(loss, fmaxf(v, 0.f) / (float)B);
   const float cu = nu > EPS ? 1.f : 0.f, cp = np_ > EPS ? 1.f : 0.f, cq = nq > EPS ? 1.f : 0.f;
   float* dp = dE + (int64_t)pos[b] * lde;
   float* dn = dE + (int64_t)neg[b] * lde;
-  float g[4][4];
+  float g[4];
   float ug = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = j * 256 + lane * 4;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float uh = u[j][t] * iu, ph = ep[j][t] * ip, qh = en[j][t] * iq;
-      g[j][t] = gsp * (ph - cu * sp * uh) * iu + gsn * (qh - cu * sn * uh) * iu;
-      ug = fmaf(u[j][t], g[j][t], ug);
-      atomicAdd(dp + c + t, gsp * (uh - cp * sp * ph) * ip);
-      atomicAdd(dn + c + t, gsn * (uh - cq * sn * qh) * iq);
-    }
+    const int c = j * 256 + tid;
+    const float uh = u[j] * iu, ph = ep[j] * ip, qh = en[j] * iq;
+    g[j] = gsp * (ph - cu * sp * uh) * iu + gsn * (qh - cu * sn * uh) * iu;
+    ug = fmaf(u[j], g[j], ug);
+    atomicAdd(dp + c, gsp * (uh - cp * sp * ph) * ip);
+    atomicAdd(dn + c, gsn * (uh - cq * sn * qh) * iq);
   }
-  ug = wave_sum(ug);
+  ug = block_sum(ug, red);
   const float icnt = 1.0f / (float)(off[b + 1] - off[b]);
   const bool live = nm > NEPS;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = j * 256 + lane * 4;
-    float dm[4], dc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      dm[t] = (live ? g[j][t] - u[j][t] * ug : g[j][t]) / den;
-      dc[t] = dm[t] * icnt;
-      atomicAdd(gb2 + c + t, dm[t]);
-    }
-    if (users) st4<float>(users + b * D + c, u[j]);
-    st4<TA>(dmA + b * D + c, dm);
-    st4<TA>(dmc + b * D + c, dc);
+    const int c = j * 256 + tid;
+    const float dm = (live ? g[j] - u[j] * ug : g[j]) / den;
+    atomicAdd(gb2 + c, dm);
+    if (users) users[b * D + c] = u[j];
+    dmA[b * D + c] = (TA)dm;
+    dmc[b * D + c] = (TA)(dm * icnt);
   }
 }
 
 // ------------------------------------------------------------------ backward rows
-// dG = (dz gelu(g), dz a gelu'(g)) with dz = dZseg[row_seg[row]] (the per-row
-// dZ of the mean trick, f32), padding slots zero; gb1 += column sums (one
-// atomic per column per block).  Block = (rows_per_block rows, 1024 a-columns),
-// 4 columns per thread.
+// dG = (dz gelu(g), dz a gelu'(g)) over the slots of batch row b, with
+// dz = sum_p dZ[p][b] (the per-row dZ of the mean trick: split-K partials of
+// dmc . W2, f32), and gpart[b] = the column sums of dG over the row's slots
+// (reduced over b by nr_col_sum: db1, deterministic).  Block = (row b, 2048
+// a-columns), 8 columns per thread, two slots in flight.  Block b == B zeroes
+// the padding slots.
 template <typename TA>
-__global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t rows, int rpb, const TA* __restrict__ G,
-                                                        const float* __restrict__ dZ, const int32_t* __restrict__ row_seg,
-                                                        TA* __restrict__ dG, float* __restrict__ gb1) {
-  const int c = (int)blockIdx.y * 1024 + threadIdx.x * 4;
-  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = min(rows, r0 + rpb);
-  float sa[4] = {0.f, 0.f, 0.f, 0.f}, sg[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t r = r0; r < r1; ++r) {
-    const int32_t s = row_seg[r];
-    if (s < 0) {
-      st4z<TA>(dG + r * 2 * F + c);
-      st4z<TA>(dG + r * 2 * F + F + c);
-      continue;
+__global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t B, const int64_t* __restrict__ off, int64_t n_rows,
+                                                        const TA* __restrict__ G, int nparts,
+                                                        const float* __restrict__ dZ, int64_t Bp,
+                                                        TA* __restrict__ dG, float* __restrict__ gpart) {
+  const int64_t b = blockIdx.x;
+  const int c = (int)blockIdx.y * 2048 + threadIdx.x * 8;
+  const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (b >= B) {
+    for (int64_t r = off[B]; r < n_rows; ++r) {
+      st8<TA>(dG + r * 2 * F + c, zero);
+      st8<TA>(dG + r * 2 * F + F + c, zero);
     }
-    float a[4], g[4], d[4], da[4], dg[4];
-    ld4<TA>(G + r * 2 * F + c, a);
-    ld4<TA>(G + r * 2 * F + F + c, g);
-    ld4<float>(dZ + (int64_t)s * F + c, d);
+    return;
+  }
+  float d[8];
+  ld8<float>(dZ + b * F + c, d);
+  for (int p = 1; p < nparts; ++p) {
+    float t[8];
+    ld8<float>(dZ + ((int64_t)p * Bp + b) * F + c, t);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float cdf = 0.5f * (1.0f + erff(g[t] * 0.70710678118654752440f));
-      const float pdf = 0.39894228040143267794f * expf(-0.5f * g[t] * g[t]);
-      da[t] = d[t] * g[t] * cdf;
-      dg[t] = d[t] * a[t] * (cdf + g[t] * pdf);
-      sa[t] += da[t];
-      sg[t] += dg[t];
+    for (int k = 0; k < 8; ++k) d[k] += t[k];
+  }
+  float sa[8], sg[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sa[k] = 0.f; sg[k] = 0.f; }
+  auto one = [&](int64_t r, const float (&a)[8], const float (&g)[8]) {
+    float da[8], dg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float cdf = 0.5f * (1.0f + erff(g[k] * 0.70710678118654752440f));
+      const float pdf = 0.39894228040143267794f * __expf(-0.5f * g[k] * g[k]);
+      da[k] = d[k] * g[k] * cdf;
+      dg[k] = d[k] * a[k] * (cdf + g[k] * pdf);
+      sa[k] += da[k];
+      sg[k] += dg[k];
     }
-    st4<TA>(dG + r * 2 * F + c, da);
-    st4<TA>(dG + r * 2 * F + F + c, dg);
+    st8<TA>(dG + r * 2 * F + c, da);
+    st8<TA>(dG + r * 2 * F + F + c, dg);
+  };
+  const int64_t r0 = off[b], r1 = off[b + 1];
+  int64_t r = r0;
+  for (; r + 1 < r1; r += 2) {
+    float a0[8], g0[8], a1[8], g1[8];
+    ld8<TA>(G + r * 2 * F + c, a0);
+    ld8<TA>(G + r * 2 * F + F + c, g0);
+    ld8<TA>(G + (r + 1) * 2 * F + c, a1);
+    ld8<TA>(G + (r + 1) * 2 * F + F + c, g1);
+    one(r, a0, g0);
+    one(r + 1, a1, g1);
   }
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    atomicAdd(gb1 + c + t, sa[t]);
-    atomicAdd(gb1 + F + c + t, sg[t]);
+  if (r < r1) {
+    float a0[8], g0[8];
+    ld8<TA>(G + r * 2 * F + c, a0);
+    ld8<TA>(G + r * 2 * F + F + c, g0);
+    one(r, a0, g0);
   }
+  st8<float>(gpart + b * 2 * F + c, sa);
+  st8<float>(gpart + b * 2 * F + F + c, sg);
 }
 
 // LayerNorm input gradient (stats recomputed from x with the forward's
@@ -343,14 +400,18 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t rows, int rpb, c
 // MODE 0 (LN_f of H1): res = dmc[row_seg[row]] (the broadcast dH of the mean),
 //   dx -> out rows (TA); padding slots (row_seg < 0) -> zero rows.
 // MODE 1 (LN_q of S):  res = dH1 row (TA); dx scattered into dE[idx[row]]
-//   (f32 atomics: the gradient of the history gather), idx < 0 skipped.
+//   (the gradient of the history gather): the row is staged in the wave's LDS
+//   and added with lane-contiguous f32 atomics (256 B per wave instruction, the
+//   full-rate shape of MI355X_MICROARCH.md "Global float atomics"); idx < 0 skipped.
 template <typename TA, int MODE>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, const TA* __restrict__ x, const float* __restrict__ gamma,
-                                                     float eps, const TA* __restrict__ dy, const TA* __restrict__ res,
+__global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, const TA* __restrict__ x,
+                                                     const float* __restrict__ gamma, float eps,
+                                                     const TA* __restrict__ dy, const TA* __restrict__ res,
                                                      const int32_t* __restrict__ sel, TA* __restrict__ out,
                                                      float* __restrict__ dE, int64_t lde, float* __restrict__ dgamma,
                                                      float* __restrict__ dbeta) {
   __shared__ float sg[4][D], sb[4][D];
+  __shared__ float stage[MODE == 1 ? 4 : 1][MODE == 1 ? D : 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float ag[4][4], ab[4][4], gm[4][4];
 #pragma unroll
@@ -405,13 +466,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, 
       ld4<TA>(res + (MODE == 0 ? (int64_t)s : row) * D + c, r4);
 #pragma unroll
       for (int t = 0; t < 4; ++t) o[t] = rstd * (g[j][t] - m1 - v[j][t] * m2) + r4[t];
-      if constexpr (MODE == 0) {
-        st4<TA>(out + row * D + c, o);
-      } else {
-        float* d = dE + (int64_t)s * lde + c;
+      if constexpr (MODE == 0) st4<TA>(out + row * D + c, o);
+      else *reinterpret_cast<float4*>(&stage[wave][c]) = float4{o[0], o[1], o[2], o[3]};
+    }
+    if constexpr (MODE == 1) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float* d = dE + (int64_t)s * lde;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) atomicAdd(d + t, o[t]);
-      }
+      for (int k = 0; k < 16; ++k) atomicAdd(d + k * 64 + lane, stage[wave][k * 64 + lane]);
+      __builtin_amdgcn_wave_barrier();  // the stage is rewritten by the wave's next row
     }
   }
 #pragma unroll
@@ -444,92 +509,82 @@ __global__ __launch_bounds__(256) void softmax64_bwd_kernel(int64_t rows, const 
 }
 
 // Backward of the latents' LayerNorm (norm_context, 64 rows) with dy = the sum
-// of `ns` split-K partials [ns][64][1024]: dlatents (written), dgamma / dbeta
-// (one block: plain accumulation into the caller-zeroed grads).
+// of `ns` split-K partials [ns][64][1024]: one wave per row (16 blocks),
+// dlatents written, dgamma / dbeta accumulated (one atomic per column per block).
 __global__ __launch_bounds__(256) void lnc_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
                                                       float eps, int ns, const float* __restrict__ parts,
                                                       float* __restrict__ dx, float* __restrict__ dgamma,
                                                       float* __restrict__ dbeta) {
   __shared__ float sg[4][D], sb[4][D];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float ag[4][4], ab[4][4];
+  const int row = (int)blockIdx.x * 4 + wave;  // 16 blocks x 4 waves = the 64 latents
+  float v[4][4], g[4][4], dy[4][4];
+  float sum = 0.f;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < 4; ++j) {
+    const int c = j * 256 + lane * 4;
+    ld4<float>(x + row * D + c, v[j]);
+    sum += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) { ag[j][t] = 0.f; ab[j][t] = 0.f; }
-  for (int row = wave; row < NL; row += 4) {
-    float v[4][4], g[4][4], dy[4][4];
-    float sum = 0.f;
+    for (int t = 0; t < 4; ++t) dy[j][t] = 0.f;
+    for (int s = 0; s < ns; ++s) {
+      float p4[4];
+      ld4<float>(parts + ((int64_t)s * NL + row) * D + c, p4);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = j * 256 + lane * 4;
-      ld4<float>(x + row * D + c, v[j]);
-      sum += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) dy[j][t] = 0.f;
-      for (int s = 0; s < ns; ++s) {
-        float p4[4];
-        ld4<float>(parts + ((int64_t)s * NL + row) * D + c, p4);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) dy[j][t] += p4[t];
-      }
-    }
-    const float mean = wave_sum(sum) / (float)D;
-    float q = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) { const float d = v[j][t] - mean; q = fmaf(d, d, q); }
-    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float gm[4];
-      ld4<float>(gamma + j * 256 + lane * 4, gm);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        v[j][t] = (v[j][t] - mean) * rstd;
-        ag[j][t] = fmaf(dy[j][t], v[j][t], ag[j][t]);
-        ab[j][t] += dy[j][t];
-        g[j][t] = dy[j][t] * gm[t];
-        s1 += g[j][t];
-        s2 = fmaf(g[j][t], v[j][t], s2);
-      }
-    }
-    const float m1 = wave_sum(s1) / (float)D, m2 = wave_sum(s2) / (float)D;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float o[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) o[t] = rstd * (g[j][t] - m1 - v[j][t] * m2);
-      st4<float>(dx + row * D + j * 256 + lane * 4, o);
+      for (int t = 0; t < 4; ++t) dy[j][t] += p4[t];
     }
   }
+  const float mean = wave_sum(sum) / (float)D;
+  float q = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
+    for (int t = 0; t < 4; ++t) { const float d = v[j][t] - mean; q = fmaf(d, d, q); }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + eps);
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float gm[4];
+    ld4<float>(gamma + j * 256 + lane * 4, gm);
+#pragma unroll
     for (int t = 0; t < 4; ++t) {
-      sg[wave][j * 256 + lane * 4 + t] = ag[j][t];
-      sb[wave][j * 256 + lane * 4 + t] = ab[j][t];
+      v[j][t] = (v[j][t] - mean) * rstd;
+      sg[wave][j * 256 + lane * 4 + t] = dy[j][t] * v[j][t];
+      sb[wave][j * 256 + lane * 4 + t] = dy[j][t];
+      g[j][t] = dy[j][t] * gm[t];
+      s1 += g[j][t];
+      s2 = fmaf(g[j][t], v[j][t], s2);
     }
+  }
+  const float m1 = wave_sum(s1) / (float)D, m2 = wave_sum(s2) / (float)D;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[t] = rstd * (g[j][t] - m1 - v[j][t] * m2);
+    st4<float>(dx + row * D + j * 256 + lane * 4, o);
+  }
   __syncthreads();
   for (int c = threadIdx.x; c < D; c += 256) {
-    dgamma[c] += (sg[0][c] + sg[1][c]) + (sg[2][c] + sg[3][c]);
-    dbeta[c] += (sb[0][c] + sb[1][c]) + (sb[2][c] + sb[3][c]);
+    atomicAdd(dgamma + c, (sg[0][c] + sg[1][c]) + (sg[2][c] + sg[3][c]));
+    atomicAdd(dbeta + c, (sb[0][c] + sb[1][c]) + (sb[2][c] + sb[3][c]));
   }
 }
 
 // ------------------------------------------------------------------ batched transposes
 // Up to kTMax matrices per launch (the step's weight transposes, the weight-grad
 // operands, the fold's operands): dst = src^T (transpose = 1) or dst = src
-// (a dtype conversion), 64 x 64 tiles through a float LDS tile.
+// (a dtype conversion), 64 x 64 tiles.  A source may be `parts` f32 split-K
+// planes (pstride elements apart) that are summed on the way.  rows_pad >= rows:
+// a transposed dst gets zero columns [rows, rows_pad) (the zero K tail of a
+// split-K weight-grad GEMM).
 constexpr int kTMax = 8;
 struct TBatch {
   int n;
-  int tile_end[kTMax], tiles_x[kTMax], transpose[kTMax];
+  int tile_end[kTMax], tiles_x[kTMax], transpose[kTMax], parts[kTMax];
   const void* src[kTMax];
   void* dst[kTMax];
-  int64_t rows[kTMax], cols[kTMax], lds[kTMax], ldd[kTMax];
+  int64_t rows[kTMax], rows_pad[kTMax], cols[kTMax], lds[kTMax], ldd[kTMax], pstride[kTMax];
 };
 
 template <typename TI, typename TO>
@@ -542,13 +597,20 @@ __global__ __launch_bounds__(256) void transpose_batched_kernel(TBatch tb) {
   const int64_t r0 = (int64_t)(local / tb.tiles_x[p]) * 64, c0 = (int64_t)(local % tb.tiles_x[p]) * 64;
   const TI* src = (const TI*)tb.src[p];
   TO* dst = (TO*)tb.dst[p];
-  const int64_t rows = tb.rows[p], cols = tb.cols[p], lds = tb.lds[p], ldd = tb.ldd[p];
+  const int64_t rows = tb.rows[p], rpad = tb.rows_pad[p], cols = tb.cols[p], lds = tb.lds[p], ldd = tb.ldd[p];
+  const int np = tb.parts[p];
+  const int64_t ps = tb.pstride[p];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  auto val = [&](int64_t r, int64_t c) {
+    float v = (float)src[r * lds + c];
+    for (int q = 1; q < np; ++q) v += (float)src[q * ps + r * lds + c];
+    return v;
+  };
   if (!tb.transpose[p]) {
 #pragma unroll 4
     for (int k = 0; k < 16; ++k) {
       const int64_t r = r0 + ty + 4 * k, c = c0 + tx;
-      if (r < rows && c < cols) dst[r * ldd + c] = (TO)(float)src[r * lds + c];
+      if (r < rows && c < cols) dst[r * ldd + c] = (TO)val(r, c);
     }
     return;
   }
@@ -556,19 +618,19 @@ __global__ __launch_bounds__(256) void transpose_batched_kernel(TBatch tb) {
   for (int k = 0; k < 16; ++k) {
     const int rr = ty + 4 * k;
     const int64_t r = r0 + rr, c = c0 + tx;
-    tile[rr][tx] = (r < rows && c < cols) ? (float)src[r * lds + c] : 0.f;
+    tile[rr][tx] = (r < rows && c < cols) ? val(r, c) : 0.f;
   }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int cc = ty + 4 * k;
     const int64_t c = c0 + cc, r = r0 + tx;
-    if (c < cols && r < rows) dst[c * ldd + r] = (TO)tile[tx][cc];
+    if (c < cols && r < rpad) dst[c * ldd + r] = (TO)tile[tx][cc];
   }
 }
 
 // 16-bit -> 16-bit transposes with 16-B global accesses (train.hip's
-// transpose16_kernel, batched): rows / cols / strides multiples of 8.
+// transpose16_kernel, batched): rows_pad / cols / strides multiples of 8.
 __global__ __launch_bounds__(256) void transpose16_batched_kernel(TBatch tb) {
   constexpr int P = 66;
   __shared__ uint16_t tile[64 * P];
@@ -579,7 +641,7 @@ __global__ __launch_bounds__(256) void transpose16_batched_kernel(TBatch tb) {
   const int64_t r0 = (int64_t)(local / tb.tiles_x[p]) * 64, c0 = (int64_t)(local % tb.tiles_x[p]) * 64;
   const uint16_t* src = (const uint16_t*)tb.src[p];
   uint16_t* dst = (uint16_t*)tb.dst[p];
-  const int64_t rows = tb.rows[p], cols = tb.cols[p], lds = tb.lds[p], ldd = tb.ldd[p];
+  const int64_t rows = tb.rows[p], rpad = tb.rows_pad[p], cols = tb.cols[p], lds = tb.lds[p], ldd = tb.ldd[p];
   const int th = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -599,7 +661,7 @@ __global__ __launch_bounds__(256) void transpose16_batched_kernel(TBatch tb) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       w[j] = (uint32_t)tile[(8 * rc + 2 * j) * P + oc] | ((uint32_t)tile[(8 * rc + 2 * j + 1) * P + oc] << 16);
-    if (c < cols && r < rows) *reinterpret_cast<uint4*>(dst + c * ldd + r) = make_uint4(w[0], w[1], w[2], w[3]);
+    if (c < cols && r < rpad) *reinterpret_cast<uint4*>(dst + c * ldd + r) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 
@@ -607,14 +669,17 @@ struct TList {
   TBatch b{};
   int tiles = 0;
   bool all16 = true;
-  void add(const void* src, int64_t lds, void* dst, int64_t ldd, int64_t rows, int64_t cols, bool tr) {
+  void add(const void* src, int64_t lds, void* dst, int64_t ldd, int64_t rows, int64_t cols, bool tr,
+           int64_t rows_pad = 0, int parts = 1, int64_t pstride = 0) {
     const int i = b.n++;
-    b.src[i] = src; b.dst[i] = dst; b.rows[i] = rows; b.cols[i] = cols; b.lds[i] = lds; b.ldd[i] = ldd;
+    if (rows_pad < rows) rows_pad = rows;
+    b.src[i] = src; b.dst[i] = dst; b.rows[i] = rows; b.rows_pad[i] = rows_pad; b.cols[i] = cols;
+    b.lds[i] = lds; b.ldd[i] = ldd; b.parts[i] = parts; b.pstride[i] = pstride;
     b.transpose[i] = tr ? 1 : 0;
     b.tiles_x[i] = (int)((cols + 63) / 64);
-    tiles += (int)(((rows + 63) / 64) * b.tiles_x[i]);
+    tiles += (int)(((rows_pad + 63) / 64) * b.tiles_x[i]);
     b.tile_end[i] = tiles;
-    all16 = all16 && tr && rows % 8 == 0 && cols % 8 == 0 && lds % 8 == 0 && ldd % 8 == 0;
+    all16 = all16 && tr && parts == 1 && rows_pad % 8 == 0 && cols % 8 == 0 && lds % 8 == 0 && ldd % 8 == 0;
   }
 };
 
@@ -633,24 +698,31 @@ int launch_tlist(const TList& l, hipStream_t s) {
 static int64_t pad64(int64_t n) { return n < 64 ? 64 : (n + 63) / 64 * 64; }
 static int64_t al(int64_t b) { return (b + 255) / 256 * 256; }
 
+constexpr int kKVParts = 4;    // split-K slices of KV = latn Wkv^T (K = 1024 -> 256)
+constexpr int kHParts = 16;    // split-K slices of the m GEMM (K = 4096 -> 256)
+constexpr int kZParts = 8;     // split-K slices of dZ = dmc W2 (K = 1024 -> 128)
+constexpr int kWParts = 8;     // split-K slices of dA / dBt (K = Hp -> Hpp / 8)
+constexpr int kLatParts = 32;  // split-K slices of dlatents' GEMM (K = 8192 -> 256)
+
 // Workspace layout (byte offsets), shared by the size query and the step.
 struct Layout {
-  int64_t Hp, Bp, es;
-  int64_t E, Sx, X, P, H1, Y, G, Z, zbar, h1bar, row_seg, hparts, dmA, dmc, dZ, dG, dY, dH1, dP, dS, dX, dE;
+  int64_t Hp, Hpp, kw, Bp, es;
+  int64_t E, Sx, X, P, H1, Y, G, Z, zbar, h1bar, row_seg, hparts, dmA, dmc, dZ, gpart, dG, dY, dH1, dP, dS, dX, dE;
   int64_t dGT, YT, dH1T, PT, dST, XT, dmT, zbarT;
-  int64_t WqT, W1T, W2T, WoT, WkvT, latn, latnT, KV, KVT, A, AT, BtT, Bt;
+  int64_t WqT, W1T, W2T, WoT, WkvT, latn, latnT, KVp, KV, KVT, A, AT, BtT, Bt;
   int64_t gA, gBt, gA16, gAT16, gBt16, gBtT16, dKV, dKV16, dKVT16, dlat;
   int64_t total;
 };
-constexpr int kHParts = 16;  // split-K slices of the m GEMM (K = 4096 -> 256)
-constexpr int kLatParts = 32;  // split-K slices of dlatents' GEMM (K = 8192 -> 256)
 
 static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs) {
   Layout L{};
   L.Hp = pad64(Hs);
+  // dA / dBt run as kWParts K-slices of kw rows: Hpp = kWParts kw >= Hp (zero columns past Hp)
+  L.kw = (L.Hp / 64 + kWParts - 1) / kWParts * 64;
+  L.Hpp = L.kw * kWParts;
   L.Bp = pad64(B);
   L.es = dtype == NR_F32 ? 4 : 2;
-  const int64_t Hp = L.Hp, Bp = L.Bp, es = L.es;
+  const int64_t Hp = L.Hp, Hpp = L.Hpp, Bp = L.Bp, es = L.es;
   int64_t o = 0;
   auto take = [&](int64_t bytes) { const int64_t r = o; o += al(bytes); return r; };
   L.E = take(U * D * 4);
@@ -658,16 +730,18 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs) {
   L.Y = take(Hp * D * es); L.G = take(Hp * 2 * F * es); L.Z = take(Hp * F * es);
   L.zbar = take(Bp * F * es); L.h1bar = take(Bp * D * 4); L.row_seg = take(Hp * 4);
   L.hparts = take((int64_t)kHParts * Bp * D * 4);
-  L.dmA = take(Bp * D * es); L.dmc = take(Bp * D * es); L.dZ = take(Bp * F * 4);
+  L.dmA = take(Bp * D * es); L.dmc = take(Bp * D * es); L.dZ = take((int64_t)kZParts * Bp * F * 4);
+  L.gpart = take(Bp * 2 * F * 4);
   L.dG = take(Hp * 2 * F * es); L.dY = take(Hp * D * es); L.dH1 = take(Hp * D * es);
   L.dP = take(Hp * S * es); L.dS = take(Hp * S * es); L.dX = take(Hp * D * es); L.dE = take(U * D * 4);
-  L.dGT = take(2 * F * Hp * es); L.YT = take(D * Hp * es); L.dH1T = take(D * Hp * es); L.PT = take(S * Hp * es);
-  L.dST = take(S * Hp * es); L.XT = take(D * Hp * es); L.dmT = take(D * Bp * es); L.zbarT = take(F * Bp * es);
+  L.dGT = take(2 * F * Hp * es); L.YT = take(D * Hp * es); L.dH1T = take(D * Hpp * es); L.PT = take(S * Hpp * es);
+  L.dST = take(S * Hpp * es); L.XT = take(D * Hpp * es); L.dmT = take(D * Bp * es); L.zbarT = take(F * Bp * es);
   L.WqT = take(D * F * es); L.W1T = take(D * 2 * F * es); L.W2T = take(F * D * es); L.WoT = take(F * D * es);
   L.WkvT = take(D * 2 * F * es);
-  L.latn = take(NL * D * es); L.latnT = take(D * NL * es); L.KV = take(NL * 2 * F * es); L.KVT = take(2 * F * NL * es);
+  L.latn = take(NL * D * es); L.latnT = take(D * NL * es); L.KVp = take((int64_t)kKVParts * NL * 2 * F * 4);
+  L.KV = take(NL * 2 * F * es); L.KVT = take(2 * F * NL * es);
   L.A = take(S * D * es); L.AT = take(D * S * es); L.BtT = take(S * D * es); L.Bt = take(D * S * es);
-  L.gA = take(S * D * 4); L.gBt = take(D * S * 4);
+  L.gA = take((int64_t)kWParts * S * D * 4); L.gBt = take((int64_t)kWParts * D * S * 4);
   L.gA16 = take(S * D * es); L.gAT16 = take(D * S * es); L.gBt16 = take(D * S * es); L.gBtT16 = take(S * D * es);
   L.dKV = take(NL * 2 * F * 4); L.dKV16 = take(NL * 2 * F * es); L.dKVT16 = take(2 * F * NL * es);
   L.dlat = take((int64_t)kLatParts * NL * D * 4);
@@ -680,11 +754,39 @@ static int grid_rows(int64_t rows, int cap = 1024) {
   return (int)(g < cap ? (g > 0 ? g : 1) : cap);
 }
 
+// The step's second stream (the weight-grad GEMM of W1 runs there beside the
+// data-grad chain) and its fork / join events: one set per host thread and
+// device, created on first use and kept (streams are reentrant per thread).
+struct Side {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+static int side_stream(Side& out) {
+  thread_local Side t_side[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    set_error("nr_latent_train_step: no current HIP device");
+    return NR_ERR_HIP;
+  }
+  Side& sd = t_side[dev];
+  if (!sd.s) {
+    if (hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess) {
+      set_error("nr_latent_train_step: cannot create the side stream / events");
+      sd = Side{};
+      return NR_ERR_HIP;
+    }
+  }
+  out = sd;
+  return NR_OK;
+}
+
 template <typename TA>
 int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   const int dt = a.dtype;
   const Layout L = layout(dt, a.B, a.U, a.Hs);
-  const int64_t B = a.B, U = a.U, Hp = L.Hp, Bp = L.Bp;
+  const int64_t B = a.B, U = a.U, Hp = L.Hp, Hpp = L.Hpp, Bp = L.Bp;
   auto P_ = [&](int64_t off) { return (void*)(ws + off); };
   float* E = (float*)P_(L.E);
   TA *Sx = (TA*)P_(L.Sx), *X = (TA*)P_(L.X), *Pm = (TA*)P_(L.P), *H1 = (TA*)P_(L.H1), *Y = (TA*)P_(L.Y);
@@ -694,6 +796,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   float* hparts = (float*)P_(L.hparts);
   TA *dmA = (TA*)P_(L.dmA), *dmc = (TA*)P_(L.dmc);
   float* dZ = (float*)P_(L.dZ);
+  float* gpart = (float*)P_(L.gpart);
   TA *dG = (TA*)P_(L.dG), *dY = (TA*)P_(L.dY), *dH1 = (TA*)P_(L.dH1), *dP = (TA*)P_(L.dP), *dS = (TA*)P_(L.dS);
   TA* dX = (TA*)P_(L.dX);
   float* dE = (float*)P_(L.dE);
@@ -702,6 +805,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   TA *WqT = (TA*)P_(L.WqT), *W1T = (TA*)P_(L.W1T), *W2T = (TA*)P_(L.W2T), *WoT = (TA*)P_(L.WoT),
      *WkvT = (TA*)P_(L.WkvT);
   TA *latn = (TA*)P_(L.latn), *latnT = (TA*)P_(L.latnT), *KV = (TA*)P_(L.KV), *KVT = (TA*)P_(L.KVT);
+  float* KVp = (float*)P_(L.KVp);
   TA *Am = (TA*)P_(L.A), *AT = (TA*)P_(L.AT), *BtT = (TA*)P_(L.BtT), *Bt = (TA*)P_(L.Bt);
   float *gA = (float*)P_(L.gA), *gBt = (float*)P_(L.gBt);
   TA *gA16 = (TA*)P_(L.gA16), *gAT16 = (TA*)P_(L.gAT16), *gBt16 = (TA*)P_(L.gBt16), *gBtT16 = (TA*)P_(L.gBtT16);
@@ -711,10 +815,24 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   const TA *Wq = (const TA*)a.Wq, *Wkv = (const TA*)a.Wkv, *Wo = (const TA*)a.Wo, *W1 = (const TA*)a.W1,
            *W2 = (const TA*)a.W2;
   const float scale = 1.0f / sqrtf((float)DH);  // SDPA default scale (latent_attention.py:72)
+  Side side;
   int rc;
+  if ((rc = side_stream(side))) return rc;
 #define NR_LT_CHECK(name) NR_CHECK_LAUNCH("nr_latent_train_step (" name ")")
 
-  // ---- weight transposes (the data-grad GEMMs' W operands) and zeroed accumulators
+  // ---- accumulators: the step zeroes every gradient it accumulates (the GEMM-written
+  // ones are overwritten whole), the loss and the history-gather gradient dE
+  {
+    ZList z{};
+    float* zp[] = {a.g_tok_g, a.g_tok_b, a.g_nq_g, a.g_nq_b, a.g_nc_g, a.g_nc_b, a.g_nf_g, a.g_nf_b, a.g_b2, a.g_b1, a.loss};
+    const int64_t zn[] = {D, D, D, D, D, D, D, D, D, 2 * F, 1};
+    for (int i = 0; i < 11; ++i) { z.p[i] = zp[i]; z.len[i] = zn[i]; }
+    z.p[11] = dE; z.len[11] = U * D;
+    z.n = 12;
+    hipLaunchKernelGGL(zero_kernel, dim3(1024), dim3(256), 0, st, z);
+    NR_LT_CHECK("zero");
+  }
+  // ---- weight transposes (the data-grad GEMMs' W operands)
   {
     TList t;
     t.add(Wq, D, WqT, F, F, D, true);          // [4096, 1024] -> [1024, 4096]
@@ -724,20 +842,20 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     t.add(Wkv, D, WkvT, 2 * F, 2 * F, D, true);
     if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
   }
-  if (hipMemsetAsync(dE, 0, U * D * 4, st) != hipSuccess || hipMemsetAsync(a.loss, 0, 4, st) != hipSuccess) {
-    set_error("nr_latent_train_step: hipMemsetAsync failed");
-    return NR_ERR_HIP;
-  }
   // ---- E = token LN of the last tokens (f32)
-  {
-    const float* gs = a.tok_g;
-    const float* bs = a.tok_b;
-    if ((rc = gather_ln_dispatch(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1, gs, bs, 1e-12f, E, D, st))) return rc;
-  }
-  // ---- fold: latn = LN_c(latents); KV = latn Wkv^T; A_h = s K_h Wq_h; BtT_h = V_h Wo_h^T
-  if ((rc = layernorm_dispatch(NR_F32, dt, NL, D, a.latents, D, a.nc_g, a.nc_b, 1e-5f, latn, D, st))) return rc;
-  if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, NL, 2 * F, D, latn, D, Wkv, D, nullptr, nullptr, 0, KV, 2 * F, st)))
+  if ((rc = gather_ln_dispatch(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1, a.tok_g, a.tok_b, 1e-12f, E, D, st)))
     return rc;
+  // ---- fold: latn = LN_c(latents); KV = latn Wkv^T (split-K); A_h = s K_h Wq_h; BtT_h = V_h Wo_h^T
+  if ((rc = layernorm_dispatch(NR_F32, dt, NL, D, a.latents, D, a.nc_g, a.nc_b, 1e-5f, latn, D, st))) return rc;
+  {
+    const int64_t ks = D / kKVParts;
+    GemmProblem p = {NL, 2 * F, ks, latn, D, ks, Wkv, D, ks, KVp, 2 * F, (int64_t)NL * 2 * F, kKVParts, 1.0f};
+    if ((rc = gemm_group_dispatch(dt, NR_F32, &p, 1, st))) return rc;
+    TList t;
+    t.add(KVp, 2 * F, KV, 2 * F, NL, 2 * F, false, 0, kKVParts, (int64_t)NL * 2 * F);
+    t.add(KVp, 2 * F, KVT, NL, NL, 2 * F, true, 0, kKVParts, (int64_t)NL * 2 * F);
+    if ((rc = launch_tlist<float, TA>(t, st))) return rc;
+  }
   {
     GemmProblem p[2] = {
         {NL, D, DH, KV, 2 * F, DH, WqT, F, DH, Am, D, (int64_t)NL * D, HEADS, scale},
@@ -747,24 +865,23 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   }
   {
     TList t;
-    t.add(Am, D, AT, S, S, D, true);        // A [512, 1024] -> AT [1024, 512]
-    t.add(BtT, D, Bt, S, S, D, true);       // BtT [512, 1024] -> Bt [1024, 512]
-    t.add(latn, D, latnT, NL, NL, D, true); // [64, 1024] -> [1024, 64]
-    t.add(KV, 2 * F, KVT, NL, NL, 2 * F, true);  // [64, 8192] -> [8192, 64]
+    t.add(Am, D, AT, S, S, D, true);         // A [512, 1024] -> AT [1024, 512]
+    t.add(BtT, D, Bt, S, S, D, true);        // BtT [512, 1024] -> Bt [1024, 512]
+    t.add(latn, D, latnT, NL, NL, D, true);  // [64, 1024] -> [1024, 64]
     if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
   }
   // ---- per-slot forward
-  hipLaunchKernelGGL((gather_ln_kernel<TA>), dim3(grid_rows(Hp)), dim3(256), 0, st, Hp, a.Hs, E, (int64_t)D, a.hist_idx,
-                     a.nq_g, a.nq_b, 1e-5f, Sx, X);
+  hipLaunchKernelGGL((gather_ln_kernel<TA>), dim3(grid_rows(Hp)), dim3(256), 0, st, Hp, a.Hs, E, (int64_t)D,
+                     a.hist_idx, a.nq_g, a.nq_b, 1e-5f, Sx, X);
   NR_LT_CHECK("gather_ln");
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_SOFTMAX64, Hp, S, D, X, D, Am, D, nullptr, nullptr, 0, Pm, S, st))) return rc;
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_RESADD, Hp, D, S, Pm, S, Bt, S, nullptr, Sx, D, H1, D, st))) return rc;
   if ((rc = layernorm_dispatch(dt, dt, Hp, D, H1, D, a.nf_g, a.nf_b, 1e-5f, Y, D, st))) return rc;
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, 2 * F, D, Y, D, W1, D, a.b1, nullptr, 0, G, 2 * F, st))) return rc;
   {
-    const int64_t q = Hp * (F / 4);
+    const int64_t q = Hp * (F / 8);
     const int64_t g = (q + 255) / 256;
-    hipLaunchKernelGGL((geglu_fwd_kernel<TA>), dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, Hp, G, Z);
+    hipLaunchKernelGGL((geglu_fwd_kernel<TA>), dim3((unsigned)(g < 8192 ? g : 8192)), dim3(256), 0, st, Hp, G, Z);
     NR_LT_CHECK("geglu_fwd");
   }
   // ---- per batch row: means, m = zbar W2^T (split-K) + b2 + h1bar, loss
@@ -776,23 +893,47 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     GemmProblem p = {Bp, D, ks, zbar, F, ks, W2, F, ks, hparts, D, Bp * D, kHParts, 1.0f};
     if ((rc = gemm_group_dispatch(dt, NR_F32, &p, 1, st))) return rc;
   }
-  hipLaunchKernelGGL((head_kernel<TA>), dim3((unsigned)((Bp + 3) / 4)), dim3(256), 0, st, B, Bp, kHParts, hparts,
-                     a.b2, h1bar, a.hist_off, E, (int64_t)D, a.pos, a.neg, a.margin, a.loss, a.users, dmA, dmc, dE,
-                     a.g_b2);
+  hipLaunchKernelGGL((head_kernel<TA>), dim3((unsigned)Bp), dim3(256), 0, st, B, Bp, kHParts, hparts, a.b2, h1bar,
+                     a.hist_off, E, (int64_t)D, a.pos, a.neg, a.margin, a.loss, a.users, dmA, dmc, dE, a.g_b2);
   NR_LT_CHECK("head");
   // ---- backward
-  // dZ_b = (dm_b / h_b) W2  (f32 [Bp, 4096]): C = dmc . W2T^T
-  if ((rc = gemm_dispatch(dt, NR_F32, NR_EPI_NONE, Bp, F, D, dmc, D, W2T, D, nullptr, nullptr, 0, dZ, F, st))) return rc;
+  // dZ_b = (dm_b / h_b) W2 (f32, split-K partials [kZParts, Bp, 4096]): C = dmc . W2T^T
   {
-    const int rpb = 64;
-    hipLaunchKernelGGL((geglu_bwd_kernel<TA>), dim3((unsigned)((Hp + rpb - 1) / rpb), F / 1024), dim3(256), 0, st, Hp,
-                       rpb, G, dZ, row_seg, dG, a.g_b1);
-    NR_LT_CHECK("geglu_bwd");
+    const int64_t ks = D / kZParts;
+    GemmProblem p = {Bp, F, ks, dmc, D, ks, W2T, D, ks, dZ, F, Bp * F, kZParts, 1.0f};
+    if ((rc = gemm_group_dispatch(dt, NR_F32, &p, 1, st))) return rc;
+  }
+  hipLaunchKernelGGL((geglu_bwd_kernel<TA>), dim3((unsigned)(B + 1), F / 2048), dim3(256), 0, st, B, a.hist_off, Hp,
+                     G, kZParts, dZ, Bp, dG, gpart);
+  NR_LT_CHECK("geglu_bwd");
+  if ((rc = nr_col_sum(NR_F32, B, 2 * F, gpart, 2 * F, a.g_b1, st))) return rc;
+  // fork: the weight grads of W1 (K = Hp, 128 tiles) and W2 on the side stream,
+  // beside the data-grad GEMM dY = dG W1 (132 persistent workgroups) on this one
+  if (hipEventRecord(side.fork, st) != hipSuccess || hipStreamWaitEvent(side.s, side.fork, 0) != hipSuccess) {
+    set_error("nr_latent_train_step: fork failed");
+    return NR_ERR_HIP;
+  }
+  {
+    TList t;
+    t.add(dG, 2 * F, dGT, Hp, Hp, 2 * F, true);
+    t.add(Y, D, YT, Hp, Hp, D, true);
+    t.add(dmA, D, dmT, Bp, Bp, D, true);
+    t.add(zbar, F, zbarT, Bp, Bp, F, true);
+    if ((rc = launch_tlist<TA, TA>(t, side.s))) return rc;
+    GemmProblem p[2] = {
+        {2 * F, D, Hp, dGT, Hp, 0, YT, Hp, 0, a.g_W1, D, 0, 1, 1.0f},
+        {D, F, Bp, dmT, Bp, 0, zbarT, Bp, 0, a.g_W2, F, 0, 1, 1.0f},
+    };
+    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, side.s))) return rc;
+    if (hipEventRecord(side.join, side.s) != hipSuccess) {
+      set_error("nr_latent_train_step: join record failed");
+      return NR_ERR_HIP;
+    }
   }
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, 2 * F, dG, 2 * F, W1T, 2 * F, nullptr, nullptr, 0, dY, D, st)))
     return rc;
-  hipLaunchKernelGGL((ln_bwd_kernel<TA, 0>), dim3(grid_rows(Hp, 256)), dim3(256), 0, st, Hp, Hp, H1, a.nf_g, 1e-5f, dY, dmc,
-                     row_seg, dH1, nullptr, (int64_t)0, a.g_nf_g, a.g_nf_b);
+  hipLaunchKernelGGL((ln_bwd_kernel<TA, 0>), dim3(grid_rows(Hp, 256)), dim3(256), 0, st, Hp, Hp, H1, a.nf_g, 1e-5f, dY,
+                     dmc, row_seg, dH1, nullptr, (int64_t)0, a.g_nf_g, a.g_nf_b);
   NR_LT_CHECK("ln_f_bwd");
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, S, D, dH1, D, BtT, D, nullptr, nullptr, 0, dP, S, st))) return rc;
   {
@@ -802,45 +943,38 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     NR_LT_CHECK("softmax64_bwd");
   }
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, S, dS, S, AT, S, nullptr, nullptr, 0, dX, D, st))) return rc;
-  hipLaunchKernelGGL((ln_bwd_kernel<TA, 1>), dim3(grid_rows(Hp, 256)), dim3(256), 0, st, Hp, a.Hs, Sx, a.nq_g, 1e-5f, dX, dH1,
-                     a.hist_idx, nullptr, dE, (int64_t)D, a.g_nq_g, a.g_nq_b);
+  hipLaunchKernelGGL((ln_bwd_kernel<TA, 1>), dim3(grid_rows(Hp, 256)), dim3(256), 0, st, Hp, a.Hs, Sx, a.nq_g, 1e-5f,
+                     dX, dH1, a.hist_idx, nullptr, dE, (int64_t)D, a.g_nq_g, a.g_nq_b);
   NR_LT_CHECK("ln_q_bwd");
   // token LayerNorm parameter grads from dE (history scatter + cosine grads)
   if ((rc = nr_ln_param_grad(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1e-12f, dE, D, a.g_tok_g, a.g_tok_b, st)))
     return rc;
-  // ---- weight grads: W1 = dG^T Y, W2 = dm^T zbar, A = dS^T X, Bt = dH1^T P (K = Hp / Bp)
+  // ---- dA = dS^T X and dBt = dH1^T P as kWParts K-slices (16 + 16 tiles alone would hold 32 CUs
+  // for a K = Hp tile time), summed while converting to the fold backward's operands
   {
     TList t;
-    t.add(dG, 2 * F, dGT, Hp, Hp, 2 * F, true);
-    t.add(Y, D, YT, Hp, Hp, D, true);
-    t.add(dH1, D, dH1T, Hp, Hp, D, true);
-    t.add(Pm, S, PT, Hp, Hp, S, true);
-    t.add(dS, S, dST, Hp, Hp, S, true);
-    t.add(X, D, XT, Hp, Hp, D, true);
-    t.add(dmA, D, dmT, Bp, Bp, D, true);
-    t.add(zbar, F, zbarT, Bp, Bp, F, true);
+    t.add(dH1, D, dH1T, Hpp, Hp, D, true, Hpp);
+    t.add(Pm, S, PT, Hpp, Hp, S, true, Hpp);
+    t.add(dS, S, dST, Hpp, Hp, S, true, Hpp);
+    t.add(X, D, XT, Hpp, Hp, D, true, Hpp);
     if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
-  }
-  {
-    GemmProblem p[4] = {
-        {2 * F, D, Hp, dGT, Hp, 0, YT, Hp, 0, a.g_W1, D, 0, 1, 1.0f},
-        {D, F, Bp, dmT, Bp, 0, zbarT, Bp, 0, a.g_W2, F, 0, 1, 1.0f},
-        {S, D, Hp, dST, Hp, 0, XT, Hp, 0, gA, D, 0, 1, 1.0f},
-        {D, S, Hp, dH1T, Hp, 0, PT, Hp, 0, gBt, S, 0, 1, 1.0f},
+    const int64_t kw = L.kw;
+    GemmProblem p[2] = {
+        {S, D, kw, dST, Hpp, kw, XT, Hpp, kw, gA, D, (int64_t)S * D, kWParts, 1.0f},
+        {D, S, kw, dH1T, Hpp, kw, PT, Hpp, kw, gBt, S, (int64_t)D * S, kWParts, 1.0f},
     };
-    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 4, st))) return rc;
+    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, st))) return rc;
   }
   // ---- fold backward
   {
     TList t;
-    t.add(gA, D, gA16, D, S, D, false);
-    t.add(gA, D, gAT16, S, S, D, true);
-    t.add(gBt, S, gBt16, S, D, S, false);
-    t.add(gBt, S, gBtT16, D, D, S, true);
+    t.add(gA, D, gA16, D, S, D, false, 0, kWParts, (int64_t)S * D);
+    t.add(gA, D, gAT16, S, S, D, true, 0, kWParts, (int64_t)S * D);
+    t.add(gBt, S, gBt16, S, D, S, false, 0, kWParts, (int64_t)D * S);
+    t.add(gBt, S, gBtT16, D, D, S, true, 0, kWParts, (int64_t)D * S);
     if ((rc = launch_tlist<float, TA>(t, st))) return rc;
   }
   {
-    // per head h: dWq_h = s K_h^T gA_h; dK_h = s gA_h Wq_h^T... as C = A W^T problems over the 8 heads
     GemmProblem p[4] = {
         // dWq_h [512, 1024] = s K_h^T gA_h: A = KT rows h*512 [512, 64], W = gAT cols h*64 [1024, 64]
         {DH, D, NL, KVT, NL, (int64_t)DH * NL, gAT16, S, NL, a.g_Wq, D, (int64_t)DH * D, HEADS, scale},
@@ -869,9 +1003,14 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     };
     if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, st))) return rc;
   }
-  hipLaunchKernelGGL(lnc_bwd_kernel, dim3(1), dim3(256), 0, st, a.latents, a.nc_g, 1e-5f, kLatParts, dlat, a.g_latents,
-                     a.g_nc_g, a.g_nc_b);
+  hipLaunchKernelGGL(lnc_bwd_kernel, dim3(NL / 4), dim3(256), 0, st, a.latents, a.nc_g, 1e-5f, kLatParts, dlat,
+                     a.g_latents, a.g_nc_g, a.g_nc_b);
   NR_LT_CHECK("ln_c_bwd");
+  // join: the side stream's weight grads are done before anything later on `stream`
+  if (hipStreamWaitEvent(st, side.join, 0) != hipSuccess) {
+    set_error("nr_latent_train_step: join failed");
+    return NR_ERR_HIP;
+  }
 #undef NR_LT_CHECK
   return NR_OK;
 }
@@ -893,7 +1032,8 @@ extern "C" int nr_latent_train_step(const nr_latent_train_args* args, void* ws, 
                "nr_latent_train_step: bad tok_dtype");
   NR_CHECK_ARG(a.B >= 1 && a.U >= 1 && a.Hs >= 1, "nr_latent_train_step: empty batch (B=%lld U=%lld Hs=%lld)",
                (long long)a.B, (long long)a.U, (long long)a.Hs);
-  NR_CHECK_ARG(a.Hs <= (1ll << 31) - 64 && a.U <= (1ll << 31), "nr_latent_train_step: batch too large");
+  NR_CHECK_ARG(a.Hs <= (1ll << 31) - 1024 && a.U <= (1ll << 31) && a.B <= (1ll << 24),
+               "nr_latent_train_step: batch too large");
   NR_CHECK_DEVICE("nr_latent_train_step", a.tok_last, a.hist_idx, a.hist_off, a.pos, a.neg, a.tok_g, a.tok_b,
                   a.latents, a.nq_g, a.nq_b, a.nc_g, a.nc_b, a.Wq, a.Wkv, a.Wo, a.nf_g, a.nf_b, a.W1, a.b1, a.W2, a.b2);
   NR_CHECK_DEVICE("nr_latent_train_step", a.g_tok_g, a.g_tok_b, a.g_latents, a.g_nq_g, a.g_nq_b, a.g_nc_g, a.g_nc_b,

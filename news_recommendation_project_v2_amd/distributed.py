@@ -66,7 +66,7 @@ class NrComm:
             _lib.check(self._lib.nr_comm_unique_id(idb), "nr_comm_unique_id")
         dev = torch.device("cuda", torch.cuda.current_device())
         staged = _host_staged(group)
-        t_id = torch.tensor(bytes(idb), dtype=torch.uint8, device="cpu" if staged else dev)
+        t_id = torch.tensor(list(idb), dtype=torch.uint8, device="cpu" if staged else dev)
         dist.broadcast(t_id, src=0, group=group)
         idb = (ctypes.c_ubyte * 128)(*t_id.cpu().tolist())
         self._lib.nr_init(dev.index)

@@ -380,8 +380,9 @@ class LatentAttentionTrainStep:
             raise NewsRecHIPError(f"unexpected LatentAttentionModel parameters: {sorted(self.names)}")
 
     def forward_backward(self, batch: TrainBatch):
-        """Loss (device scalar) and gradients into ``self.grad`` (zeroed first).
-        Returns (loss, users, None): users = the normalized pooled users [B, D]."""
+        """Loss (device scalar) and gradients into ``self.grad`` (every slice
+        rewritten).  Returns (loss, users, None): users = the normalized pooled
+        users [B, D]."""
         from . import _lib
         U, B, Hs = batch.tok_last.shape[0], batch.B, batch.hist_idx.numel()
         lib = _lib.load()
@@ -404,7 +405,8 @@ class LatentAttentionTrainStep:
             setattr(a, f, src.data_ptr())
             setattr(a, "g_" + f, self.gviews[name].data_ptr())
         a.loss, a.users = self.loss.data_ptr(), self._users.data_ptr()
-        self.grad.zero_()
+        # (no grad.zero_(): the step writes every gradient and zeroes its own accumulators;
+        # the flat buffer's alignment gaps were zeroed at construction and are never written)
         _lib.check(lib.nr_latent_train_step(ctypes.byref(a), self._ws.data_ptr(), self._ws.numel(),
                                             torch.cuda.current_stream(self.device).cuda_stream),
                    "nr_latent_train_step")

