@@ -326,40 +326,25 @@ __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int np
 }
 
 // ------------------------------------------------------------------ backward rows
-// dG = (dz gelu(g), dz a gelu'(g)) over the slots of batch row b, with
-// dz = sum_p dZ[p][b] (the per-row dZ of the mean trick: split-K partials of
-// dmc . W2, f32), and gpart[b] = the column sums of dG over the row's slots
-// (reduced over b by nr_col_sum: db1, deterministic).  Block = (row b, 2048
-// a-columns), 8 columns per thread, two slots in flight.  Block b == B zeroes
-// the padding slots.
-template <typename TA>
-__global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t B, const int64_t* __restrict__ off, int64_t n_rows,
-                                                        const TA* __restrict__ G, int nparts,
-                                                        const float* __restrict__ dZ, int64_t Bp,
+// dG = (dz gelu(g), dz a gelu'(g)) for slot rows, with dz = dZs[row_seg[row]]
+// (the per-batch-row dZ of the mean trick, f32, L2-resident), padding slots
+// zero; gpart[chunk] = the column sums of dG over the block's rows (reduced
+// over the chunks by nr_col_sum: db1, deterministic).  Block = (RB rows, 2048
+// a-columns), 8 columns per thread, two rows in flight.  Row chunks, not batch
+// rows: a history length can be ~20x the mean, and one block per batch row
+// then waits on the longest.
+template <typename TA, int RB>
+__global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t n_rows, const TA* __restrict__ G,
+                                                        const float* __restrict__ dZs, const int32_t* __restrict__ row_seg,
                                                         TA* __restrict__ dG, float* __restrict__ gpart) {
-  const int64_t b = blockIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * RB;
   const int c = (int)blockIdx.y * 2048 + threadIdx.x * 8;
-  const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (b >= B) {
-    for (int64_t r = off[B]; r < n_rows; ++r) {
-      st8<TA>(dG + r * 2 * F + c, zero);
-      st8<TA>(dG + r * 2 * F + F + c, zero);
-    }
-    return;
-  }
-  float d[8];
-  ld8<float>(dZ + b * F + c, d);
-  for (int p = 1; p < nparts; ++p) {
-    float t[8];
-    ld8<float>(dZ + ((int64_t)p * Bp + b) * F + c, t);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] += t[k];
-  }
   float sa[8], sg[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { sa[k] = 0.f; sg[k] = 0.f; }
-  auto one = [&](int64_t r, const float (&a)[8], const float (&g)[8]) {
-    float da[8], dg[8];
+  auto one = [&](int64_t r, int32_t s, const float (&a)[8], const float (&g)[8]) {
+    float d[8], da[8], dg[8];
+    ld8<float>(dZs + (int64_t)s * F + c, d);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float cdf = 0.5f * (1.0f + erff(g[k] * 0.70710678118654752440f));
@@ -372,25 +357,21 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t B, const int64_t
     st8<TA>(dG + r * 2 * F + c, da);
     st8<TA>(dG + r * 2 * F + F + c, dg);
   };
-  const int64_t r0 = off[b], r1 = off[b + 1];
-  int64_t r = r0;
-  for (; r + 1 < r1; r += 2) {
+  const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int i = 0; i < RB; i += 2) {
+    const int64_t ra = r0 + i, rb = r0 + i + 1;
+    const int32_t sa_ = ra < n_rows ? row_seg[ra] : -2, sb_ = rb < n_rows ? row_seg[rb] : -2;
     float a0[8], g0[8], a1[8], g1[8];
-    ld8<TA>(G + r * 2 * F + c, a0);
-    ld8<TA>(G + r * 2 * F + F + c, g0);
-    ld8<TA>(G + (r + 1) * 2 * F + c, a1);
-    ld8<TA>(G + (r + 1) * 2 * F + F + c, g1);
-    one(r, a0, g0);
-    one(r + 1, a1, g1);
+    if (sa_ >= 0) { ld8<TA>(G + ra * 2 * F + c, a0); ld8<TA>(G + ra * 2 * F + F + c, g0); }
+    if (sb_ >= 0) { ld8<TA>(G + rb * 2 * F + c, a1); ld8<TA>(G + rb * 2 * F + F + c, g1); }
+    if (sa_ >= 0) one(ra, sa_, a0, g0);
+    else if (sa_ == -1) { st8<TA>(dG + ra * 2 * F + c, zero); st8<TA>(dG + ra * 2 * F + F + c, zero); }
+    if (sb_ >= 0) one(rb, sb_, a1, g1);
+    else if (sb_ == -1) { st8<TA>(dG + rb * 2 * F + c, zero); st8<TA>(dG + rb * 2 * F + F + c, zero); }
   }
-  if (r < r1) {
-    float a0[8], g0[8];
-    ld8<TA>(G + r * 2 * F + c, a0);
-    ld8<TA>(G + r * 2 * F + F + c, g0);
-    one(r, a0, g0);
-  }
-  st8<float>(gpart + b * 2 * F + c, sa);
-  st8<float>(gpart + b * 2 * F + F + c, sg);
+  st8<float>(gpart + (int64_t)blockIdx.x * 2 * F + c, sa);
+  st8<float>(gpart + (int64_t)blockIdx.x * 2 * F + F + c, sg);
 }
 
 // LayerNorm input gradient (stats recomputed from x with the forward's
@@ -700,14 +681,16 @@ static int64_t al(int64_t b) { return (b + 255) / 256 * 256; }
 
 constexpr int kKVParts = 4;    // split-K slices of KV = latn Wkv^T (K = 1024 -> 256)
 constexpr int kHParts = 16;    // split-K slices of the m GEMM (K = 4096 -> 256)
-constexpr int kZParts = 8;     // split-K slices of dZ = dmc W2 (K = 1024 -> 128)
+constexpr int kZParts = 4;     // split-K slices of dZ = dmc W2 (K = 1024 -> 256)
+constexpr int kGRows = 16;     // slot rows per GEGLU-backward block
 constexpr int kWParts = 8;     // split-K slices of dA / dBt (K = Hp -> Hpp / 8)
 constexpr int kLatParts = 32;  // split-K slices of dlatents' GEMM (K = 8192 -> 256)
 
 // Workspace layout (byte offsets), shared by the size query and the step.
 struct Layout {
   int64_t Hp, Hpp, kw, Bp, es;
-  int64_t E, Sx, X, P, H1, Y, G, Z, zbar, h1bar, row_seg, hparts, dmA, dmc, dZ, gpart, dG, dY, dH1, dP, dS, dX, dE;
+  int64_t E, Sx, X, P, H1, Y, G, Z, zbar, h1bar, row_seg, hparts, hsum, dmA, dmc, dZ, dZs, gpart, dG, dY, dH1, dP,
+      dS, dX, dE;
   int64_t dGT, YT, dH1T, PT, dST, XT, dmT, zbarT;
   int64_t WqT, W1T, W2T, WoT, WkvT, latn, latnT, KVp, KV, KVT, A, AT, BtT, Bt;
   int64_t gA, gBt, gA16, gAT16, gBt16, gBtT16, dKV, dKV16, dKVT16, dlat;
@@ -729,9 +712,10 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs) {
   L.Sx = take(Hp * D * es); L.X = take(Hp * D * es); L.P = take(Hp * S * es); L.H1 = take(Hp * D * es);
   L.Y = take(Hp * D * es); L.G = take(Hp * 2 * F * es); L.Z = take(Hp * F * es);
   L.zbar = take(Bp * F * es); L.h1bar = take(Bp * D * 4); L.row_seg = take(Hp * 4);
-  L.hparts = take((int64_t)kHParts * Bp * D * 4);
+  L.hparts = take((int64_t)kHParts * Bp * D * 4); L.hsum = take(Bp * D * 4);
   L.dmA = take(Bp * D * es); L.dmc = take(Bp * D * es); L.dZ = take((int64_t)kZParts * Bp * F * 4);
-  L.gpart = take(Bp * 2 * F * 4);
+  L.dZs = take(Bp * F * 4);
+  L.gpart = take((Hp + kGRows - 1) / kGRows * 2 * F * 4);
   L.dG = take(Hp * 2 * F * es); L.dY = take(Hp * D * es); L.dH1 = take(Hp * D * es);
   L.dP = take(Hp * S * es); L.dS = take(Hp * S * es); L.dX = take(Hp * D * es); L.dE = take(U * D * 4);
   L.dGT = take(2 * F * Hp * es); L.YT = take(D * Hp * es); L.dH1T = take(D * Hpp * es); L.PT = take(S * Hpp * es);
@@ -794,6 +778,8 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   float* h1bar = (float*)P_(L.h1bar);
   int32_t* row_seg = (int32_t*)P_(L.row_seg);
   float* hparts = (float*)P_(L.hparts);
+  float* hsum = (float*)P_(L.hsum);
+  float* dZs = (float*)P_(L.dZs);
   TA *dmA = (TA*)P_(L.dmA), *dmc = (TA*)P_(L.dmc);
   float* dZ = (float*)P_(L.dZ);
   float* gpart = (float*)P_(L.gpart);
@@ -892,8 +878,11 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     const int64_t ks = F / kHParts;
     GemmProblem p = {Bp, D, ks, zbar, F, ks, W2, F, ks, hparts, D, Bp * D, kHParts, 1.0f};
     if ((rc = gemm_group_dispatch(dt, NR_F32, &p, 1, st))) return rc;
+    TList t;  // the split-K partials summed in parallel (the head reads one row per batch row)
+    t.add(hparts, D, hsum, D, Bp, D, false, 0, kHParts, Bp * D);
+    if ((rc = launch_tlist<float, float>(t, st))) return rc;
   }
-  hipLaunchKernelGGL((head_kernel<TA>), dim3((unsigned)Bp), dim3(256), 0, st, B, Bp, kHParts, hparts, a.b2, h1bar,
+  hipLaunchKernelGGL((head_kernel<TA>), dim3((unsigned)Bp), dim3(256), 0, st, B, Bp, 1, hsum, a.b2, h1bar,
                      a.hist_off, E, (int64_t)D, a.pos, a.neg, a.margin, a.loss, a.users, dmA, dmc, dE, a.g_b2);
   NR_LT_CHECK("head");
   // ---- backward
@@ -903,10 +892,16 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     GemmProblem p = {Bp, F, ks, dmc, D, ks, W2T, D, ks, dZ, F, Bp * F, kZParts, 1.0f};
     if ((rc = gemm_group_dispatch(dt, NR_F32, &p, 1, st))) return rc;
   }
-  hipLaunchKernelGGL((geglu_bwd_kernel<TA>), dim3((unsigned)(B + 1), F / 2048), dim3(256), 0, st, B, a.hist_off, Hp,
-                     G, kZParts, dZ, Bp, dG, gpart);
+  {
+    TList t;
+    t.add(dZ, F, dZs, F, Bp, F, false, 0, kZParts, Bp * F);
+    if ((rc = launch_tlist<float, float>(t, st))) return rc;
+  }
+  const int64_t gchunks = (Hp + kGRows - 1) / kGRows;
+  hipLaunchKernelGGL((geglu_bwd_kernel<TA, kGRows>), dim3((unsigned)gchunks, F / 2048), dim3(256), 0, st, Hp, G, dZs,
+                     row_seg, dG, gpart);
   NR_LT_CHECK("geglu_bwd");
-  if ((rc = nr_col_sum(NR_F32, B, 2 * F, gpart, 2 * F, a.g_b1, st))) return rc;
+  if ((rc = nr_col_sum(NR_F32, gchunks, 2 * F, gpart, 2 * F, a.g_b1, st))) return rc;
   // fork: the weight grads of W1 (K = Hp, 128 tiles) and W2 on the side stream,
   // beside the data-grad GEMM dY = dG W1 (132 persistent workgroups) on this one
   if (hipEventRecord(side.fork, st) != hipSuccess || hipStreamWaitEvent(side.s, side.fork, 0) != hipSuccess) {
