@@ -67,6 +67,10 @@ extern "C" {
                            (acc + bias): SDPA's softmax over the 64 latents of
                            latent_attention.py:72 fused into the score GEMM
                            (needs N % 256 == 0, 16-byte aligned C rows)      */
+#define NR_EPI_SOFTMAX64_BWD 9 /* C = R * (acc - sum over the aligned run of 64 columns
+                           of R * acc): the backward of NR_EPI_SOFTMAX64 given its
+                           output R = P and acc = dP (latent training; bf16 in /
+                           out on the persistent kernel only)               */
 
 /* Library version (major*100 + minor). */
 int nr_version(void);

@@ -63,6 +63,7 @@ NR_EPI_GELU = 5
 NR_EPI_RELU_DROPOUT = 6
 NR_EPI_DRELU = 7
 NR_EPI_SOFTMAX64 = 8
+NR_EPI_SOFTMAX64_BWD = 9
 
 _p = ctypes.c_void_p
 _i = ctypes.c_int

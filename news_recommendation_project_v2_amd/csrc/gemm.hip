@@ -1117,8 +1117,8 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
       }
     }
     uint4 rq[8][2];
-    if constexpr (EPI == NR_EPI_RESADD) {
-      // residual in the store layout (16 B per lane), all loads up front
+    if constexpr (EPI == NR_EPI_RESADD || EPI == NR_EPI_SOFTMAX64_BWD) {
+      // residual (softmax backward: the softmax output P) in the store layout (16 B per lane), all loads up front
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi) {
         const int64_t row = min(row0 + 16 * mi, M - 1);
@@ -1171,6 +1171,34 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           }
         }
         float v[4][4];
+        if constexpr (EPI == NR_EPI_SOFTMAX64_BWD) {
+          // dS = P (dP - sum_group P dP): acc = dP, P from R in the accumulator layout;
+          // the wave's 64 columns are one softmax group (lanes l, l ^ 16, l ^ 32, l ^ 48)
+          float pv[4][4];
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const uint4 sw = swap_pair16(uint2{rq[mi][p].x, rq[mi][p].y}, uint2{rq[mi][p].z, rq[mi][p].w});
+            const uint32_t w[2][2] = {{sw.x, sw.y}, {sw.z, sw.w}};
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const uint32_t u = w[h][r >> 1];
+                pv[2 * p + h][r] = (r & 1) ? bf16_hi(u) : bf16_lo(u);
+              }
+          }
+          float dot = 0.f;
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dot = fmaf(pv[ni][r], acc[mi][ni][r], dot);
+          dot += __shfl_xor(dot, 16, 64);
+          dot += __shfl_xor(dot, 32, 64);
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[mi][ni][r] = pv[ni][r] * (acc[mi][ni][r] - dot);
+        }
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
@@ -1234,7 +1262,8 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           *reinterpret_cast<uint4*>(dst) = s0;
           *reinterpret_cast<uint4*>(dst + 32) = s1;
         }
-        if constexpr (EPI == NR_EPI_RESADD) __builtin_amdgcn_sched_barrier(0);  // row groups in load order
+        if constexpr (EPI == NR_EPI_RESADD || EPI == NR_EPI_SOFTMAX64_BWD)
+          __builtin_amdgcn_sched_barrier(0);  // row groups in load order
       }
     }
     if (!more) break;
@@ -1313,6 +1342,7 @@ static int launch_gemm256_t(int epi, int64_t M, int64_t N, int64_t K, const void
     case NR_EPI_GELU: NR_T(NR_EPI_GELU); break;
     case NR_EPI_RELU_DROPOUT: NR_T(NR_EPI_RELU_DROPOUT); break;
     case NR_EPI_SOFTMAX64: NR_T(NR_EPI_SOFTMAX64); break;
+    case NR_EPI_SOFTMAX64_BWD: NR_T(NR_EPI_SOFTMAX64_BWD); break;
     default: set_error("nr_gemm: bad epilogue %d", epi); return NR_ERR_INVALID;
   }
 #undef NR_T
@@ -1489,8 +1519,16 @@ int gemm_dispatch_ex(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N,
     return NR_ERR_UNSUPPORTED;
   }
   NR_CHECK_ARG(A && W && C, "nr_gemm: null operand");
-  NR_CHECK_ARG((epi != NR_EPI_RESADD && epi != NR_EPI_DRELU) || R, "nr_gemm: RESADD/DRELU need R");
-  NR_CHECK_ARG(epi >= NR_EPI_NONE && epi <= NR_EPI_SOFTMAX64, "nr_gemm: bad epilogue %d", epi);
+  NR_CHECK_ARG((epi != NR_EPI_RESADD && epi != NR_EPI_DRELU && epi != NR_EPI_SOFTMAX64_BWD) || R,
+               "nr_gemm: RESADD/DRELU/SOFTMAX64_BWD need R");
+  NR_CHECK_ARG(epi >= NR_EPI_NONE && epi <= NR_EPI_SOFTMAX64_BWD, "nr_gemm: bad epilogue %d", epi);
+  if (epi == NR_EPI_SOFTMAX64_BWD &&
+      !(dtype_in == NR_BF16 && dtype_out == NR_BF16 && N % G2BN == 0 && persistent_ok(M, N, K, lda, ldw) &&
+        ((uintptr_t)C & 15) == 0 && ldc % 8 == 0 && ((uintptr_t)R & 15) == 0 && ldr % 8 == 0)) {
+    set_error("nr_gemm: SOFTMAX64_BWD runs on the persistent bf16 kernel only (bf16 in/out, N %% 256, K >= 128, "
+              "16-byte aligned rows)");
+    return NR_ERR_UNSUPPORTED;
+  }
   const int64_t e16 = dtype_in == NR_F32 ? 4 : 8;  // elements per 16 B
   NR_CHECK_ARG(lda >= K && ldw >= K && lda % e16 == 0 && ldw % e16 == 0 &&
                    ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0,

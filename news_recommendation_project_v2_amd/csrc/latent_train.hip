@@ -108,6 +108,27 @@ __global__ __launch_bounds__(256) void zero_kernel(ZList z) {
       z.p[i][k] = 0.f;
 }
 
+// dst[i] = sum_p src[p * pstride + i] over n contiguous f32 (split-K partials), 4 per thread
+__global__ __launch_bounds__(256) void sum_parts_kernel(int64_t n4, int parts, int64_t pstride4,
+                                                        const float4* __restrict__ src, float4* __restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 v = src[i];
+    for (int p = 1; p < parts; ++p) {
+      const float4 w = src[p * pstride4 + i];
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+    dst[i] = v;
+  }
+}
+
+static int sum_parts(const float* src, int parts, int64_t pstride, float* dst, int64_t n, hipStream_t st) {
+  const int64_t n4 = n / 4, g = (n4 + 255) / 256;
+  hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, n4, parts,
+                     pstride / 4, (const float4*)src, (float4*)dst);
+  NR_CHECK_LAUNCH("nr_latent_train_step (sum_parts)");
+  return NR_OK;
+}
+
 // ------------------------------------------------------------------ forward rows
 // S = E[idx[row]], X = LN_q(S) (eps 1e-5); idx < 0 or row >= nvalid
 // (padding): both rows zero.  One wave per row, lane columns 256 j + 4 lane .. +3.
@@ -742,8 +763,8 @@ static int grid_rows(int64_t rows, int cap = 1024) {
 // data-grad chain) and its fork / join events: one set per host thread and
 // device, created on first use and kept (streams are reentrant per thread).
 struct Side {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipStream_t s = nullptr, s2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, fork2 = nullptr, join2 = nullptr;
 };
 static int side_stream(Side& out) {
   thread_local Side t_side[64];
@@ -755,8 +776,11 @@ static int side_stream(Side& out) {
   Side& sd = t_side[dev];
   if (!sd.s) {
     if (hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&sd.s2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sd.fork2, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sd.join2, hipEventDisableTiming) != hipSuccess) {
       set_error("nr_latent_train_step: cannot create the side stream / events");
       sd = Side{};
       return NR_ERR_HIP;
@@ -878,9 +902,8 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     const int64_t ks = F / kHParts;
     GemmProblem p = {Bp, D, ks, zbar, F, ks, W2, F, ks, hparts, D, Bp * D, kHParts, 1.0f};
     if ((rc = gemm_group_dispatch(dt, NR_F32, &p, 1, st))) return rc;
-    TList t;  // the split-K partials summed in parallel (the head reads one row per batch row)
-    t.add(hparts, D, hsum, D, Bp, D, false, 0, kHParts, Bp * D);
-    if ((rc = launch_tlist<float, float>(t, st))) return rc;
+    // the split-K partials summed in parallel (the head reads one row per batch row)
+    if ((rc = sum_parts(hparts, kHParts, Bp * D, hsum, Bp * D, st))) return rc;
   }
   hipLaunchKernelGGL((head_kernel<TA>), dim3((unsigned)Bp), dim3(256), 0, st, B, Bp, 1, hsum, a.b2, h1bar,
                      a.hist_off, E, (int64_t)D, a.pos, a.neg, a.margin, a.loss, a.users, dmA, dmc, dE, a.g_b2);
@@ -892,11 +915,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     GemmProblem p = {Bp, F, ks, dmc, D, ks, W2T, D, ks, dZ, F, Bp * F, kZParts, 1.0f};
     if ((rc = gemm_group_dispatch(dt, NR_F32, &p, 1, st))) return rc;
   }
-  {
-    TList t;
-    t.add(dZ, F, dZs, F, Bp, F, false, 0, kZParts, Bp * F);
-    if ((rc = launch_tlist<float, float>(t, st))) return rc;
-  }
+  if ((rc = sum_parts(dZ, kZParts, Bp * F, dZs, Bp * F, st))) return rc;
   const int64_t gchunks = (Hp + kGRows - 1) / kGRows;
   hipLaunchKernelGGL((geglu_bwd_kernel<TA, kGRows>), dim3((unsigned)gchunks, F / 2048), dim3(256), 0, st, Hp, G, dZs,
                      row_seg, dG, gpart);
@@ -930,12 +949,23 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   hipLaunchKernelGGL((ln_bwd_kernel<TA, 0>), dim3(grid_rows(Hp, 256)), dim3(256), 0, st, Hp, Hp, H1, a.nf_g, 1e-5f, dY,
                      dmc, row_seg, dH1, nullptr, (int64_t)0, a.g_nf_g, a.g_nf_b);
   NR_LT_CHECK("ln_f_bwd");
-  if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, S, D, dH1, D, BtT, D, nullptr, nullptr, 0, dP, S, st))) return rc;
-  {
+  if (dt == NR_BF16) {
+    // dS = P (dP - sum_group P dP) in the dP GEMM's epilogue (NR_EPI_SOFTMAX64_BWD, R = P)
+    if ((rc = gemm_dispatch(dt, dt, NR_EPI_SOFTMAX64_BWD, Hp, S, D, dH1, D, BtT, D, nullptr, Pm, S, dS, S, st)))
+      return rc;
+  } else {
+    if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, S, D, dH1, D, BtT, D, nullptr, nullptr, 0, dP, S, st)))
+      return rc;
     const int64_t g = (Hp * HEADS + 3) / 4;
     hipLaunchKernelGGL((softmax64_bwd_kernel<TA>), dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, Hp, Pm,
                        dP, dS);
     NR_LT_CHECK("softmax64_bwd");
+  }
+  // fork 2: dA / dBt and the whole fold backward need only dS, dH1, P, X from here on,
+  // so they run on a third stream beside dX, the scatter and the token LN grads
+  if (hipEventRecord(side.fork2, st) != hipSuccess || hipStreamWaitEvent(side.s2, side.fork2, 0) != hipSuccess) {
+    set_error("nr_latent_train_step: fork 2 failed");
+    return NR_ERR_HIP;
   }
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, S, dS, S, AT, S, nullptr, nullptr, 0, dX, D, st))) return rc;
   hipLaunchKernelGGL((ln_bwd_kernel<TA, 1>), dim3(grid_rows(Hp, 256)), dim3(256), 0, st, Hp, a.Hs, Sx, a.nq_g, 1e-5f,
@@ -944,6 +974,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   // token LayerNorm parameter grads from dE (history scatter + cosine grads)
   if ((rc = nr_ln_param_grad(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1e-12f, dE, D, a.g_tok_g, a.g_tok_b, st)))
     return rc;
+  hipStream_t s2 = side.s2;
   // ---- dA = dS^T X and dBt = dH1^T P as kWParts K-slices (16 + 16 tiles alone would hold 32 CUs
   // for a K = Hp tile time), summed while converting to the fold backward's operands
   {
@@ -952,13 +983,13 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     t.add(Pm, S, PT, Hpp, Hp, S, true, Hpp);
     t.add(dS, S, dST, Hpp, Hp, S, true, Hpp);
     t.add(X, D, XT, Hpp, Hp, D, true, Hpp);
-    if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
+    if ((rc = launch_tlist<TA, TA>(t, s2))) return rc;
     const int64_t kw = L.kw;
     GemmProblem p[2] = {
         {S, D, kw, dST, Hpp, kw, XT, Hpp, kw, gA, D, (int64_t)S * D, kWParts, 1.0f},
         {D, S, kw, dH1T, Hpp, kw, PT, Hpp, kw, gBt, S, (int64_t)D * S, kWParts, 1.0f},
     };
-    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, st))) return rc;
+    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, s2))) return rc;
   }
   // ---- fold backward
   {
@@ -967,7 +998,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     t.add(gA, D, gAT16, S, S, D, true, 0, kWParts, (int64_t)S * D);
     t.add(gBt, S, gBt16, S, D, S, false, 0, kWParts, (int64_t)D * S);
     t.add(gBt, S, gBtT16, D, D, S, true, 0, kWParts, (int64_t)D * S);
-    if ((rc = launch_tlist<float, TA>(t, st))) return rc;
+    if ((rc = launch_tlist<float, TA>(t, s2))) return rc;
   }
   {
     GemmProblem p[4] = {
@@ -980,13 +1011,13 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
         // dWo_h [1024, 512] = gBt_h V_h: A = gBt cols h*64 [1024, 64], W = VT rows h*512 [512, 64]
         {D, DH, NL, gBt16, S, NL, KVT + (int64_t)F * NL, NL, (int64_t)DH * NL, a.g_Wo, F, DH, HEADS, 1.0f},
     };
-    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 4, st))) return rc;
+    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 4, s2))) return rc;
   }
   {
     TList t;
     t.add(dKV, 2 * F, dKV16, 2 * F, NL, 2 * F, false);
     t.add(dKV, 2 * F, dKVT16, NL, NL, 2 * F, true);
-    if ((rc = launch_tlist<float, TA>(t, st))) return rc;
+    if ((rc = launch_tlist<float, TA>(t, s2))) return rc;
   }
   {
     const int64_t ks = 2 * F / kLatParts;
@@ -996,13 +1027,17 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
         // dlatn [64, 1024] = dKV Wkv, split-K: A = dKV16 cols, W = WkvT cols
         {NL, D, ks, dKV16, 2 * F, ks, WkvT, 2 * F, ks, dlat, D, (int64_t)NL * D, kLatParts, 1.0f},
     };
-    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, st))) return rc;
+    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, s2))) return rc;
   }
-  hipLaunchKernelGGL(lnc_bwd_kernel, dim3(NL / 4), dim3(256), 0, st, a.latents, a.nc_g, 1e-5f, kLatParts, dlat,
+  hipLaunchKernelGGL(lnc_bwd_kernel, dim3(NL / 4), dim3(256), 0, s2, a.latents, a.nc_g, 1e-5f, kLatParts, dlat,
                      a.g_latents, a.g_nc_g, a.g_nc_b);
   NR_LT_CHECK("ln_c_bwd");
+  if (hipEventRecord(side.join2, s2) != hipSuccess) {
+    set_error("nr_latent_train_step: join 2 record failed");
+    return NR_ERR_HIP;
+  }
   // join: the side stream's weight grads are done before anything later on `stream`
-  if (hipStreamWaitEvent(st, side.join, 0) != hipSuccess) {
+  if (hipStreamWaitEvent(st, side.join, 0) != hipSuccess || hipStreamWaitEvent(st, side.join2, 0) != hipSuccess) {
     set_error("nr_latent_train_step: join failed");
     return NR_ERR_HIP;
   }

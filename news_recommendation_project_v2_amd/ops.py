@@ -22,6 +22,7 @@ _EPI = {
     "resadd": _lib.NR_EPI_RESADD,
     "gelu": _lib.NR_EPI_GELU,
     "softmax64": _lib.NR_EPI_SOFTMAX64,
+    "softmax64_bwd": _lib.NR_EPI_SOFTMAX64_BWD,  # residual = the softmax output P
 }
 POOLERS = {"final": _lib.NR_POOL_FINAL, "latent": _lib.NR_POOL_LATENT, "mean": _lib.NR_POOL_MEAN}
 

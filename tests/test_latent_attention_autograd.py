@@ -275,3 +275,27 @@ def test_latent_train_step_bf16_close_to_f32(gpu_device, tmp_path):
         a, b = g32[k], g16[k]
         cos = float((a @ b) / (a.norm() * b.norm() + 1e-30))
         assert cos > 0.99, (k, cos)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [8320, 72023, 300])
+def test_gemm_softmax64_bwd_epilogue(gpu_device, M):
+    """NR_EPI_SOFTMAX64_BWD (the latent step's dP GEMM with the softmax backward
+    fused: dS = P (dP - sum over each head's 64 latents of P dP), bf16 in / out on
+    the persistent kernel) against torch on the same bf16 operands (f32 math):
+    within a few bf16 ulps of the row-group scale, incl. a ragged last tile."""
+    from news_recommendation_project_v2_amd import ops
+    g = torch.Generator(device=gpu_device).manual_seed(M)
+    a = (torch.randn(M, 1024, device=gpu_device, generator=g) * 0.05).bfloat16()
+    w = (torch.randn(512, 1024, device=gpu_device, generator=g) * 0.05).bfloat16()
+    logits = torch.randn(M, 8, 64, device=gpu_device, generator=g) * 2
+    P = torch.softmax(logits, -1).reshape(M, 512).bfloat16()
+    got = ops.gemm(a, w, None, epilogue="softmax64_bwd", residual=P)
+    dP = (a.float() @ w.float().T).reshape(M, 8, 64)
+    p = P.float().reshape(M, 8, 64)
+    want = (p * (dP - (p * dP).sum(-1, keepdim=True))).reshape(M, 512)
+    scale = want.abs().amax(1, keepdim=True).clamp_min(1e-6)
+    err = float(((got.float() - want).abs() / scale).max())
+    assert err <= 3e-2, err
+    with pytest.raises(Exception):
+        ops.gemm(a.float(), w.float(), None, epilogue="softmax64_bwd", residual=P.float())  # bf16 only
