@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void zero_kernel(ZList z) {
 
 // dst[i] = sum_p src[p * pstride + i] over n contiguous f32 (split-K partials), 4 per thread
 __global__ __launch_bounds__(256) void sum_parts_kernel(int64_t n4, int parts, int64_t pstride4,
-                                                        const float4* __restrict__ src, float4* __restrict__ dst) {
+                                                        const float4* src, float4* dst) {  // dst may alias src (in place)
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     float4 v = src[i];
     for (int p = 1; p < parts; ++p) {
@@ -993,11 +993,14 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   }
   // ---- fold backward
   {
+    // the K-slices summed in place into slice 0, then converted / transposed once each
+    if ((rc = sum_parts(gA, kWParts, (int64_t)S * D, gA, (int64_t)S * D, s2))) return rc;
+    if ((rc = sum_parts(gBt, kWParts, (int64_t)D * S, gBt, (int64_t)D * S, s2))) return rc;
     TList t;
-    t.add(gA, D, gA16, D, S, D, false, 0, kWParts, (int64_t)S * D);
-    t.add(gA, D, gAT16, S, S, D, true, 0, kWParts, (int64_t)S * D);
-    t.add(gBt, S, gBt16, S, D, S, false, 0, kWParts, (int64_t)D * S);
-    t.add(gBt, S, gBtT16, D, D, S, true, 0, kWParts, (int64_t)D * S);
+    t.add(gA, D, gA16, D, S, D, false);
+    t.add(gA, D, gAT16, S, S, D, true);
+    t.add(gBt, S, gBt16, S, D, S, false);
+    t.add(gBt, S, gBtT16, D, D, S, true);
     if ((rc = launch_tlist<float, TA>(t, s2))) return rc;
   }
   {
@@ -1029,7 +1032,8 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     };
     if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, s2))) return rc;
   }
-  hipLaunchKernelGGL(lnc_bwd_kernel, dim3(NL / 4), dim3(256), 0, s2, a.latents, a.nc_g, 1e-5f, kLatParts, dlat,
+  if ((rc = sum_parts(dlat, kLatParts, (int64_t)NL * D, dlat, (int64_t)NL * D, s2))) return rc;
+  hipLaunchKernelGGL(lnc_bwd_kernel, dim3(NL / 4), dim3(256), 0, s2, a.latents, a.nc_g, 1e-5f, 1, dlat,
                      a.g_latents, a.g_nc_g, a.g_nc_b);
   NR_LT_CHECK("ln_c_bwd");
   if (hipEventRecord(side.join2, s2) != hipSuccess) {
