@@ -98,6 +98,13 @@ int nr_set_persistent_workgroups(int n);
  * restore what it found. */
 int nr_persistent_workgroups(void);
 
+/* Half-tile tail of the persistent bf16 GEMM (on by default).  When the
+ * output tiles leave a last partial round of at most half the grid, those
+ * tiles run as 128-row halves, one per workgroup, so the round takes about
+ * half a tile's time.  A row's bits are the same either way (same K chain and
+ * epilogue per element): the switch exists for A/B timing.  Process-wide. */
+int nr_set_gemm_half_tail(int on);
+
 /* Thread-local message of the last failed call ("" if none). */
 const char* nr_last_error(void);
 

@@ -87,6 +87,7 @@ SIGNATURES = {
     "nr_is_device_pointer": (_i, [_p]),
     "nr_set_persistent_workgroups": (_i, [_i]),
     "nr_persistent_workgroups": (_i, []),
+    "nr_set_gemm_half_tail": (_i, [_i]),
     "nr_gemm": (_i, [_i, _i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, _p, _l, _p]),
     "nr_gemm_relu_dropout": (_i, [_i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, ctypes.c_uint64, _f, _p]),
     "nr_gemm_drelu": (_i, [_i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _l, _p, _l, _f, _p]),

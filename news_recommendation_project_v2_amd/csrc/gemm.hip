@@ -852,7 +852,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
                                                           const __bf16* __restrict__ W, int64_t ldw,
                                                           const float* __restrict__ bias, const __bf16* R,
                                                           int64_t ldr, __bf16* C, int64_t ldc, EpiArgs ea,
-                                                          int ntn, int ntm, int n_tiles) {
+                                                          int ntn, int ntm, int n_tiles, int n_half) {
   constexpr int BK = 64;
   // operand stages + one 256-B bias slice per wave (LDS-DMA'd with the tile's step 0)
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE + 8 * 256 + (LNF ? 2 * kLnSlot : 0)];
@@ -878,11 +878,28 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     t_end = n_tiles;
     t_step = G;
   }
-  if (t >= t_end) return;  // workgroup-uniform
-  auto tile_base = [&](int tile, uint32_t& mb, uint32_t& nb) {
-    int mt, nt;
+  // Units: full tiles 0 .. n_tiles - 1 (whole rounds of the grid), then the
+  // tiles of the last partial round cut into 128-row halves, unit n_tiles + h
+  // = half h & 1 of tile n_tiles + h / 2, one per workgroup h < n_half
+  // (host: only when they fit one round).  A half is computed by wave group
+  // 0 alone (rows mb .. mb + 127) with the same per-element K chain and
+  // epilogue as a full tile, so every row's bits are independent of the cut;
+  // group 1 keeps its barriers and DMA pieces and skips reads, MFMAs and
+  // stores.  The tail round then takes a half tile's time instead of a
+  // tile's (at M = 72,023, N = 1024: 4 rounds + 208 halves, not 5 rounds).
+  const int hb = (int)blockIdx.x < n_half ? n_tiles + (int)blockIdx.x : -1;
+  int u = t < t_end ? t : hb;
+  if (u < 0) return;  // workgroup-uniform
+  auto next_unit = [&](int cur) { return cur < n_tiles ? (cur + t_step < t_end ? cur + t_step : hb) : -1; };
+  auto tile_base = [&](int unit, uint32_t& mb, uint32_t& nb) {
+    int mt, nt, tile = unit;
+    uint32_t off = 0;
+    if (unit >= n_tiles) {
+      tile = n_tiles + ((unit - n_tiles) >> 1);
+      off = (uint32_t)((unit - n_tiles) & 1) * (G2BM / 2);
+    }
     tile_of(tile, ntn, ntm, ea.group_m, mt, nt);
-    mb = (uint32_t)mt * G2BM;
+    mb = (uint32_t)mt * G2BM + off;
     nb = (uint32_t)nt * G2BN;
   };
 
@@ -1000,7 +1017,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   __builtin_amdgcn_sched_barrier(0);                   \
   __builtin_amdgcn_s_barrier();                        \
   __builtin_amdgcn_s_setprio(1);                       \
-  mma(QM, NI, FB);                                     \
+  if constexpr (!IDLE) mma(QM, NI, FB);               \
   __builtin_amdgcn_s_setprio(0);                       \
   __builtin_amdgcn_s_barrier();
   // K step kt of the current tile (stage st).  Step kt + 2 is prefetched into
@@ -1016,14 +1033,21 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   // latent / FinalAttention transforms at M = 72,023 (profiles/round3/s4/).
   bool a1p = false;  // the previous step's A1 refill (stage st ^ 1, step a1k), issued in this step's P1
   int a1k = 0;
-  auto kstep = [&](int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {
+  // IDLE: wave group 1 in a half unit -- the same barriers and DMA pieces, no
+  // fragment reads or MFMAs.  A separate loop after the unit loop (a half unit
+  // is a workgroup's last): a runtime branch inside the unit loop costs the
+  // main loop its register allocation (spills)
+  auto kstep = [&](auto idle, int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {
+    constexpr bool IDLE = decltype(idle)::value;
     const bool pf = kt + 2 < nk || more;
     const int kf = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
-    readA(st, 0);
-    readB(st, 0, fb0);
+    if constexpr (!IDLE) {
+      readA(st, 0);
+      readB(st, 0, fb0);
+    }
     if (a1p) dmaA(1, st ^ 1, a1k);
     NR_PHASE_SYNC_MMA(0, 0, fb0)
-    readB(st, 1, fb1);
+    if constexpr (!IDLE) readB(st, 1, fb1);
     if (pf) {
       if (kt + 2 == nk) {
         set_offA(nm0);
@@ -1033,7 +1057,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
       dmaA(0, st, kf);
     }
     NR_PHASE_SYNC_MMA(0, 1, fb1)
-    readA(st, 1);
+    if constexpr (!IDLE) readA(st, 1);
     if (pf) dmaB(0, st, kf);
     NR_PHASE_SYNC_MMA(1, 1, fb1)
     if (pf) {
@@ -1051,13 +1075,13 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     a1k = kf;
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
-    mma(1, 0, fb0);
+    if constexpr (!IDLE) mma(1, 0, fb0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   };
 
   uint32_t m0, n0;
-  tile_base(t, m0, n0);
+  tile_base(u, m0, n0);
   set_offA(m0);
   set_offB(n0);
   // first tile: LN slices, bias slice + steps 0 and 1 (stages 0 and 1)
@@ -1075,8 +1099,9 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   if (wmu == 1) __builtin_amdgcn_s_barrier();  // skew the wave groups by one barrier
   int st = 0;
   while (true) {
-    const int tn = t + t_step;
-    const bool more = tn < t_end;
+    const int tn = next_unit(u);
+    const bool more = tn >= 0;
+    if (u >= n_tiles && wmu == 1) break;  // group 1 of a half unit: below
     uint32_t nm0 = 0, nn0 = 0;
     if (more) tile_base(tn, nm0, nn0);
     // the accumulators start at the bias (acc = bias + A.W^T); this wave's
@@ -1090,11 +1115,12 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = b4[ni];
     for (int kt = 0; kt < nk; ++kt) {
-      kstep(kt, st, more, nm0, nn0);
+      kstep(std::false_type{}, kt, st, more, nm0, nn0);
       st ^= 1;
     }
 
     if (wmu == 0) __builtin_amdgcn_s_barrier();  // realign: group 1 has finished its last MFMA phase
+    {
     // ---------------- epilogue of tile (m0, n0) ----------------
     // The next tile's first stage is resident or in flight; nothing here
     // touches LDS or waits on the operand DMAs.  Rows past M are clamped to
@@ -1266,12 +1292,19 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           __builtin_amdgcn_sched_barrier(0);  // row groups in load order
       }
     }
+    }
     if (!more) break;
     if (wmu == 1) __builtin_amdgcn_s_barrier();  // re-skew
     lslot ^= 1;
-    t = tn;
+    u = tn;
     m0 = nm0;
     n0 = nn0;
+  }
+  if (u >= n_tiles && wmu == 1) {  // the half unit's K loop for group 1 (its last unit: nothing to prefetch)
+    for (int kt = 0; kt < nk; ++kt) {
+      kstep(std::true_type{}, kt, st, false, 0u, 0u);
+      st ^= 1;
+    }
   }
 #undef NR_PHASE_SYNC_MMA
 }
@@ -1311,6 +1344,26 @@ static int num_cus() {
 
 // The persistent kernel's operand stream needs >= 2 K steps per tile and
 // addresses A and W through 32-bit buffer offsets.
+// Half-tile tail (gemm256t_kernel's units): on unless a tuning caller turned it off.
+static std::atomic<int> g_half_tail{1};
+
+extern "C" int nr_set_gemm_half_tail(int on) {
+  g_half_tail.store(on ? 1 : 0);
+  return NR_OK;
+}
+
+// Persistent grid over `tiles` output tiles: *nt full tiles (whole rounds)
+// and *nh half units (the last partial round's tiles cut in two, when they
+// fit one round); returns the workgroup count.
+static int persistent_schedule(int64_t tiles, int* nt, int* nh) {
+  const int ncu = num_cus();
+  const int rem = (int)(tiles % ncu);
+  const bool split = g_half_tail.load() && rem > 0 && 2 * rem <= ncu;
+  *nt = (int)tiles - (split ? rem : 0);
+  *nh = split ? 2 * rem : 0;
+  return *nt >= ncu ? ncu : (*nt > *nh ? *nt : *nh);
+}
+
 static bool persistent_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldw) {
   constexpr int64_t kMax = 0xFFFFFFFFll;
   return K >= 128 && M * lda * 2 <= kMax && N * ldw * 2 <= kMax;
@@ -1326,13 +1379,13 @@ static int launch_gemm256_t(int epi, int64_t M, int64_t N, int64_t K, const void
     set_error("nr_gemm: too many tiles");
     return NR_ERR_UNSUPPORTED;
   }
-  const int nt = (int)tiles, ncu = num_cus();
-  const dim3 grid((unsigned)(nt < ncu ? nt : ncu));
+  int nt, nh;
+  const dim3 grid((unsigned)persistent_schedule(tiles, &nt, &nh));
   const __bf16* a = (const __bf16*)A;
   const __bf16* w = (const __bf16*)W;
   const __bf16* r = (const __bf16*)R;
   __bf16* c = (__bf16*)C;
-#define NR_T(E) hipLaunchKernelGGL((gemm256t_kernel<E>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea, ntn, (int)ntm, nt)
+#define NR_T(E) hipLaunchKernelGGL((gemm256t_kernel<E>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea, ntn, (int)ntm, nt, nh)
   switch (epi) {
     case NR_EPI_NONE: NR_T(NR_EPI_NONE); break;
     case NR_EPI_RELU: NR_T(NR_EPI_RELU); break;
@@ -1456,8 +1509,8 @@ int gemm_lnfold_dispatch(int epi, int64_t M, int64_t N, int64_t K, const void* A
   const int ntn = (int)(N / G2BN);
   const int64_t ntm = (M + G2BM - 1) / G2BM;
   NR_CHECK_ARG(ntm * ntn <= (1ll << 30), "nr_gemm_lnfold: too many tiles");
-  const int nt = (int)(ntm * ntn), ncu = num_cus();
-  const dim3 grid((unsigned)(nt < ncu ? nt : ncu));
+  int nt, nh;
+  const dim3 grid((unsigned)persistent_schedule(ntm * ntn, &nt, &nh));
   EpiArgs ea{0, 0, 1.f};
   ea.group_m = kGemmGroupM;
   ea.ln_stats = stats;
@@ -1467,10 +1520,10 @@ int gemm_lnfold_dispatch(int epi, int64_t M, int64_t N, int64_t K, const void* A
   __bf16* c = (__bf16*)C;
   if (epi == NR_EPI_GEGLU)
     hipLaunchKernelGGL((gemm256t_kernel<NR_EPI_GEGLU, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, nullptr,
-                       nullptr, 0, c, ldc, ea, ntn, (int)ntm, nt);
+                       nullptr, 0, c, ldc, ea, ntn, (int)ntm, nt, nh);
   else
     hipLaunchKernelGGL((gemm256t_kernel<NR_EPI_SOFTMAX64, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw,
-                       nullptr, nullptr, 0, c, ldc, ea, ntn, (int)ntm, nt);
+                       nullptr, nullptr, 0, c, ldc, ea, ntn, (int)ntm, nt, nh);
   NR_CHECK_LAUNCH("nr_gemm_lnfold");
   return NR_OK;
 }

@@ -73,6 +73,12 @@ def persistent_workgroups() -> int:
     return int(_lib.load().nr_persistent_workgroups())
 
 
+def set_gemm_half_tail(on: bool = True) -> None:
+    """Half-tile tail of the persistent bf16 GEMM (default on; bit-identical
+    either way -- the switch is for A/B timing)."""
+    _lib.call("nr_set_gemm_half_tail", int(bool(on)))
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
          epilogue: str = "none", residual: Optional[torch.Tensor] = None,
          out: Optional[torch.Tensor] = None, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:

@@ -80,7 +80,7 @@ def _calls(P):
 
 def test_every_entry_with_pointers_is_covered():
     """The table below names every header entry that takes a device pointer."""
-    no_ptr = {"nr_version", "nr_build_hash", "nr_init", "nr_last_error", "nr_set_persistent_workgroups",
+    no_ptr = {"nr_version", "nr_build_hash", "nr_init", "nr_last_error", "nr_set_persistent_workgroups", "nr_set_gemm_half_tail",
               "nr_persistent_workgroups", "nr_final_attn_workspace_bytes", "nr_latent_workspace_bytes",
               "nr_encoder_workspace_bytes", "nr_residency_flush", "nr_is_device_pointer",
               # communicator handles (tests/test_comm.py)

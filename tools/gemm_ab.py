@@ -6,6 +6,10 @@ check of every build against a float64 reference on sampled rows.
 
     python tools/gemm_ab.py [--m 72023] [--libs name=path ...] [--rounds 5]
 
+A library given as name=path:notail runs with its half-tile tail switched off
+(nr_set_gemm_half_tail(0) around each call), so one build can be A/B'd
+against itself.
+
 Tool only: each library is loaded with ctypes straight from its path (the
 product loader, news_recommendation_project_v2_amd/_lib.py, always loads the
 in-tree libnewsrec_hip.so).
@@ -47,7 +51,17 @@ def load(path):
     return lib
 
 
-def run(lib, a, w, b, epi, r, out):
+def run(lib, a, w, b, epi, r, out, tail=True):
+    if not tail:
+        lib.nr_set_gemm_half_tail(0)
+    try:
+        _run(lib, a, w, b, epi, r, out)
+    finally:
+        if not tail:
+            lib.nr_set_gemm_half_tail(1)
+
+
+def _run(lib, a, w, b, epi, r, out):
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
     rc = lib.nr_gemm(1, 1, EPI[epi], a.shape[0], w.shape[0], a.shape[1], p(a), a.shape[1], p(w), w.shape[1], p(b),
@@ -82,7 +96,11 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--shapes", default="")
     args = ap.parse_args()
-    libs = {kv.split("=", 1)[0]: load(kv.split("=", 1)[1]) for kv in args.libs}
+    libs, tails = {}, {}
+    for kv in args.libs:
+        lab, path = kv.split("=", 1)
+        tails[lab] = not path.endswith(":notail")
+        libs[lab] = load(path[:-len(":notail")] if path.endswith(":notail") else path)
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     summary = []
@@ -100,10 +118,11 @@ def main():
         ref = reference_rows(a, w, b, epi, r, rows)
         err = {}
         for lab, lib in libs.items():
-            run(lib, a, w, b, epi, r, outs[lab])
+            run(lib, a, w, b, epi, r, outs[lab], tails[lab])
             torch.cuda.synchronize()
             err[lab] = float((outs[lab][rows].double() - ref).abs().max())
-        fns = {lab: (lambda lib=lib, o=outs[lab]: run(lib, a, w, b, epi, r, o)) for lab, lib in libs.items()}
+        fns = {lab: (lambda lib=lib, o=outs[lab], tl=tails[lab]: run(lib, a, w, b, epi, r, o, tl))
+               for lab, lib in libs.items()}
         fns["torch"] = lambda: torch.matmul(a, w.T)
         # the same op as a hipBLASLt user runs it: addmm (bias in the GEMM) + torch's epilogue kernels
         b16 = b.to(torch.bfloat16)
