@@ -838,7 +838,7 @@ __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t v) {  // v_pk_max_i16 w
 // not inline asm, so the compiler's own wait insertion sees them: it then knows
 // the older stores have retired and keeps its waits for the epilogue's
 // residual loads counted instead of vmcnt(0).
-constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt8 = 0x0F78, kVmcnt6 = 0x0F76, kVmcnt9 = 0x0F79;
+constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt4 = 0x0F74, kVmcnt8 = 0x0F78, kVmcnt6 = 0x0F76, kVmcnt9 = 0x0F79;  // lgkmcnt/expcnt left at max
 
 // LNF (LayerNorm folded into the epilogue): per tile, every wave's (u, c)
 // column slices (2 x 256 B) and the tile's 256 row stats (2 KiB), in two
@@ -856,9 +856,10 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   constexpr int BK = 64;
   // operand stages + one 256-B bias slice per wave (LDS-DMA'd with the tile's step 0)
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE + 8 * 256 + (LNF ? 2 * kLnSlot : 0)];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave-derived values are scalars (readfirstlane): VGPRs are the kernel's limit
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
-  const int wmu = __builtin_amdgcn_readfirstlane(wm);
+  const int wmu = wm;
   const int nk = (int)(K / BK);  // >= 2 (host)
 
   // tile schedule: XCD group x = blockIdx % 8 owns a contiguous range of tile
@@ -913,40 +914,46 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     const int n = __builtin_amdgcn_readfirstlane((int)(bytes > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)bytes));
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
   };
-  const __amdgpu_buffer_rsrc_t rA = rsrc(A, M * lda * 2), rW = rsrc(W, N * ldw * 2);
+  // per-tile descriptors: A from the unit's first row (its range = the rows
+  // left, so rows past M fail the range check on the VGPR offset alone and
+  // read zeros), W from the tile's first column; the per-lane offsets below
+  // are then the same for every tile
+  __amdgpu_buffer_rsrc_t rA, rW;
+  // (a half unit may start past M: no records then)
+  auto set_tileA = [&](uint32_t mb) { rA = rsrc(A + (int64_t)mb * lda, max(M - (int64_t)mb, (int64_t)0) * lda * 2); };
+  auto set_tileB = [&](uint32_t nb) { rW = rsrc(W + (int64_t)nb * ldw, (N - (int64_t)nb) * ldw * 2); };
   // DMA units are the quarters the phases finish reading: A unit q = rows
   // 64 q .. +63 of both wave-group halves (lane l of wave w: row
   // 128 (w >> 2) + 64 q + 16 (w & 3) + 8 j + l / 8), B unit q = rows 32 q .. +31
   // of all four wn slices (row 64 (w >> 1) + 32 q + 16 (w & 1) + 8 j + l / 8);
   // 16-B chunk (l & 7) ^ ((row >> 1) & 7) of the LDS image (T2 swizzle on the
-  // source); rows past M are clamped to M - 1 (never stored)
+  // source).  Per-lane offsets relative to the tile's descriptors, fixed for
+  // the whole launch: A per (unit, j) (a row past M must fail the range check
+  // on its own VGPR offset), B per j with the unit's 32 rows in the scalar
+  // offset (W rows are always in range).  Rows past M are never stored.
   const int qa = (wave >> 2) * 128 + (wave & 3) * 16, qb = (wave >> 1) * 64 + (wave & 1) * 16;
   const uint32_t ldab = (uint32_t)lda * 2, ldwb = (uint32_t)ldw * 2, mlast = (uint32_t)(M - 1);
   auto chunk = [&](int j) { return (uint32_t)(((lane & 7) ^ ((4 * j + (lane >> 4)) & 7)) * 16); };
-  uint32_t oA[2][2], oB[2][2];
-  auto set_offA = [&](uint32_t mb) {
+  uint32_t oA[2][2], oB[2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) oA[h][j] = min(mb + (uint32_t)(qa + 64 * h + 8 * j + (lane >> 3)), mlast) * ldab + chunk(j);
-  };
-  auto set_offB = [&](uint32_t nb) {
+    for (int j = 0; j < 2; ++j) oA[h][j] = (uint32_t)(qa + 64 * h + 8 * j + (lane >> 3)) * ldab + chunk(j);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) oB[h][j] = (nb + (uint32_t)(qb + 32 * h + 8 * j + (lane >> 3))) * ldwb + chunk(j);
-  };
+  for (int j = 0; j < 2; ++j) oB[j] = (uint32_t)(qb + 8 * j + (lane >> 3)) * ldwb + chunk(j);
   auto dmaA = [&](int h, int stage, int kt) {
     unsigned char* sa = smem + stage * G2_STAGE + (qa + 64 * h) * 128;
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)kt * (BK * 2));
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sa + 8 * j * 128), 16, oA[h][j], kt * (BK * 2), 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(sa + 8 * j * 128), 16, oA[h][j], so, 0, 0);
   };
   auto dmaB = [&](int h, int stage, int kt) {
     unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128 + (qb + 32 * h) * 128;
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)kt * (BK * 2) + (uint32_t)h * 32u * ldwb);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(sb + 8 * j * 128), 16, oB[h][j], kt * (BK * 2), 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (lds_void*)(sb + 8 * j * 128), 16, oB[j], so, 0, 0);
   };
   unsigned char* bias_lds = smem + 2 * G2_STAGE + wave * 256;  // this wave's 64 bias floats
   // (a buffer op like the operands: a global_load_lds here would be a FLAT
@@ -982,7 +989,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   const int bbase = G2BM * 128 + (wn * 64 + c16) * 128;
   const int cf0 = ((0 + q4) ^ sw) << 4, cf1 = ((4 + q4) ^ sw) << 4;
   typedef f32x4 frag_t;
-  frag_t fa[4][2], fb0[2][2], fb1[2][2];  // [row tile][k half]
+  frag_t fa[4][2], fbx[2][2], fby[2][2];  // [row tile][k half]; B fragments in two alternating sets
   f32x4 acc[8][4];
   auto readA = [&](int stage, int qm) {
     const unsigned char* sp = smem + stage * G2_STAGE + abase + qm * 4 * 2048;
@@ -1024,34 +1031,35 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   // this stage, each quarter at least one phase after its last read (both
   // wave groups' reads of phase p retire before the barrier instance the
   // leading group passes to enter phase p + 1), two 1-KiB pieces per wave in
-  // every phase: A0 in P2 (read in P1), B0 in P3 (read in P1), B1 in P4 (read
-  // in P2), and A1 (read in P3) in the NEXT step's P1 -- this tile's step, or
-  // past its end the next tile's steps 0 and 1 (with the next tile's bias
-  // slice ahead of step 0).  P4 then waits for step kt + 1 (its A1 issued in
-  // this step's P1) with 6 pieces of step kt + 2 in flight.  Round 3: the even
-  // spread (was P2: A0 + B0, P3: B1, P4: A1) is 1.5 % / 2.6 % faster on the
-  // latent / FinalAttention transforms at M = 72,023 (profiles/round3/s4/).
+  // every phase: A0 in P2 (read in P1), B0 in P3 (read in the previous step's
+  // P4), B1 in P4 (read in P2), and A1 (read in P3) in the NEXT step's P1 --
+  // this tile's step, or past its end the next tile's steps 0 and 1 (with the
+  // next tile's bias slice ahead of step 0).  P4 then waits for step kt + 1
+  // (its A1 issued in this step's P1) with 6 pieces of step kt + 2 in flight.
+  // Fragment reads per phase 8 / 4 / 8 / 4 (round 4; was 12 / 4 / 8 / 0): P4
+  // reads step kt + 1's B0 into the B set P3 has finished with, so the two B
+  // sets swap roles every step (B0 in fbx on even steps, in fby on odd ones);
+  // P3 waits (vmcnt 8) for step kt + 1's B0, issued in step kt - 1's P3, so
+  // that P4 reads it one phase after the wait.  A tile's step-0 B0 is read at
+  // the tile top (retired by the previous tile's last P4 wait, or the
+  // prologue's, and a barrier since) and its last step reads none in P4, so no
+  // fragments live across the epilogue.
   bool a1p = false;  // the previous step's A1 refill (stage st ^ 1, step a1k), issued in this step's P1
   int a1k = 0;
-  // IDLE: wave group 1 in a half unit -- the same barriers and DMA pieces, no
-  // fragment reads or MFMAs.  A separate loop after the unit loop (a half unit
-  // is a workgroup's last): a runtime branch inside the unit loop costs the
-  // main loop its register allocation (spills)
-  auto kstep = [&](auto idle, int kt, int st, bool more, uint32_t nm0, uint32_t nn0) {
+  // fb0: this step's B0 (rows qn = 0); fb1: its B1, then step kt + 1's B0
+  auto kstep = [&](auto idle, int kt, int st, bool more, uint32_t nm0, uint32_t nn0, frag_t(&fb0)[2][2],
+                   frag_t(&fb1)[2][2]) __attribute__((always_inline)) {
     constexpr bool IDLE = decltype(idle)::value;
     const bool pf = kt + 2 < nk || more;
     const int kf = kt + 2 < nk ? kt + 2 : kt + 2 - nk;
-    if constexpr (!IDLE) {
-      readA(st, 0);
-      readB(st, 0, fb0);
-    }
+    if constexpr (!IDLE) readA(st, 0);
     if (a1p) dmaA(1, st ^ 1, a1k);
     NR_PHASE_SYNC_MMA(0, 0, fb0)
     if constexpr (!IDLE) readB(st, 1, fb1);
     if (pf) {
       if (kt + 2 == nk) {
-        set_offA(nm0);
-        set_offB(nn0);
+        set_tileA(nm0);
+        set_tileB(nn0);
         dma_bias(nn0);
       }
       dmaA(0, st, kf);
@@ -1059,7 +1067,17 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     NR_PHASE_SYNC_MMA(0, 1, fb1)
     if constexpr (!IDLE) readA(st, 1);
     if (pf) dmaB(0, st, kf);
+    // step kt + 1's B0 landed (read in P4): issued after it are its B1 and A1
+    // and, when pf, step kt + 2's A0 and B0 (2 instructions each; a bias or LN
+    // DMA among them only makes the wait stricter)
+    if (pf)
+      __builtin_amdgcn_s_waitcnt(kVmcnt8);
+    else
+      __builtin_amdgcn_s_waitcnt(kVmcnt4);
     NR_PHASE_SYNC_MMA(1, 1, fb1)
+    if constexpr (!IDLE) {
+      if (kt + 1 < nk) readB(st ^ 1, 0, fb1);
+    }
     if (pf) {
       dmaB(1, st, kf);
       if (LNF && kt + 2 == nk) {
@@ -1073,17 +1091,26 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     }
     a1p = pf;
     a1k = kf;
+    __builtin_amdgcn_sched_barrier(0);  // the B0 reads stay ahead of the MFMA cluster (not waited for: P4's MFMAs do not use them)
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
     if constexpr (!IDLE) mma(1, 0, fb0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   };
+  // a tile's K loop: steps in (even, odd) pairs (nk even, host), B0 in fbx on
+  // even steps; every tile starts on stage 0
+  auto kloop = [&](auto idle, bool more, uint32_t nm0, uint32_t nn0) __attribute__((always_inline)) {
+    for (int kt = 0; kt < nk; kt += 2) {
+      kstep(idle, kt, 0, more, nm0, nn0, fbx, fby);
+      kstep(idle, kt + 1, 1, more, nm0, nn0, fby, fbx);
+    }
+  };
 
   uint32_t m0, n0;
   tile_base(u, m0, n0);
-  set_offA(m0);
-  set_offB(n0);
+  set_tileA(m0);
+  set_tileB(n0);
   // first tile: LN slices, bias slice + steps 0 and 1 (stages 0 and 1)
   dma_ln(0, m0, n0);
   dma_bias(n0);
@@ -1097,7 +1124,6 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
   __builtin_amdgcn_s_waitcnt(kVmcnt8);
   __builtin_amdgcn_s_barrier();
   if (wmu == 1) __builtin_amdgcn_s_barrier();  // skew the wave groups by one barrier
-  int st = 0;
   while (true) {
     const int tn = next_unit(u);
     const bool more = tn >= 0;
@@ -1114,10 +1140,8 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = b4[ni];
-    for (int kt = 0; kt < nk; ++kt) {
-      kstep(std::false_type{}, kt, st, more, nm0, nn0);
-      st ^= 1;
-    }
+    readB(0, 0, fbx);  // step 0's B0
+    kloop(std::false_type{}, more, nm0, nn0);
 
     if (wmu == 0) __builtin_amdgcn_s_barrier();  // realign: group 1 has finished its last MFMA phase
     {
@@ -1132,26 +1156,23 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     const int64_t col0 = (int64_t)n0 + wn * 64;          // this wave's 64 columns
     const int qo = 16 * (q4 & 1) + 8 * (q4 >> 1);        // lane's 8 columns after swap_pair16
     // LNF: this lane's 16 columns' (u, c) and the tile's row stats (slot lslot)
-    f32x4 lu[4], lc[4];
+    // (re-read from LDS per row group: 32 VGPRs held across the epilogue spilled)
     const unsigned char* ln_st = ln_lds + lslot * kLnSlot + 8 * 512;
-    if constexpr (LNF) {
-      const unsigned char* uc = ln_lds + lslot * kLnSlot + wave * 512;
+    const unsigned char* ln_uc = ln_lds + lslot * kLnSlot + wave * 512;
+    // residual (softmax backward: the softmax output P) in the store layout (16
+    // B per lane): a window of 4 row groups in flight, row group mi + 4 loaded
+    // into mi's slot once mi is stored (all 8 up front held 64 VGPRs beside the
+    // accumulators and spilled)
+    uint4 rq[4][2];
+    auto load_r = [&](int mi) {
+      const int64_t row = min(row0 + 16 * mi, M - 1);
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        lu[ni] = *reinterpret_cast<const f32x4*>(uc + (16 * ni + 4 * q4) * 4);
-        lc[ni] = *reinterpret_cast<const f32x4*>(uc + 256 + (16 * ni + 4 * q4) * 4);
-      }
-    }
-    uint4 rq[8][2];
+      for (int p = 0; p < 2; ++p) rq[mi & 3][p] = *reinterpret_cast<const uint4*>(R + row * ldr + col0 + 32 * p + qo);
+      __builtin_amdgcn_sched_barrier(0);  // issue order = use order: counted waits, not vmcnt(0)
+    };
     if constexpr (EPI == NR_EPI_RESADD || EPI == NR_EPI_SOFTMAX64_BWD) {
-      // residual (softmax backward: the softmax output P) in the store layout (16 B per lane), all loads up front
 #pragma unroll
-      for (int mi = 0; mi < 8; ++mi) {
-        const int64_t row = min(row0 + 16 * mi, M - 1);
-#pragma unroll
-        for (int p = 0; p < 2; ++p) rq[mi][p] = *reinterpret_cast<const uint4*>(R + row * ldr + col0 + 32 * p + qo);
-        __builtin_amdgcn_sched_barrier(0);  // issue order = use order: counted waits vmcnt(14), not (0)
-      }
+      for (int mi = 0; mi < 4; ++mi) load_r(mi);
     }
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
@@ -1159,11 +1180,15 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
       const bool live = row0 + 16 * mi < M;  // clamped duplicates of row M - 1 never store
       if constexpr (LNF) {
         // LN(a) . w = rstd (a . (w o gamma) - mean u) + c   (row stats of the A row)
+        asm volatile("" ::: "memory");  // no CSE of the (u, c) reads across row groups
         const float2 ms = *reinterpret_cast<const float2*>(ln_st + (wm * 128 + c16 + 16 * mi) * 8);
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
+        for (int ni = 0; ni < 4; ++ni) {
+          const f32x4 lu = *reinterpret_cast<const f32x4*>(ln_uc + (16 * ni + 4 * q4) * 4);
+          const f32x4 lc = *reinterpret_cast<const f32x4*>(ln_uc + 256 + (16 * ni + 4 * q4) * 4);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[mi][ni][r] = fmaf(ms.y, fmaf(-ms.x, lu[ni][r], acc[mi][ni][r]), lc[ni][r]);
+          for (int r = 0; r < 4; ++r) acc[mi][ni][r] = fmaf(ms.y, fmaf(-ms.x, lu[r], acc[mi][ni][r]), lc[r]);
+        }
       }
       if constexpr (EPI == NR_EPI_GEGLU) {
         // W rows interleaved in 32-row (a, g) blocks: ni 0, 1 = a, ni 2, 3 = g
@@ -1185,7 +1210,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           // the residual to the accumulator layout by the same (involutive) swap
 #pragma unroll
           for (int p = 0; p < 2; ++p) {
-            const uint4 s = swap_pair16(uint2{rq[mi][p].x, rq[mi][p].y}, uint2{rq[mi][p].z, rq[mi][p].w});
+            const uint4 s = swap_pair16(uint2{rq[mi & 3][p].x, rq[mi & 3][p].y}, uint2{rq[mi & 3][p].z, rq[mi & 3][p].w});
             const uint32_t w[2][2] = {{s.x, s.y}, {s.z, s.w}};  // tile 2p, tile 2p + 1
 #pragma unroll
             for (int h = 0; h < 2; ++h)
@@ -1203,7 +1228,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           float pv[4][4];
 #pragma unroll
           for (int p = 0; p < 2; ++p) {
-            const uint4 sw = swap_pair16(uint2{rq[mi][p].x, rq[mi][p].y}, uint2{rq[mi][p].z, rq[mi][p].w});
+            const uint4 sw = swap_pair16(uint2{rq[mi & 3][p].x, rq[mi & 3][p].y}, uint2{rq[mi & 3][p].z, rq[mi & 3][p].w});
             const uint32_t w[2][2] = {{sw.x, sw.y}, {sw.z, sw.w}};
 #pragma unroll
             for (int h = 0; h < 2; ++h)
@@ -1288,8 +1313,10 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           *reinterpret_cast<uint4*>(dst) = s0;
           *reinterpret_cast<uint4*>(dst + 32) = s1;
         }
-        if constexpr (EPI == NR_EPI_RESADD || EPI == NR_EPI_SOFTMAX64_BWD)
+        if constexpr (EPI == NR_EPI_RESADD || EPI == NR_EPI_SOFTMAX64_BWD) {
           __builtin_amdgcn_sched_barrier(0);  // row groups in load order
+          if (mi + 4 < 8) load_r(mi + 4);
+        }
       }
     }
     }
@@ -1301,10 +1328,7 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     n0 = nn0;
   }
   if (u >= n_tiles && wmu == 1) {  // the half unit's K loop for group 1 (its last unit: nothing to prefetch)
-    for (int kt = 0; kt < nk; ++kt) {
-      kstep(std::true_type{}, kt, st, false, 0u, 0u);
-      st ^= 1;
-    }
+    kloop(std::true_type{}, false, 0u, 0u);
   }
 #undef NR_PHASE_SYNC_MMA
 }
@@ -1342,8 +1366,6 @@ static int num_cus() {
   return c;
 }
 
-// The persistent kernel's operand stream needs >= 2 K steps per tile and
-// addresses A and W through 32-bit buffer offsets.
 // Half-tile tail (gemm256t_kernel's units): on unless a tuning caller turned it off.
 static std::atomic<int> g_half_tail{1};
 
@@ -1364,9 +1386,12 @@ static int persistent_schedule(int64_t tiles, int* nt, int* nh) {
   return *nt >= ncu ? ncu : (*nt > *nh ? *nt : *nh);
 }
 
+// The persistent kernel's operand stream needs an even number (>= 2) of
+// 64-deep K steps per tile (its K loop runs them in pairs, the B fragment sets
+// swapping roles) and addresses A and W through 32-bit buffer offsets.
 static bool persistent_ok(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldw) {
   constexpr int64_t kMax = 0xFFFFFFFFll;
-  return K >= 128 && M * lda * 2 <= kMax && N * ldw * 2 <= kMax;
+  return K >= 128 && K % 128 == 0 && M * lda * 2 <= kMax && N * ldw * 2 <= kMax;
 }
 
 static int launch_gemm256_t(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W,

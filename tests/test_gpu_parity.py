@@ -97,7 +97,7 @@ def test_gemm_bf16_256_epilogues(gpu_device, epi, out_dt):
     """The 256x256 bf16 kernel's register epilogue (transposed accumulators) for
     every epilogue and both output dtypes, ragged M, several N tiles, vs float64."""
     g = torch.Generator().manual_seed(11)
-    M, N, K = 600, 512, 192
+    M, N, K = 600, 512, 256
     a = (torch.randn(M, K, generator=g) * 0.2).bfloat16()
     w = (torch.randn(N, K, generator=g) * 0.1).bfloat16()
     b = torch.randn(N, generator=g) * 0.1
@@ -131,11 +131,12 @@ def test_gemm_bf16_256_epilogues(gpu_device, epi, out_dt):
 def test_gemm_persistent_bf16_multi_tile(gpu_device, epi):
     """The persistent bf16 -> bf16 kernel (gemm256t_kernel) at sizes where every
     workgroup walks several tiles (the operand stream and its stage parity
-    cross tile boundaries, incl. an odd K-step count and the 2-step minimum)
-    and the last round is partial: full outputs vs float64 of the same bf16
-    operands."""
+    cross tile boundaries, incl. an odd count of K-step pairs and the 2-step
+    minimum) and the last round is partial: full outputs vs float64 of the same
+    bf16 operands.  K = 192 (an odd step count) is not persistent since round 4
+    (the K loop runs steps in pairs) and checks the fallback to the tile kernel."""
     g = torch.Generator(device=gpu_device).manual_seed(5)
-    for M, N, K in [(70001, 1024, 256), (33000, 512, 128), (90000, 768, 192)]:
+    for M, N, K in [(70001, 1024, 256), (33000, 512, 128), (90000, 768, 384), (20000, 768, 192)]:
         a = (torch.randn(M, K, device=gpu_device, generator=g) * 0.2).bfloat16()
         w = (torch.randn(N, K, device=gpu_device, generator=g) * 0.1).bfloat16()
         b = torch.randn(N, device=gpu_device, generator=g) * 0.1
