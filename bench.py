@@ -362,35 +362,50 @@ def host_parse_leg(n_news: int, rows: int = 100_000) -> dict:
             "rows_per_s": round(rows / dt, 1), "MB_per_s": round(nbytes / dt / 1e6, 1)}
 
 
-def hipblaslt_yardstick(pooler: str, n: int, ours_ms: float, dev, reps: int = 5) -> dict:
+def hipblaslt_yardstick(pooler: str, n: int, ours_ms: float, dev, reps: int = 5, rounds: int = 3) -> dict:
     """The same per-news transform GEMM shapes (M = n) as bare torch.matmul
     (hipBLASLt: bf16, no bias, no LayerNorm, no epilogue, so less work than
-    the fused transform) summed, beside the fused transform's own time: a
-    vendor-library yardstick for transform_peak_frac.  Yardstick only; the
-    product path never calls it."""
-    shapes = ([(4096, 1024), (4096, 4096), (1024, 4096), (4096, 1024), (1024, 4096)] if pooler == "final" else
-              [(512, 1024), (1024, 512), (8192, 1024), (1024, 4096)])  # (N, K); latent ff1 = GEGLU's 2F
+    the fused transform) beside our own bf16 GEMM on each shape with the
+    transform's epilogue (bias + ReLU / exp / softmax64 / GEGLU / residual; the
+    LayerNorm fold of S and ff1 aside), interleaved in rounds (medians), and
+    the fused transform's own time: a vendor-library yardstick per shape and
+    for transform_peak_frac.  Yardstick only; the product path never calls it."""
+    from news_recommendation_project_v2_amd import ops
+    shapes = ([(4096, 1024, "relu"), (4096, 4096, "relu"), (1024, 4096, "none"), (4096, 1024, "relu"),
+               (1024, 4096, "exp")] if pooler == "final" else
+              [(512, 1024, "softmax64"), (1024, 512, "resadd"), (8192, 1024, "geglu"), (1024, 4096, "resadd")])
     g = torch.Generator(device=dev).manual_seed(7)
-    tot = 0.0
-    per = []
-    for nn, kk in shapes:
+    per, ours = [], []
+    for nn, kk, epi in shapes:
         a = torch.randn((n, kk), device=dev, generator=g).bfloat16()
-        w = torch.randn((nn, kk), device=dev, generator=g).bfloat16()
-        torch.matmul(a, w.T)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            torch.matmul(a, w.T)
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / reps
-        per.append(round(ms, 4))
-        tot += ms
-        del a, w
+        w = (torch.randn((nn, kk), device=dev, generator=g) * kk ** -0.5).bfloat16()
+        b = torch.randn(nn, device=dev, generator=g) * 0.1
+        nc = nn // 2 if epi == "geglu" else nn
+        r = torch.randn((n, nc), device=dev, generator=g).bfloat16() if epi == "resadd" else None
+        out = torch.empty((n, nc), device=dev, dtype=torch.bfloat16)
+        fns = {"hipblaslt": lambda: torch.matmul(a, w.T),
+               "ours": lambda: ops.gemm(a, w, b, epilogue=epi, residual=r, out=out)}
+        times = {k: [] for k in fns}
+        for _ in range(rounds):
+            for k, fn in fns.items():
+                fn()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                times[k].append(e0.elapsed_time(e1) / reps)
+        per.append(round(float(np.median(times["hipblaslt"])), 4))
+        ours.append(round(float(np.median(times["ours"])), 4))
+        del a, w, b, r, out
     _lib.empty_cache()
+    tot = sum(per)
     fl = tx_flops(n, pooler)
-    return {"shapes_NK": shapes, "hipblaslt_ms_each": per, "hipblaslt_sum_ms": round(tot, 4),
+    ratio = [round(o / h, 3) for o, h in zip(ours, per)]
+    return {"shapes_NK_epi": shapes, "hipblaslt_ms_each": per, "ours_ms_each": ours, "ours_over_hipblaslt_each": ratio,
+            "every_shape_at_most_hipblaslt": all(x <= 1.0 for x in ratio), "hipblaslt_sum_ms": round(tot, 4),
             "hipblaslt_peak_frac": round(fl / (tot * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS["bf16"], 3),
             "fused_transform_ms": round(float(ours_ms), 4), "fused_over_hipblaslt_time": round(ours_ms / tot, 3)}
 
