@@ -1132,14 +1132,29 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
     if (more) tile_base(tn, nm0, nn0);
     // the accumulators start at the bias (acc = bias + A.W^T); this wave's
     // columns wn*64 + 16 ni + 4 q4 .. +3
-    f32x4 b4[4];
+    if constexpr (LNF) {
+      // LNF: acc starts at -mean(row) u(col), so the epilogue is one fma per
+      // element, rstd acc + c (the tile's LN slot landed with its step 0)
+      const unsigned char* ls = ln_lds + lslot * kLnSlot;
+      f32x4 u4[4];
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-      b4[ni] = bias ? *reinterpret_cast<const f32x4*>(bias_lds + (16 * ni + 4 * q4) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ni = 0; ni < 4; ++ni) u4[ni] = *reinterpret_cast<const f32x4*>(ls + wave * 512 + (16 * ni + 4 * q4) * 4);
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
+      for (int mi = 0; mi < 8; ++mi) {
+        const float nmean = -*reinterpret_cast<const float*>(ls + 8 * 512 + (wm * 128 + c16 + 16 * mi) * 8);
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = b4[ni];
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = nmean * u4[ni];
+      }
+    } else {
+      f32x4 b4[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        b4[ni] = bias ? *reinterpret_cast<const f32x4*>(bias_lds + (16 * ni + 4 * q4) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = b4[ni];
+    }
     readB(0, 0, fbx);  // step 0's B0
     kloop(std::false_type{}, more, nm0, nn0);
 
@@ -1179,15 +1194,15 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
       const int64_t row = min(row0 + 16 * mi, M - 1);
       const bool live = row0 + 16 * mi < M;  // clamped duplicates of row M - 1 never store
       if constexpr (LNF) {
-        // LN(a) . w = rstd (a . (w o gamma) - mean u) + c   (row stats of the A row)
-        asm volatile("" ::: "memory");  // no CSE of the (u, c) reads across row groups
-        const float2 ms = *reinterpret_cast<const float2*>(ln_st + (wm * 128 + c16 + 16 * mi) * 8);
+        // LN(a) . w = rstd (a . (w o gamma) - mean u) + c   (row stats of the A row;
+        // acc started at -mean u)
+        asm volatile("" ::: "memory");  // no CSE of the c reads across row groups
+        const float rstd = *reinterpret_cast<const float*>(ln_st + (wm * 128 + c16 + 16 * mi) * 8 + 4);
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
-          const f32x4 lu = *reinterpret_cast<const f32x4*>(ln_uc + (16 * ni + 4 * q4) * 4);
           const f32x4 lc = *reinterpret_cast<const f32x4*>(ln_uc + 256 + (16 * ni + 4 * q4) * 4);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[mi][ni][r] = fmaf(ms.y, fmaf(-ms.x, lu[r], acc[mi][ni][r]), lc[r]);
+          for (int r = 0; r < 4; ++r) acc[mi][ni][r] = fmaf(rstd, acc[mi][ni][r], lc[r]);
         }
       }
       if constexpr (EPI == NR_EPI_GEGLU) {
