@@ -137,11 +137,12 @@ class XLMREncoder:
     def _chunks(self, lens: np.ndarray):
         """Consecutive sequence ranges [s, e) of at most max_tokens tokens."""
         off = np.concatenate([[0], np.cumsum(lens)])
-        s = 0
-        while s < len(lens):
-            e = s + 1
-            while e < len(lens) and off[e + 1] - off[s] <= self.max_tokens:
-                e += 1
+        n, s = len(lens), 0
+        while s < n:
+            # the last e with off[e] - off[s] <= max_tokens (at least one sequence):
+            # one binary search, not a Python step per sequence (16 k titles per pass)
+            e = int(np.searchsorted(off, off[s] + self.max_tokens, side="right")) - 1
+            e = min(max(e, s + 1), n)
             yield s, e, off
             s = e
 
