@@ -80,6 +80,8 @@ def reference_rows(a, w, b, epi, r, rows):
         return x + r[rows].double()
     if epi == "softmax64":
         return torch.softmax(x.reshape(len(rows), -1, 64), -1).reshape(len(rows), -1)
+    if epi == "gelu":
+        return torch.nn.functional.gelu(x)
     if epi == "geglu":
         n = x.shape[1]
         xa = x.reshape(len(rows), n // 64, 2, 32)  # 32-row interleave: (a block, g block) per 64 columns
