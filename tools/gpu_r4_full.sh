@@ -16,7 +16,7 @@ timeout -k 10 300 python -u tools/gemm_ab.py --m 1030000 --libs new=news_recomme
   --rounds 3 --reps 5 --shapes final.l3,latent.ff2 > "$OUT/gemm_ab_m1030000.jsonl" 2> "$OUT/gemm_ab_m1030000.err" || exit 4
 echo "gemm_ab ok" >> "$OUT/status.txt"
 timeout -k 10 300 python -u tools/gemm_ab.py --libs new=news_recommendation_project_v2_amd/libnewsrec_hip.so \
-  rb3=tools/gemm_lab/libnewsrec_rb3.so --rounds 5 --shapes final,latent > "$OUT/gemm_ab.jsonl" 2> "$OUT/gemm_ab.err" || exit 5
+  --rounds 5 --shapes final,latent > "$OUT/gemm_ab.jsonl" 2> "$OUT/gemm_ab.err" || exit 5
 echo "gemm_ab72k ok" >> "$OUT/status.txt"
 bash tools/profile_round3.sh "$OUT/prof" > "$OUT/prof.log" 2>&1
 echo "profile rc=$?" >> "$OUT/status.txt"
