@@ -58,8 +58,12 @@ def positions_for(ids: np.ndarray, lens: np.ndarray) -> np.ndarray:
 
 
 class XLMREncoder:
+    # max_tokens: tokens per nr_encoder_forward call.  The workspace is ~14 KB
+    # per bf16 token (QKV / FFN hidden [T x 4096] + three [T x 1024]): 1 M
+    # tokens = 15 GB of the MI355X's 288 GB, so a 16 k-title query pass (~750 k
+    # tokens) is one call and its GEMMs run as few, full-size persistent launches.
     def __init__(self, state_dict: dict, dtype: torch.dtype = torch.float32, device=None,
-                 max_tokens: int = 262144):
+                 max_tokens: int = 1 << 20):
         sd = strip_prefix(state_dict)
         self.dtype = dtype
         self.device = device or torch.device("cuda")
