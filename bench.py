@@ -362,7 +362,7 @@ def host_parse_leg(n_news: int, rows: int = 100_000) -> dict:
             "rows_per_s": round(rows / dt, 1), "MB_per_s": round(nbytes / dt / 1e6, 1)}
 
 
-def hipblaslt_yardstick(pooler: str, n: int, ours_ms: float, dev, reps: int = 5, rounds: int = 3) -> dict:
+def hipblaslt_yardstick(pooler: str, n: int, ours_ms: float, dev, reps: int = 10, rounds: int = 5) -> dict:
     """The same per-news transform GEMM shapes (M = n) as bare torch.matmul
     (hipBLASLt: bf16, no bias, no LayerNorm, no epilogue, so less work than
     the fused transform) beside our own bf16 GEMM on each shape with the
