@@ -64,6 +64,31 @@ __device__ __forceinline__ void st4z(T* p) {
 
 __device__ __forceinline__ float gelu_x(float g) { return 0.5f * g * (1.0f + erff(g * 0.70710678118654752440f)); }
 
+// bf16 step only (the f32 step keeps erff / expf): for two values, h = erfc(|g| /
+// sqrt 2) / 2 and e = exp(-g^2 / 2) with one packed polynomial and v_exp_f32, no
+// branches -- the erfc form of gelu_erf2x2 (nr_common.h: s = g sqrt(log2(e) / 2),
+// erfc = 2^(P(min(|s|, 4 sqrt(log2 e))) - s^2), P a degree-8 minimax fit of
+// log2(erfcx), its -1 folded in so 2^(P - s^2) = erfc / 2; relative error <= 2.2e-6
+// on erfc).  The divergent two-range erff plus expf made GEGLU's backward
+// VALU-heavy (~65 instructions per element).
+__device__ __forceinline__ void erfc_half2(f32x2v g, f32x2v& h, f32x2v& e) {
+  constexpr float kS = 0.8493218002880191f, kSmax = 4.804489635145799f;
+  const f32x2v s = g * kS;
+  const f32x2v c = {fminf(fabsf(s.x), kSmax), fminf(fabsf(s.y), kSmax)};
+  f32x2v q = (f32x2v)-3.57632359e-07f;
+  q = fma2(q, c, (f32x2v)8.19052786e-07f);
+  q = fma2(q, c, (f32x2v)0.000115395807f);
+  q = fma2(q, c, (f32x2v)-0.00191940868f);
+  q = fma2(q, c, (f32x2v)0.0159611721f);
+  q = fma2(q, c, (f32x2v)-0.0876397938f);
+  q = fma2(q, c, (f32x2v)0.364198327f);
+  q = fma2(q, c, (f32x2v)-1.35544741f);
+  q = fma2(q, c, (f32x2v)(3.20236495e-06f - 1.0f));
+  const f32x2v ns2 = -s * s, w = q + ns2;
+  e = (f32x2v){__builtin_amdgcn_exp2f(ns2.x), __builtin_amdgcn_exp2f(ns2.y)};
+  h = (f32x2v){__builtin_amdgcn_exp2f(w.x), __builtin_amdgcn_exp2f(w.y)};
+}
+
 template <typename T>
 __device__ __forceinline__ void ld8(const T* p, float v[8]) {
   if constexpr (sizeof(T) == 4) {
@@ -174,83 +199,102 @@ __global__ __launch_bounds__(256) void gather_ln_kernel(int64_t n, int64_t nvali
   }
 }
 
-// Z = a * gelu(g), (a | g) = the two halves of G's 2F columns (GEGLU,
-// latent_attention.py:24-27, exact erf).  8 columns (16 B of bf16) per thread.
+// Per batch row b: zbar_b = mean over its slots of Z = a * gelu(g), (a | g) =
+// the two halves of G's 2F columns (GEGLU, latent_attention.py:24-27, exact erf;
+// the bf16 step through gelu_erf2x2, |error| <= 3.9e-7), h1bar_b = mean of H1
+// (f32), and row_seg[slot] = b.  Z itself is never stored (f32 in registers): its
+// only consumer is this mean (m = mean(Z) W2^T + ..., and the backward needs G
+// and dZ).  Block = (row b, 256-column chunk: chunks 0..15 of Z, 16..19 of H1);
+// the 8 waves stride the segment's rows with 4 rows in flight each, 4 columns
+// per lane, fixed-order LDS fold (measured, config-5 step: 512-column chunks and
+// 2 rows in flight 66 us; 4 rows, 256 columns 56 us; column chunks as the fast
+// grid dimension 48 us; 16 waves 70 us, 8 rows in flight 64 us).  Rows b in
+// [B, Bp) of zbar are zero; the last block marks the padding slots -1.
 template <typename TA>
-__global__ __launch_bounds__(256) void geglu_fwd_kernel(int64_t rows, const TA* __restrict__ G, TA* __restrict__ Z) {
-  const int64_t total = rows * (F / 8);
-  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
-    const int64_t r = q / (F / 8), c = (q % (F / 8)) * 8;
-    float a[8], g[8], o[8];
-    ld8<TA>(G + r * 2 * F + c, a);
-    ld8<TA>(G + r * 2 * F + F + c, g);
+__device__ __forceinline__ void geglu4(const float (&a)[4], const float (&g)[4], float (&z)[4]) {
+  if constexpr (sizeof(TA) == 4) {
 #pragma unroll
-    for (int t = 0; t < 8; ++t) o[t] = a[t] * gelu_x(g[t]);
-    st8<TA>(Z + r * F + c, o);
+    for (int t = 0; t < 4; ++t) z[t] = a[t] * gelu_x(g[t]);
+  } else {
+    f32x2v g0 = {g[0], g[1]}, g1 = {g[2], g[3]};
+    gelu_erf2x2(g0, g1);
+    z[0] = a[0] * g0.x; z[1] = a[1] * g0.y; z[2] = a[2] * g1.x; z[3] = a[3] * g1.y;
   }
 }
 
-// Per batch row b: zbar_b = mean of Z over its slots (TA, the m GEMM's A
-// operand), h1bar_b = mean of H1 (f32), and row_seg[slot] = b.  Block =
-// (row b, 512-column chunk: chunks 0..7 of Z, 8..9 of H1); the 4 waves stride
-// the segment's rows (two rows in flight), 8 columns per lane, fixed-order LDS
-// fold.  Rows b in [B, Bp) of zbar are zero; the last block marks the padding
-// slots -1.
 template <typename TA>
-__global__ __launch_bounds__(256) void segmean_kernel(int64_t B, int64_t Bp, const int64_t* __restrict__ off,
-                                                      int64_t n_rows, const TA* __restrict__ Z,
+__global__ __launch_bounds__(512) void segmean_kernel(int64_t B, int64_t Bp, const int64_t* __restrict__ off,
+                                                      int64_t n_rows, const TA* __restrict__ G,
                                                       const TA* __restrict__ H1, TA* __restrict__ zbar,
                                                       float* __restrict__ h1bar, int32_t* __restrict__ row_seg) {
-  __shared__ float part[4][512];
-  const int64_t b = blockIdx.x;
-  const int y = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int NW = 8, RW = 4, CW = 256, NZ = F / CW;
+  __shared__ float part[NW][CW];
+  // blockIdx.x = the column chunk: a segment's 20 blocks are dispatched together and
+  // read each G row within a short window (DRAM pages / L2 shared), where a
+  // chunk-major order touched every G row 32 times, spread over the whole kernel
+  const int64_t b = blockIdx.y;
+  const int y = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (b >= Bp) {  // the padding slots
     if (y == 0)
-      for (int64_t r = off[B] + threadIdx.x; r < n_rows; r += 256) row_seg[r] = -1;
+      for (int64_t r = off[B] + threadIdx.x; r < n_rows; r += 512) row_seg[r] = -1;
     return;
   }
-  const bool zpart = y < 8;
-  const int64_t ld = zpart ? F : D;
-  const int c0 = (zpart ? y : y - 8) * 512 + lane * 8;
+  const bool zpart = y < NZ;
+  const int c0 = (zpart ? y : y - NZ) * CW + lane * 4;
   if (b >= B) {
-    if (zpart && wave == 0) {
-      const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      st8<TA>(zbar + b * F + c0, z);
-    }
+    if (zpart && wave == 0) st4z<TA>(zbar + b * F + c0);
     return;
   }
   const int64_t r0 = off[b], r1 = off[b + 1];
   if (y == 0)
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) row_seg[r] = (int32_t)b;
-  const TA* src = zpart ? Z : H1;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int64_t r = r0 + wave;
-  for (; r + 4 < r1; r += 8) {
-    float v[8], w[8];
-    ld8<TA>(src + r * ld + c0, v);
-    ld8<TA>(src + (r + 4) * ld + c0, w);
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += 512) row_seg[r] = (int32_t)b;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  // all RW rows' loads issued before any math (rows past the segment re-read its
+  // last row and are dropped): a load under a per-row branch is waited on inside it
+  for (int64_t r = r0 + wave; r < r1; r += NW * RW) {
+    float v[RW][4];
+    if (zpart) {
+      float a[RW][4], g[RW][4];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc[t] += v[t] + w[t];
+      for (int i = 0; i < RW; ++i) {
+        const int64_t ri = min(r + (int64_t)i * NW, r1 - 1);
+        ld4<TA>(G + ri * 2 * F + c0, a[i]);
+        ld4<TA>(G + ri * 2 * F + F + c0, g[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < RW; ++i) geglu4<TA>(a[i], g[i], v[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < RW; ++i) ld4<TA>(H1 + min(r + (int64_t)i * NW, r1 - 1) * D + c0, v[i]);
+    }
+#pragma unroll
+    for (int i = 1; i < RW; ++i)
+      if (r + (int64_t)i * NW >= r1)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[i][t] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] += (v[0][t] + v[1][t]) + (v[2][t] + v[3][t]);
   }
-  if (r < r1) {
-    float v[8];
-    ld8<TA>(src + r * ld + c0, v);
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc[t] += v[t];
-  }
-#pragma unroll
-  for (int t = 0; t < 8; ++t) part[wave][lane * 8 + t] = acc[t];
+  for (int t = 0; t < 4; ++t) part[wave][lane * 4 + t] = acc[t];
   __syncthreads();
   if (wave != 0) return;
   const float inv = 1.0f / (float)(r1 - r0);  // an empty row gives NaN, as the reference's s / d
-  float o[8];
+  float o[4];
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int c = lane * 8 + t;
-    o[t] = ((part[0][c] + part[1][c]) + (part[2][c] + part[3][c])) * inv;
+  for (int t = 0; t < 4; ++t) {
+    const int c = lane * 4 + t;
+    float q[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) q[w] = part[w][c];
+#pragma unroll
+    for (int h = NW / 2; h > 0; h /= 2)  // pairwise tree, fixed order
+#pragma unroll
+      for (int w = 0; w < h; ++w) q[w] = q[2 * w] + q[2 * w + 1];
+    o[t] = q[0] * inv;
   }
-  if (zpart) st8<TA>(zbar + b * F + c0, o);
-  else st8<float>(h1bar + b * D + c0, o);
+  if (zpart) st4<TA>(zbar + b * F + c0, o);
+  else st4<float>(h1bar + b * D + c0, o);
 }
 
 // One block per batch row b (256 threads, columns tid + 256 j):
@@ -349,50 +393,96 @@ __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int np
 // ------------------------------------------------------------------ backward rows
 // dG = (dz gelu(g), dz a gelu'(g)) for slot rows, with dz = dZs[row_seg[row]]
 // (the per-batch-row dZ of the mean trick, f32, L2-resident), padding slots
-// zero; gpart[chunk] = the column sums of dG over the block's rows (reduced
-// over the chunks by nr_col_sum: db1, deterministic).  Block = (RB rows, 2048
-// a-columns), 8 columns per thread, two rows in flight.  Row chunks, not batch
-// rows: a history length can be ~20x the mean, and one block per batch row
-// then waits on the longest.
+// zero; gpart[chunk] = the column sums of dG over the chunk's RB rows (reduced
+// over the chunks by nr_col_sum: db1, deterministic).  Block = (RB rows, 512
+// a-columns): wave w takes rows RB/4 w .. +RB/4 - 1, all of their G and dZs loads
+// issued before any math (4 rows, 128 + 128 B per lane in flight: the two-rows-
+// per-iteration loop over 16 rows per thread ran at 3.8 TB/s, latency-bound),
+// 8 columns per lane; the waves' column sums fold in LDS in a fixed order.  Row
+// chunks, not batch rows: a history length can be ~20x the mean, and one block
+// per batch row then waits on the longest.
 template <typename TA, int RB>
 __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t n_rows, const TA* __restrict__ G,
                                                         const float* __restrict__ dZs, const int32_t* __restrict__ row_seg,
                                                         TA* __restrict__ dG, float* __restrict__ gpart) {
-  const int64_t r0 = (int64_t)blockIdx.x * RB;
-  const int c = (int)blockIdx.y * 2048 + threadIdx.x * 8;
+  constexpr int RW = RB / 4;  // rows per wave
+  __shared__ float red[3][2][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // blockIdx.x = the column chunk (fast): a row chunk's 8 blocks run together
+  const int64_t r0 = (int64_t)blockIdx.y * RB + wave * RW;
+  const int c = (int)blockIdx.x * 512 + lane * 8;
+  int32_t sg_[RW];
+  float a[RW][8], g[RW][8], d[RW][8];
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const int64_t r = r0 + i;
+    sg_[i] = r < n_rows ? row_seg[r] : -2;
+  }
+  // every row's loads issued unconditionally (clamped row / segment 0 for the
+  // padding): a load under a per-row branch is waited on inside that branch
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const int64_t r = min(r0 + i, n_rows - 1);
+    ld8<TA>(G + r * 2 * F + c, a[i]);
+    ld8<TA>(G + r * 2 * F + F + c, g[i]);
+    ld8<float>(dZs + (int64_t)max(sg_[i], 0) * F + c, d[i]);
+  }
   float sa[8], sg[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { sa[k] = 0.f; sg[k] = 0.f; }
-  auto one = [&](int64_t r, int32_t s, const float (&a)[8], const float (&g)[8]) {
-    float d[8], da[8], dg[8];
-    ld8<float>(dZs + (int64_t)s * F + c, d);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float cdf = 0.5f * (1.0f + erff(g[k] * 0.70710678118654752440f));
-      const float pdf = 0.39894228040143267794f * __expf(-0.5f * g[k] * g[k]);
-      da[k] = d[k] * g[k] * cdf;
-      dg[k] = d[k] * a[k] * (cdf + g[k] * pdf);
-      sa[k] += da[k];
-      sg[k] += dg[k];
+  for (int i = 0; i < RW; ++i) {
+    const int64_t r = r0 + i;
+    if (sg_[i] >= 0) {
+      float da[8], dg[8];
+#pragma unroll
+      for (int k = 0; k < 8; k += 2) {
+        float cdf[2], pdf[2];
+        if constexpr (sizeof(TA) == 4) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            cdf[j] = 0.5f * (1.0f + erff(g[i][k + j] * 0.70710678118654752440f));
+            pdf[j] = 0.39894228040143267794f * __expf(-0.5f * g[i][k + j] * g[i][k + j]);
+          }
+        } else {
+          f32x2v h, e;
+          erfc_half2((f32x2v){g[i][k], g[i][k + 1]}, h, e);
+          cdf[0] = g[i][k] >= 0.f ? 1.0f - h.x : h.x;
+          cdf[1] = g[i][k + 1] >= 0.f ? 1.0f - h.y : h.y;
+          pdf[0] = 0.39894228040143267794f * e.x;
+          pdf[1] = 0.39894228040143267794f * e.y;
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float gk = g[i][k + j], dk = d[i][k + j];
+          da[k + j] = dk * gk * cdf[j];
+          dg[k + j] = dk * a[i][k + j] * (cdf[j] + gk * pdf[j]);
+          sa[k + j] += da[k + j];
+          sg[k + j] += dg[k + j];
+        }
+      }
+      st8<TA>(dG + r * 2 * F + c, da);
+      st8<TA>(dG + r * 2 * F + F + c, dg);
+    } else if (sg_[i] == -1) {
+      const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      st8<TA>(dG + r * 2 * F + c, zero);
+      st8<TA>(dG + r * 2 * F + F + c, zero);
     }
-    st8<TA>(dG + r * 2 * F + c, da);
-    st8<TA>(dG + r * 2 * F + F + c, dg);
-  };
-  const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int i = 0; i < RB; i += 2) {
-    const int64_t ra = r0 + i, rb = r0 + i + 1;
-    const int32_t sa_ = ra < n_rows ? row_seg[ra] : -2, sb_ = rb < n_rows ? row_seg[rb] : -2;
-    float a0[8], g0[8], a1[8], g1[8];
-    if (sa_ >= 0) { ld8<TA>(G + ra * 2 * F + c, a0); ld8<TA>(G + ra * 2 * F + F + c, g0); }
-    if (sb_ >= 0) { ld8<TA>(G + rb * 2 * F + c, a1); ld8<TA>(G + rb * 2 * F + F + c, g1); }
-    if (sa_ >= 0) one(ra, sa_, a0, g0);
-    else if (sa_ == -1) { st8<TA>(dG + ra * 2 * F + c, zero); st8<TA>(dG + ra * 2 * F + F + c, zero); }
-    if (sb_ >= 0) one(rb, sb_, a1, g1);
-    else if (sb_ == -1) { st8<TA>(dG + rb * 2 * F + c, zero); st8<TA>(dG + rb * 2 * F + F + c, zero); }
   }
-  st8<float>(gpart + (int64_t)blockIdx.x * 2 * F + c, sa);
-  st8<float>(gpart + (int64_t)blockIdx.x * 2 * F + F + c, sg);
+  if (wave > 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { red[wave - 1][0][lane * 8 + k] = sa[k]; red[wave - 1][1][lane * 8 + k] = sg[k]; }
+  }
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int j = lane * 8 + k;
+    sa[k] = (sa[k] + red[0][0][j]) + (red[1][0][j] + red[2][0][j]);
+    sg[k] = (sg[k] + red[0][1][j]) + (red[1][1][j] + red[2][1][j]);
+  }
+  st8<float>(gpart + (int64_t)blockIdx.y * 2 * F + c, sa);
+  st8<float>(gpart + (int64_t)blockIdx.y * 2 * F + F + c, sg);
 }
 
 // LayerNorm input gradient (stats recomputed from x with the forward's
@@ -710,7 +800,7 @@ constexpr int kLatParts = 32;  // split-K slices of dlatents' GEMM (K = 8192 -> 
 // Workspace layout (byte offsets), shared by the size query and the step.
 struct Layout {
   int64_t Hp, Hpp, kw, Bp, es;
-  int64_t E, Sx, X, P, H1, Y, G, Z, zbar, h1bar, row_seg, hparts, hsum, dmA, dmc, dZ, dZs, gpart, dG, dY, dH1, dP,
+  int64_t E, Sx, X, P, H1, Y, G, zbar, h1bar, row_seg, hparts, hsum, dmA, dmc, dZ, dZs, gpart, dG, dY, dH1, dP,
       dS, dX, dE;
   int64_t dGT, YT, dH1T, PT, dST, XT, dmT, zbarT;
   int64_t WqT, W1T, W2T, WoT, WkvT, latn, latnT, KVp, KV, KVT, A, AT, BtT, Bt;
@@ -731,7 +821,7 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs) {
   auto take = [&](int64_t bytes) { const int64_t r = o; o += al(bytes); return r; };
   L.E = take(U * D * 4);
   L.Sx = take(Hp * D * es); L.X = take(Hp * D * es); L.P = take(Hp * S * es); L.H1 = take(Hp * D * es);
-  L.Y = take(Hp * D * es); L.G = take(Hp * 2 * F * es); L.Z = take(Hp * F * es);
+  L.Y = take(Hp * D * es); L.G = take(Hp * 2 * F * es);
   L.zbar = take(Bp * F * es); L.h1bar = take(Bp * D * 4); L.row_seg = take(Hp * 4);
   L.hparts = take((int64_t)kHParts * Bp * D * 4); L.hsum = take(Bp * D * 4);
   L.dmA = take(Bp * D * es); L.dmc = take(Bp * D * es); L.dZ = take((int64_t)kZParts * Bp * F * 4);
@@ -798,7 +888,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   auto P_ = [&](int64_t off) { return (void*)(ws + off); };
   float* E = (float*)P_(L.E);
   TA *Sx = (TA*)P_(L.Sx), *X = (TA*)P_(L.X), *Pm = (TA*)P_(L.P), *H1 = (TA*)P_(L.H1), *Y = (TA*)P_(L.Y);
-  TA *G = (TA*)P_(L.G), *Z = (TA*)P_(L.Z), *zbar = (TA*)P_(L.zbar);
+  TA *G = (TA*)P_(L.G), *zbar = (TA*)P_(L.zbar);
   float* h1bar = (float*)P_(L.h1bar);
   int32_t* row_seg = (int32_t*)P_(L.row_seg);
   float* hparts = (float*)P_(L.hparts);
@@ -888,14 +978,8 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_RESADD, Hp, D, S, Pm, S, Bt, S, nullptr, Sx, D, H1, D, st))) return rc;
   if ((rc = layernorm_dispatch(dt, dt, Hp, D, H1, D, a.nf_g, a.nf_b, 1e-5f, Y, D, st))) return rc;
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, 2 * F, D, Y, D, W1, D, a.b1, nullptr, 0, G, 2 * F, st))) return rc;
-  {
-    const int64_t q = Hp * (F / 8);
-    const int64_t g = (q + 255) / 256;
-    hipLaunchKernelGGL((geglu_fwd_kernel<TA>), dim3((unsigned)(g < 8192 ? g : 8192)), dim3(256), 0, st, Hp, G, Z);
-    NR_LT_CHECK("geglu_fwd");
-  }
   // ---- per batch row: means, m = zbar W2^T (split-K) + b2 + h1bar, loss
-  hipLaunchKernelGGL((segmean_kernel<TA>), dim3((unsigned)(Bp + 1), 10), dim3(256), 0, st, B, Bp, a.hist_off, Hp, Z,
+  hipLaunchKernelGGL((segmean_kernel<TA>), dim3((F + D) / 256, (unsigned)(Bp + 1)), dim3(512), 0, st, B, Bp, a.hist_off, Hp, G,
                      H1, zbar, h1bar, row_seg);
   NR_LT_CHECK("segmean");
   {
@@ -917,7 +1001,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   }
   if ((rc = sum_parts(dZ, kZParts, Bp * F, dZs, Bp * F, st))) return rc;
   const int64_t gchunks = (Hp + kGRows - 1) / kGRows;
-  hipLaunchKernelGGL((geglu_bwd_kernel<TA, kGRows>), dim3((unsigned)gchunks, F / 2048), dim3(256), 0, st, Hp, G, dZs,
+  hipLaunchKernelGGL((geglu_bwd_kernel<TA, kGRows>), dim3(F / 512, (unsigned)gchunks), dim3(256), 0, st, Hp, G, dZs,
                      row_seg, dG, gpart);
   NR_LT_CHECK("geglu_bwd");
   if ((rc = nr_col_sum(NR_F32, gchunks, 2 * F, gpart, 2 * F, a.g_b1, st))) return rc;
@@ -962,7 +1046,9 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     NR_LT_CHECK("softmax64_bwd");
   }
   // fork 2: dA / dBt and the whole fold backward need only dS, dH1, P, X from here on,
-  // so they run on a third stream beside dX, the scatter and the token LN grads
+  // so they run on a third stream beside dX, the scatter and the token LN grads.
+  // (Starting dBt's transposes and GEMM before the dS GEMM, on a third event, measured
+  // no gain: they slowed dS by as much, profiles/round4/train/r4s9.)
   if (hipEventRecord(side.fork2, st) != hipSuccess || hipStreamWaitEvent(side.s2, side.fork2, 0) != hipSuccess) {
     set_error("nr_latent_train_step: fork 2 failed");
     return NR_ERR_HIP;
@@ -993,14 +1079,13 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   }
   // ---- fold backward
   {
-    // the K-slices summed in place into slice 0, then converted / transposed once each
-    if ((rc = sum_parts(gA, kWParts, (int64_t)S * D, gA, (int64_t)S * D, s2))) return rc;
-    if ((rc = sum_parts(gBt, kWParts, (int64_t)D * S, gBt, (int64_t)D * S, s2))) return rc;
+    // the K-slices summed on the way into each converted / transposed operand (one
+    // launch; the same slice order as sum_parts, so bit-identical to summing first)
     TList t;
-    t.add(gA, D, gA16, D, S, D, false);
-    t.add(gA, D, gAT16, S, S, D, true);
-    t.add(gBt, S, gBt16, S, D, S, false);
-    t.add(gBt, S, gBtT16, D, D, S, true);
+    t.add(gA, D, gA16, D, S, D, false, 0, kWParts, (int64_t)S * D);
+    t.add(gA, D, gAT16, S, S, D, true, 0, kWParts, (int64_t)S * D);
+    t.add(gBt, S, gBt16, S, D, S, false, 0, kWParts, (int64_t)D * S);
+    t.add(gBt, S, gBtT16, D, D, S, true, 0, kWParts, (int64_t)D * S);
     if ((rc = launch_tlist<float, TA>(t, s2))) return rc;
   }
   {

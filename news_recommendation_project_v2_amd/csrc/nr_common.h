@@ -98,6 +98,47 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// GELU of four values (two float2 chains, v_pk_fma_f32 / v_pk_mul_f32) for the
+// persistent bf16 kernel's GELU and GEGLU epilogues (gemm.hip) and the
+// latent step's bf16 GEGLU (latent_train.hip).  Round 4: no reciprocal.
+// With s = g sqrt(log2(e) / 2) (so s^2 = log2(e) z^2, z = |g| / sqrt 2),
+//   erfc(z) = 2^(P(min(|s|, 4 sqrt(log2 e))) - s^2),
+// P(s) ~ log2(erfcx(s / sqrt(log2 e))) a degree-8 polynomial (Lawson minimax on
+// z in [0, 4]: |error| <= 3.2e-6 in log2 units, 2.2e-6 relative on erfc; past
+// z = 4 only erfc's Gaussian factor keeps falling, where gelu is g or ~0 to
+// 1e-8).  gelu = g (1 - erfc / 2) for g >= 0, g erfc / 2 below: |gelu - exact|
+// <= 3.9e-7 over |g| <= 12 in f32, as the Numerical-Recipes erfc form of
+// gelu_erf (3.8e-7) -- checked in float64 emulation of these f32 steps.  Per
+// four values 2 fewer pk_fma chains steps, no v_rcp_f32 and no t multiply:
+// the plain-GELU epilogue (encoder FFN1) cost 22 % of its GEMM at the ff1
+// shape (probe 0.961 -> 1.171 ms, profiles/round4/gemm/r4g5_*).  The f32
+// kernels keep gelu_erf.
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2v fma2(f32x2v a, f32x2v b, f32x2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ void gelu_erf2x2(f32x2v& g0, f32x2v& g1) {
+  constexpr float kS = 0.8493218002880191f, kSmax = 4.804489635145799f;
+  const f32x2v s0 = g0 * kS, s1 = g1 * kS;
+  const f32x2v c0 = {fminf(fabsf(s0.x), kSmax), fminf(fabsf(s0.y), kSmax)};
+  const f32x2v c1 = {fminf(fabsf(s1.x), kSmax), fminf(fabsf(s1.y), kSmax)};
+  f32x2v p0 = (f32x2v)-3.57632359e-07f, p1 = (f32x2v)-3.57632359e-07f;
+#define NR_G4(c)                      \
+  p0 = fma2(p0, c0, (f32x2v)(c)); \
+  p1 = fma2(p1, c1, (f32x2v)(c));
+  NR_G4(8.19052786e-07f) NR_G4(0.000115395807f) NR_G4(-0.00191940868f) NR_G4(0.0159611721f)
+  NR_G4(-0.0876397938f) NR_G4(0.364198327f) NR_G4(-1.35544741f) NR_G4(3.20236495e-06f - 1.0f)
+#undef NR_G4
+  // w = P - 1 - s^2: 2^w = erfc / 2; gelu = max(g, 0) - |g| erfc / 2 (g (1 - erfc / 2)
+  // for g >= 0, g erfc / 2 below) -- one fma with |.| / neg modifiers, no select
+  const f32x2v w0 = fma2(-s0, s0, p0), w1 = fma2(-s1, s1, p1);
+  // max(g, 0) as a signed-integer max on the bits (a negative float, -0 included,
+  // is a negative int): one v_max_i32, where fmaxf adds an IEEE canonicalize
+  auto relu = [](float v) { return __int_as_float(max(__float_as_int(v), 0)); };
+  g0 = (f32x2v){fmaf(-fabsf(g0.x), __builtin_amdgcn_exp2f(w0.x), relu(g0.x)),
+                fmaf(-fabsf(g0.y), __builtin_amdgcn_exp2f(w0.y), relu(g0.y))};
+  g1 = (f32x2v){fmaf(-fabsf(g1.x), __builtin_amdgcn_exp2f(w1.x), relu(g1.x)),
+                fmaf(-fabsf(g1.y), __builtin_amdgcn_exp2f(w1.y), relu(g1.y))};
+}
+
 }  // namespace nr
 
 #define NR_CHECK_ARG(cond, ...)                 \
