@@ -787,6 +787,94 @@ int launch_tlist(const TList& l, hipStream_t s) {
   return NR_OK;
 }
 
+// f32 split-K partials -> their sum in TO twice, as is (plain) and transposed:
+// the fold's operands (KV / KV^T, gA / gA^T, gBt / gBt^T, dKV / dKV^T).  One
+// 64 x 64 tile per block, up to kSCMax matrices per launch: each partial is
+// read once with 16-B loads, all `parts` loads of a row issued together, the sum
+// in slice order (as sum_parts), the plain tile stored from registers and the
+// transposed one through LDS.  The generic TBatch path read every partial twice
+// (once per output) with 4-B loads: 34-38 us for the gA / gBt set, ~12 us here.
+constexpr int kSCMax = 2;
+struct SCBatch {
+  int n;
+  int tile_end[kSCMax], tiles_x[kSCMax], parts[kSCMax];
+  const float* src[kSCMax];
+  void* plain[kSCMax];
+  void* trans[kSCMax];
+  int64_t cols[kSCMax], lds[kSCMax], ldp[kSCMax], ldt[kSCMax], pstride[kSCMax];
+};
+
+template <typename TO>
+__global__ __launch_bounds__(256) void sumconv_kernel(SCBatch sb) {
+  __shared__ float tile[64][65];
+  const int t = (int)blockIdx.x;
+  int p = 0;
+  while (p + 1 < sb.n && t >= sb.tile_end[p]) ++p;
+  const int local = t - (p ? sb.tile_end[p - 1] : 0);
+  const int64_t r0 = (int64_t)(local / sb.tiles_x[p]) * 64, c0 = (int64_t)(local % sb.tiles_x[p]) * 64;
+  const float* src = sb.src[p];
+  const int np = sb.parts[p];
+  const int64_t lds = sb.lds[p], ps = sb.pstride[p];
+  const int th = threadIdx.x, rg = th >> 4, c4 = (th & 15) * 4;
+  TO* plain = (TO*)sb.plain[p];
+  const int64_t ldp = sb.ldp[p];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int rr = rg + 16 * k;
+    const float* s = src + (r0 + rr) * lds + c0 + c4;
+    float4 v = *reinterpret_cast<const float4*>(s);
+#pragma unroll 8
+    for (int q = 1; q < np; ++q) {
+      const float4 w = *reinterpret_cast<const float4*>(s + q * ps);
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+    const float o[4] = {v.x, v.y, v.z, v.w};
+    st4<TO>(plain + (r0 + rr) * ldp + c0 + c4, o);
+    tile[rr][c4] = v.x; tile[rr][c4 + 1] = v.y; tile[rr][c4 + 2] = v.z; tile[rr][c4 + 3] = v.w;
+  }
+  __syncthreads();
+  TO* trans = (TO*)sb.trans[p];
+  const int64_t ldt = sb.ldt[p];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = th + 256 * k, cc = i >> 3, rc = (i & 7) * 8;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = tile[rc + j][cc];
+    st8<TO>(trans + (c0 + cc) * ldt + r0 + rc, o);
+  }
+}
+
+struct SCList {
+  SCBatch b{};
+  int tiles = 0;
+  // src [rows, cols] (ld lds, `parts` slices pstride apart) -> plain [rows, cols] (ld ldp)
+  // and trans [cols, rows] (ld ldt); rows, cols multiples of 64
+  int add(const float* src, int64_t lds, int parts, int64_t pstride, int64_t rows, int64_t cols, void* plain,
+          int64_t ldp, void* trans, int64_t ldt) {
+    if (b.n >= kSCMax || rows % 64 || cols % 64 || lds % 4 || pstride % 4 || ldp % 8 || ldt % 8) {
+      set_error("nr_latent_train_step: sumconv operand %d: rows %lld / cols %lld not multiples of 64", b.n,
+                (long long)rows, (long long)cols);
+      return NR_ERR_INVALID;
+    }
+    const int i = b.n++;
+    b.src[i] = src; b.plain[i] = plain; b.trans[i] = trans; b.parts[i] = parts; b.pstride[i] = pstride;
+    b.cols[i] = cols; b.lds[i] = lds; b.ldp[i] = ldp; b.ldt[i] = ldt;
+    b.tiles_x[i] = (int)(cols / 64);
+    tiles += (int)(rows / 64 * (cols / 64));
+    b.tile_end[i] = tiles;
+    return NR_OK;
+  }
+};
+
+template <typename TO>
+int launch_sumconv(const SCList& l, hipStream_t s) {
+  if (l.b.n == 0) return NR_OK;
+  hipLaunchKernelGGL((sumconv_kernel<TO>), dim3((unsigned)l.tiles), dim3(256), 0, s, l.b);
+  NR_CHECK_LAUNCH("nr_latent_train_step (sumconv)");
+  return NR_OK;
+}
+
 static int64_t pad64(int64_t n) { return n < 64 ? 64 : (n + 63) / 64 * 64; }
 static int64_t al(int64_t b) { return (b + 255) / 256 * 256; }
 
@@ -951,10 +1039,9 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     const int64_t ks = D / kKVParts;
     GemmProblem p = {NL, 2 * F, ks, latn, D, ks, Wkv, D, ks, KVp, 2 * F, (int64_t)NL * 2 * F, kKVParts, 1.0f};
     if ((rc = gemm_group_dispatch(dt, NR_F32, &p, 1, st))) return rc;
-    TList t;
-    t.add(KVp, 2 * F, KV, 2 * F, NL, 2 * F, false, 0, kKVParts, (int64_t)NL * 2 * F);
-    t.add(KVp, 2 * F, KVT, NL, NL, 2 * F, true, 0, kKVParts, (int64_t)NL * 2 * F);
-    if ((rc = launch_tlist<float, TA>(t, st))) return rc;
+    SCList t;
+    if ((rc = t.add(KVp, 2 * F, kKVParts, (int64_t)NL * 2 * F, NL, 2 * F, KV, 2 * F, KVT, NL))) return rc;
+    if ((rc = launch_sumconv<TA>(t, st))) return rc;
   }
   {
     GemmProblem p[2] = {
@@ -1079,14 +1166,12 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   }
   // ---- fold backward
   {
-    // the K-slices summed on the way into each converted / transposed operand (one
-    // launch; the same slice order as sum_parts, so bit-identical to summing first)
-    TList t;
-    t.add(gA, D, gA16, D, S, D, false, 0, kWParts, (int64_t)S * D);
-    t.add(gA, D, gAT16, S, S, D, true, 0, kWParts, (int64_t)S * D);
-    t.add(gBt, S, gBt16, S, D, S, false, 0, kWParts, (int64_t)D * S);
-    t.add(gBt, S, gBtT16, D, D, S, true, 0, kWParts, (int64_t)D * S);
-    if ((rc = launch_tlist<float, TA>(t, s2))) return rc;
+    // the K-slices summed on the way into both converted operands (one launch; the
+    // same slice order as sum_parts, so bit-identical to summing first)
+    SCList t;
+    if ((rc = t.add(gA, D, kWParts, (int64_t)S * D, S, D, gA16, D, gAT16, S))) return rc;
+    if ((rc = t.add(gBt, S, kWParts, (int64_t)D * S, D, S, gBt16, S, gBtT16, D))) return rc;
+    if ((rc = launch_sumconv<TA>(t, s2))) return rc;
   }
   {
     GemmProblem p[4] = {
@@ -1102,10 +1187,9 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     if ((rc = gemm_group_dispatch(dt, NR_F32, p, 4, s2))) return rc;
   }
   {
-    TList t;
-    t.add(dKV, 2 * F, dKV16, 2 * F, NL, 2 * F, false);
-    t.add(dKV, 2 * F, dKVT16, NL, NL, 2 * F, true);
-    if ((rc = launch_tlist<float, TA>(t, s2))) return rc;
+    SCList t;
+    if ((rc = t.add(dKV, 2 * F, 1, 0, NL, 2 * F, dKV16, 2 * F, dKVT16, NL))) return rc;
+    if ((rc = launch_sumconv<TA>(t, s2))) return rc;
   }
   {
     const int64_t ks = 2 * F / kLatParts;
