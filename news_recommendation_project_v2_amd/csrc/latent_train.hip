@@ -942,7 +942,7 @@ static int grid_rows(int64_t rows, int cap = 1024) {
 // device, created on first use and kept (streams are reentrant per thread).
 struct Side {
   hipStream_t s = nullptr, s2 = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr, fork2 = nullptr, join2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, fork2 = nullptr, join2 = nullptr, wt = nullptr;
 };
 static int side_stream(Side& out) {
   thread_local Side t_side[64];
@@ -958,7 +958,8 @@ static int side_stream(Side& out) {
         hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&sd.fork2, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.join2, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&sd.join2, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&sd.wt, hipEventDisableTiming) != hipSuccess) {
       set_error("nr_latent_train_step: cannot create the side stream / events");
       sd = Side{};
       return NR_ERR_HIP;
@@ -1008,6 +1009,14 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   if ((rc = side_stream(side))) return rc;
 #define NR_LT_CHECK(name) NR_CHECK_LAUNCH("nr_latent_train_step (" name ")")
 
+  // ---- fork 0: the weight transposes and the fold (weights only) run on the side
+  // stream beside the token LN and the history gather (inputs only); the P GEMM
+  // joins them.  The side stream first waits for everything before the step on
+  // this one (the previous step's AdamW rewrote the weights).
+  if (hipEventRecord(side.fork, st) != hipSuccess || hipStreamWaitEvent(side.s, side.fork, 0) != hipSuccess) {
+    set_error("nr_latent_train_step: fork 0 failed");
+    return NR_ERR_HIP;
+  }
   // ---- accumulators: the step zeroes every gradient it accumulates (the GEMM-written
   // ones are overwritten whole), the loss and the history-gather gradient dE
   {
@@ -1020,47 +1029,68 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     hipLaunchKernelGGL(zero_kernel, dim3(1024), dim3(256), 0, st, z);
     NR_LT_CHECK("zero");
   }
-  // ---- weight transposes (the data-grad GEMMs' W operands)
+  // (one box, interleaved, ms/step: all of this serial on one stream 1.195-1.215, every
+  // weight transpose before the fold on the side stream 1.20, this layout 1.185 --
+  // profiles/round4/train/step_tuning/r4ab1)
+  hipStream_t fs = side.s;
+  // Wq^T, the fold's operand (the other weight transposes follow the fold)
   {
     TList t;
-    t.add(Wq, D, WqT, F, F, D, true);          // [4096, 1024] -> [1024, 4096]
-    t.add(W1, D, W1T, 2 * F, 2 * F, D, true);  // [8192, 1024] -> [1024, 8192]
-    t.add(W2, F, W2T, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
-    t.add(Wo, F, WoT, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
-    t.add(Wkv, D, WkvT, 2 * F, 2 * F, D, true);
-    if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
+    t.add(Wq, D, WqT, F, F, D, true);  // [4096, 1024] -> [1024, 4096]
+    if ((rc = launch_tlist<TA, TA>(t, fs))) return rc;
   }
-  // ---- E = token LN of the last tokens (f32)
-  if ((rc = gather_ln_dispatch(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1, a.tok_g, a.tok_b, 1e-12f, E, D, st)))
-    return rc;
-  // ---- fold: latn = LN_c(latents); KV = latn Wkv^T (split-K); A_h = s K_h Wq_h; BtT_h = V_h Wo_h^T
-  if ((rc = layernorm_dispatch(NR_F32, dt, NL, D, a.latents, D, a.nc_g, a.nc_b, 1e-5f, latn, D, st))) return rc;
+  // fold: latn = LN_c(latents); KV = latn Wkv^T (split-K); A_h = s K_h Wq_h; BtT_h = V_h Wo_h^T
+  if ((rc = layernorm_dispatch(NR_F32, dt, NL, D, a.latents, D, a.nc_g, a.nc_b, 1e-5f, latn, D, fs))) return rc;
   {
     const int64_t ks = D / kKVParts;
     GemmProblem p = {NL, 2 * F, ks, latn, D, ks, Wkv, D, ks, KVp, 2 * F, (int64_t)NL * 2 * F, kKVParts, 1.0f};
-    if ((rc = gemm_group_dispatch(dt, NR_F32, &p, 1, st))) return rc;
+    if ((rc = gemm_group_dispatch(dt, NR_F32, &p, 1, fs))) return rc;
     SCList t;
     if ((rc = t.add(KVp, 2 * F, kKVParts, (int64_t)NL * 2 * F, NL, 2 * F, KV, 2 * F, KVT, NL))) return rc;
-    if ((rc = launch_sumconv<TA>(t, st))) return rc;
+    if ((rc = launch_sumconv<TA>(t, fs))) return rc;
   }
   {
     GemmProblem p[2] = {
         {NL, D, DH, KV, 2 * F, DH, WqT, F, DH, Am, D, (int64_t)NL * D, HEADS, scale},
         {NL, D, DH, KV + F, 2 * F, DH, Wo, F, DH, BtT, D, (int64_t)NL * D, HEADS, 1.0f},
     };
-    if ((rc = gemm_group_dispatch(dt, dt, p, 2, st))) return rc;
+    if ((rc = gemm_group_dispatch(dt, dt, p, 2, fs))) return rc;
   }
   {
     TList t;
     t.add(Am, D, AT, S, S, D, true);         // A [512, 1024] -> AT [1024, 512]
     t.add(BtT, D, Bt, S, S, D, true);        // BtT [512, 1024] -> Bt [1024, 512]
     t.add(latn, D, latnT, NL, NL, D, true);  // [64, 1024] -> [1024, 64]
-    if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
+    if ((rc = launch_tlist<TA, TA>(t, fs))) return rc;
   }
+  if (hipEventRecord(side.join, fs) != hipSuccess) {
+    set_error("nr_latent_train_step: join 0 record failed");
+    return NR_ERR_HIP;
+  }
+  // the data-grad GEMMs' W operands, first needed by the dZ GEMM (event wt)
+  {
+    TList t;
+    t.add(W1, D, W1T, 2 * F, 2 * F, D, true);  // [8192, 1024] -> [1024, 8192]
+    t.add(W2, F, W2T, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
+    t.add(Wo, F, WoT, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
+    t.add(Wkv, D, WkvT, 2 * F, 2 * F, D, true);
+    if ((rc = launch_tlist<TA, TA>(t, fs))) return rc;
+  }
+  if (hipEventRecord(side.wt, fs) != hipSuccess) {
+    set_error("nr_latent_train_step: weight transpose record failed");
+    return NR_ERR_HIP;
+  }
+  // ---- E = token LN of the last tokens (f32)
+  if ((rc = gather_ln_dispatch(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1, a.tok_g, a.tok_b, 1e-12f, E, D, st)))
+    return rc;
   // ---- per-slot forward
   hipLaunchKernelGGL((gather_ln_kernel<TA>), dim3(grid_rows(Hp)), dim3(256), 0, st, Hp, a.Hs, E, (int64_t)D,
                      a.hist_idx, a.nq_g, a.nq_b, 1e-5f, Sx, X);
   NR_LT_CHECK("gather_ln");
+  if (hipStreamWaitEvent(st, side.join, 0) != hipSuccess) {
+    set_error("nr_latent_train_step: join 0 failed");
+    return NR_ERR_HIP;
+  }
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_SOFTMAX64, Hp, S, D, X, D, Am, D, nullptr, nullptr, 0, Pm, S, st))) return rc;
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_RESADD, Hp, D, S, Pm, S, Bt, S, nullptr, Sx, D, H1, D, st))) return rc;
   if ((rc = layernorm_dispatch(dt, dt, Hp, D, H1, D, a.nf_g, a.nf_b, 1e-5f, Y, D, st))) return rc;
@@ -1081,6 +1111,10 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   NR_LT_CHECK("head");
   // ---- backward
   // dZ_b = (dm_b / h_b) W2 (f32, split-K partials [kZParts, Bp, 4096]): C = dmc . W2T^T
+  if (hipStreamWaitEvent(st, side.wt, 0) != hipSuccess) {
+    set_error("nr_latent_train_step: weight transpose wait failed");
+    return NR_ERR_HIP;
+  }
   {
     const int64_t ks = D / kZParts;
     GemmProblem p = {Bp, F, ks, dmc, D, ks, W2T, D, ks, dZ, F, Bp * F, kZParts, 1.0f};
