@@ -1,6 +1,7 @@
 #!/bin/bash
 # Interleaved A/B of the latent step's stream layouts (NR_LT_VARIANT 0 / 1 / 2) on one
 # box: train_bench.py latent bf16, 3 rounds x 3 variants, one JSON line each.
+# (The switch existed only for that run; layout 2 is the product now.)
 set -o pipefail
 OUT=gpurun_out/${1:-r4ab}
 mkdir -p "$OUT"
