@@ -521,13 +521,19 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, 
       }
       continue;
     }
-    float v[4][4], g[4][4];
-    float sum = 0.f;
+    // x, dy and the residual row issued together (one memory round trip per row;
+    // dy and res behind the statistics' reductions made the kernel latency-bound)
+    float v[4][4], g[4][4], dyv[4][4], rv[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      ld4<TA>(x + row * D + j * 256 + lane * 4, v[j]);
-      sum += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+      const int c = j * 256 + lane * 4;
+      ld4<TA>(x + row * D + c, v[j]);
+      ld4<TA>(dy + row * D + c, dyv[j]);
+      ld4<TA>(res + (MODE == 0 ? (int64_t)s : row) * D + c, rv[j]);
     }
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sum += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
     const float mean = wave_sum(sum) / (float)D;
     float q = 0.f;
 #pragma unroll
@@ -538,8 +544,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, 
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float d4[4];
-      ld4<TA>(dy + row * D + j * 256 + lane * 4, d4);
+      const float* d4 = dyv[j];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         v[j][t] = (v[j][t] - mean) * rstd;  // xhat
@@ -554,10 +559,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int c = j * 256 + lane * 4;
-      float r4[4], o[4];
-      ld4<TA>(res + (MODE == 0 ? (int64_t)s : row) * D + c, r4);
+      float o[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) o[t] = rstd * (g[j][t] - m1 - v[j][t] * m2) + r4[t];
+      for (int t = 0; t < 4; ++t) o[t] = rstd * (g[j][t] - m1 - v[j][t] * m2) + rv[j][t];
       if constexpr (MODE == 0) st4<TA>(out + row * D + c, o);
       else *reinterpret_cast<float4*>(&stage[wave][c]) = float4{o[0], o[1], o[2], o[3]};
     }
@@ -1151,7 +1155,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   }
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, 2 * F, dG, 2 * F, W1T, 2 * F, nullptr, nullptr, 0, dY, D, st)))
     return rc;
-  hipLaunchKernelGGL((ln_bwd_kernel<TA, 0>), dim3(grid_rows(Hp, 256)), dim3(256), 0, st, Hp, Hp, H1, a.nf_g, 1e-5f, dY,
+  hipLaunchKernelGGL((ln_bwd_kernel<TA, 0>), dim3(grid_rows(Hp, 512)), dim3(256), 0, st, Hp, Hp, H1, a.nf_g, 1e-5f, dY,
                      dmc, row_seg, dH1, nullptr, (int64_t)0, a.g_nf_g, a.g_nf_b);
   NR_LT_CHECK("ln_f_bwd");
   if (dt == NR_BF16) {
@@ -1175,7 +1179,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     return NR_ERR_HIP;
   }
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, S, dS, S, AT, S, nullptr, nullptr, 0, dX, D, st))) return rc;
-  hipLaunchKernelGGL((ln_bwd_kernel<TA, 1>), dim3(grid_rows(Hp, 256)), dim3(256), 0, st, Hp, a.Hs, Sx, a.nq_g, 1e-5f,
+  hipLaunchKernelGGL((ln_bwd_kernel<TA, 1>), dim3(grid_rows(Hp, 512)), dim3(256), 0, st, Hp, a.Hs, Sx, a.nq_g, 1e-5f,
                      dX, dH1, a.hist_idx, nullptr, dE, (int64_t)D, a.g_nq_g, a.g_nq_b);
   NR_LT_CHECK("ln_q_bwd");
   // token LayerNorm parameter grads from dE (history scatter + cosine grads)
