@@ -17,13 +17,15 @@ WORLD_SIZE in the environment re-launches this script under
 ``torch.distributed.run`` with N ranks (as a child process, before any GPU
 call).  Every rank transforms 1/N of the news table and one RCCL all-gather
 gives every GPU the whole table (the path's one exchange step); impressions
-are the shard unit.  Default ``--scaling weak``: every rank pools + scores
-its own full MIND-large-dev-sized impression set (per-GPU work fixed as N
-grows, rank 0's set = the N = 1 set); ``value`` = all ranks' candidates / the
-step time, timed from a barrier to the last rank's completion (max over
-ranks).  ``--scaling strong`` (and the ``strong_scaling`` extra at N > 1) is
-configs[3] as ONE eval job: one set split into N contiguous cost-balanced
-ranges (``partition_by_cost``).
+are the shard unit.  Default ``--scaling strong`` = BASELINE configs[3] as ONE
+eval job: the MIND-large-dev set split into N contiguous cost-balanced ranges
+(``partition_by_cost``); ``value`` = the set's candidates / the step time,
+timed from a barrier to the last rank's completion (max over ranks); the
+per-rank pool_score times and their max / mean are in ``extra``.  At N > 1
+the extras add the same strong-scaling step on the MIND-large *test* shape
+(2.37 M impressions, so per-GPU work stays large at N = 8) and the weak-scaling
+reading (``--scaling weak``: every rank its own full MIND-large-dev-sized set,
+per-GPU work fixed as N grows, rank 0's set = the N = 1 set).
 
 Also reported in the same JSON line:
   roofline      the pool+score kernel (dominant; a random-row gather served by
@@ -221,6 +223,19 @@ def rank_parity(run: Run, n_check: int = 200, seed: int = 0) -> float:
         ref = (e @ u) / u.norm().clamp_min(1e-8) / e.norm(dim=1).clamp_min(1e-8)
         err = max(err, float((s[co[i]:co[i + 1]].double() - ref).abs().max()))
     return err
+
+
+def rank_balance(pool_ms: float, imps, dev, host_reduce: bool, world: int) -> dict:
+    """Every rank's pool_score time and candidate count (all-gathered), with the
+    max / mean of the times: how evenly partition_by_cost split the work."""
+    red = "cpu" if host_reduce else dev
+    mine = torch.tensor([pool_ms, float(imps.n_cand), float(imps.n_imp)], dtype=torch.float64, device=red)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    t = [float(x[0]) for x in allr]
+    return {"pool_score_ms_per_rank": [round(x, 4) for x in t],
+            "candidates_per_rank": [int(x[1]) for x in allr], "impressions_per_rank": [int(x[2]) for x in allr],
+            "pool_score_max_over_mean": round(max(t) / (sum(t) / len(t)), 4) if sum(t) > 0 else None}
 
 
 def table_digest(t: torch.Tensor) -> int:
@@ -603,10 +618,59 @@ def load_traffic(pooler: str, dtype: str):
     return None
 
 
+class _DryRunEngine:
+    """CPU stand-in for PoolScoreEngine in --dry-run (no GPU): the per-news
+    "transform" is a fixed elementwise map (tanh(x) + 0.25 x) and pool + score
+    is the latent pooler in float64 (mean of the history rows, F.normalize,
+    cosine with the per-vector 1e-8 clamps).  Exercises ShardedTable's real
+    partition -> all-gather -> gather_scores path over gloo; the kernels
+    themselves are covered by the GPU tests."""
+
+    pooler = "latent"
+
+    def __init__(self, table: torch.Tensor, imps):
+        self.hist_src, self.cand_table, self.imps = table, table, imps
+        self.dtype, self.device, self.hist_table = table.dtype, table.device, None
+
+    def transform(self, rows=None, out=None, src=None):
+        src = self.hist_src if src is None else src
+        x = src if rows is None else src[rows]
+        res = torch.tanh(x) + 0.25 * x
+        if out is None:
+            return res
+        out.copy_(res)
+        return out
+
+    def inv_norms(self):
+        pass
+
+    def pool_score(self, want_users=False, scores=None):
+        im = self.imps
+        tab = self.hist_table.double()
+        ho = torch.as_tensor(im.hist_off())
+        seg = torch.repeat_interleave(torch.arange(im.n_imp), torch.as_tensor(im.hist_len, dtype=torch.int64))
+        u = torch.zeros((im.n_imp, tab.shape[1]), dtype=torch.float64)
+        u.index_add_(0, seg, tab[torch.as_tensor(im.hist_idx, dtype=torch.int64)])
+        u = u / (ho[1:] - ho[:-1]).clamp_min(1).double()[:, None]
+        u = u / u.norm(dim=1, keepdim=True).clamp_min(1e-12)
+        e = self.cand_table.double()[torch.as_tensor(im.cand_idx, dtype=torch.int64)]
+        cseg = torch.repeat_interleave(torch.arange(im.n_imp), torch.as_tensor(im.cand_len, dtype=torch.int64))
+        uc = u[cseg]
+        s = (e * uc).sum(1) / uc.norm(dim=1).clamp_min(1e-8) / e.norm(dim=1).clamp_min(1e-8)
+        return s, None
+
+
 def dry_run(args, rank: int, world: int) -> None:
-    """--dry-run (CPU, gloo): the launch / partition / all-gather / max-over-ranks
-    plumbing without the GPU (what the CPU test suite can check)."""
+    """--dry-run (CPU, gloo): the multi-rank path without the GPU (what the CPU
+    test suite can check): the impression split (strong: one set partitioned by
+    cost; weak: a set per rank), the real ShardedTable (each rank transforms its
+    1/world shard of the news table, one all-gather), pool + score on the rank's
+    range (_DryRunEngine), gather_scores back to impression order, and parity of
+    the gathered scores against one process scoring the whole set from the
+    whole, unsharded transform; timing max over ranks."""
+    from news_recommendation_project_v2_amd.distributed import gather_scores
     n_news, n_imp = synthetic.SHAPES[args.shape]
+    n_news = args.dry_run_news or n_news
     n_imp = args.impressions or n_imp
     if args.scaling == "strong":
         full = synthetic.mind_impressions(n_news, n_imp, seed=1234)
@@ -614,27 +678,47 @@ def dry_run(args, rank: int, world: int) -> None:
         mine = full.slice(int(b[rank]), int(b[rank + 1]))
         expected = full.n_cand
     else:  # every rank its own set; rank r's candidates summed over the ranks
-        b = None
+        b, full = None, None
         mine = synthetic.mind_impressions(n_news, n_imp, seed=1234 + rank)
         expected = sum(synthetic.mind_impressions(n_news, n_imp, seed=1234 + r).n_cand for r in range(world))
-    rows = (n_news + world - 1) // world
-    local = torch.full((rows, 4), float(rank))
-    table = torch.empty((rows * world, 4))
+    g = torch.Generator().manual_seed(1234)
+    table = torch.randn((n_news, 1024), generator=g, dtype=torch.float32)
+    eng = _DryRunEngine(table, mine)
+    tab = ShardedTable(eng, rank, world)
+    dist.barrier()
     t0 = time.perf_counter()
-    dist.all_gather_into_tensor(table, local)
+    local, _ = sharded_step(tab)
+    dist.barrier()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    # the all-gathered table equals the unsharded transform on every rank
+    whole = _DryRunEngine(table, mine).transform()
+    ok_tab = torch.tensor([int(torch.equal(tab.full[:n_news], whole))])
+    dist.all_reduce(ok_tab, op=dist.ReduceOp.MIN)
+    if args.scaling == "strong":  # scores back in impression order == one process over the whole set
+        got = gather_scores(local, world)
+        ref_eng = _DryRunEngine(table, full)
+        ref_eng.hist_table = whole
+        want, _ = ref_eng.pool_score()
+        ok_sc = int(got.shape == want.shape and torch.equal(got, want))
+    else:
+        ref_eng = _DryRunEngine(table, mine)
+        ref_eng.hist_table = whole
+        want, _ = ref_eng.pool_score()
+        ok_sc = int(torch.equal(local, want))
+    ok_s = torch.tensor([ok_sc])
+    dist.all_reduce(ok_s, op=dist.ReduceOp.MIN)
     c = torch.tensor([mine.n_cand, mine.n_imp], dtype=torch.int64)
     dist.all_reduce(c)
-    ok = bool(torch.equal(table[:, 0], torch.arange(world).repeat_interleave(rows).float()))
     if rank == 0:
         print(json.dumps({"metric": "scored candidates/sec on MIND-large impressions; AUC parity vs CPU ref",
                           "dry_run": True, "value": None, "n_gpus": world, "scaling": args.scaling,
-                          "partition": [int(x) for x in b] if b is not None else None,
+                          "n_news": n_news, "partition": [int(x) for x in b] if b is not None else None,
                           "candidates_total": int(c[0]),
                           "impressions_total": int(c[1]), "candidates_expected": int(expected),
-                          "allgather_ok": ok, "allgather_s": float(t.item())}), flush=True)
+                          "allgather_ok": bool(ok_tab.item()), "scores_match_single_process": bool(ok_s.item()),
+                          "step_s": float(t.item())}), flush=True)
 
 
 def main():
@@ -646,9 +730,9 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--shape", default="mind_large_dev", choices=list(synthetic.SHAPES))
     ap.add_argument("--impressions", type=int, default=0, help="override the shape's impression count")
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak",
-                    help="weak (default): a full MIND-large-dev-sized set per rank, the per-GPU work fixed as N "
-                         "grows; strong: one set partitioned over the ranks (configs[3] as one eval job)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong (default): one MIND-large-dev set partitioned over the ranks (configs[3] as one "
+                         "eval job); weak: a full set per rank, the per-GPU work fixed as N grows (an extra at N > 1)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="gloo: test mode, ranks may share one GPU (tables staged through the host)")
     ap.add_argument("--cpu-shape", default="mind_small_dev", choices=list(synthetic.SHAPES))
@@ -659,6 +743,7 @@ def main():
     ap.add_argument("--no-auc-gate", action="store_true",
                     help="skip the full-size (376,471-impression) AUC parity gate vs the CPU reference")
     ap.add_argument("--dry-run", action="store_true", help="CPU-only check of the multi-rank plumbing")
+    ap.add_argument("--dry-run-news", type=int, default=8192, help="--dry-run news-table rows (0: the shape's)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -735,6 +820,9 @@ def main():
              "history_slots_rank0": imps.n_hist, "candidates_total": total_cand}
     if bounds is not None and world > 1:
         extra["partition"] = [int(x) for x in bounds]
+    if world > 1:
+        # load balance of the impression split: every rank's pool_score time (HIP events)
+        extra.update(rank_balance(stages[2], imps, dev, host_reduce, world))
     if world > 1:
         # phase A / phase B separately: the shard's transform, then the RCCL all-gather
         # (events on the current stream, which waits for RCCL's stream at the end of the call)
@@ -838,6 +926,24 @@ def main():
         extra[key]["parity_max_abs_err"] = float(pt.item())
         extra[key]["parity_ok"] = bool(float(pt.item()) <= 2e-5)
         del r, other
+        _lib.empty_cache()
+        # configs[3]'s strong scaling on the MIND-large *test* shape: 2.37 M impressions
+        # over 121 k news keep ~300 k impressions per GPU at N = 8
+        tn, ti = synthetic.SHAPES["mind_large_test"]
+        one = synthetic.mind_impressions(tn, ti, seed=1234)
+        ob = partition_by_cost(one.hist_len, one.cand_len, world, kw * 1024 * es, 1024 * es)
+        part = one.slice(int(ob[rank]), int(ob[rank + 1]))
+        n_total = one.n_cand
+        del one
+        tb = news_table(tn, dev)
+        r = Run(args.pooler, args.dtype, part, tb, dev, rank, world)
+        d = timed(r.step, max(3, args.steps // 2), 2, world, dev, host_reduce) / max(3, args.steps // 2)
+        st = r.stage_times(2)
+        extra["strong_scaling_mind_large_test"] = {
+            "n_news": tn, "impressions": ti, "candidates": int(n_total), "value": round(n_total / d, 1),
+            "ms_per_step": round(d * 1e3, 3), "partition": [int(x) for x in ob],
+            **rank_balance(st[2], part, dev, host_reduce, world)}
+        del r, tb, part
         _lib.empty_cache()
 
     if world == 1 and not args.no_extra:

@@ -233,3 +233,15 @@ class LatentAttentionComponent(FinalAttentionComponent):
 
 def labels_of(context_dict) -> np.ndarray:
     return context_dict["labels"]
+
+
+# Experiments the reference's scripts import by name (scripts/eval.py:6-20,
+# train_v3.py:6-17, train.py / train_v2.py) but that are outside the hot path
+# (SURVEY §8(f)4): import-level placeholders only; constructing one raises.
+from .out_of_scope import placeholder_class as _oos  # noqa: E402
+
+ClassificationComponent = _oos("ClassificationComponent", "components.py:261-372", __name__, PipelineComponent)
+AttentionWeightComponent = _oos("AttentionWeightComponent", "components.py:375-474", __name__, PipelineComponent)
+AttentionComponent = _oos("AttentionComponent", "components.py:477-643", __name__, PipelineComponent)
+AttentionReduceComponent = _oos("AttentionReduceComponent", "components.py:646-757", __name__, PipelineComponent)
+NewAttentionComponent = _oos("NewAttentionComponent", "components.py:760-855", __name__, PipelineComponent)

@@ -128,3 +128,20 @@ def store_embeddings(model_path: str, news_list: Iterable[str], news_text_dict: 
     enc = XLMREncoder.from_pretrained_dir(model_path, dtype=dtype)
     texts = [news_text_dict[n] for n in news_list]
     return store_token_states(enc, *tokenize(tok, texts, NEWS_TEXT_MAXLEN), db_name)
+
+
+# The classification-baseline blend and the reduce-model experiments
+# (data_model_helper.py:87-109, 134-171, 242-371) are outside the hot path
+# (SURVEY §8(f)4): import-level placeholders only; calling one raises.
+from .out_of_scope import placeholder_function as _oos  # noqa: E402
+
+get_reduced_dim_embeds = _oos("get_reduced_dim_embeds", "data_model_helper.py:87-88", __name__)
+get_classification_preds = _oos("get_classification_preds", "data_model_helper.py:91-98", __name__)
+get_classification_baseline_scores = _oos("get_classification_baseline_scores", "data_model_helper.py:101-109",
+                                          __name__)
+get_cos_sim_reduce_scores = _oos("get_cos_sim_reduce_scores", "data_model_helper.py:134-171", __name__)
+get_cos_sim_final_score = _oos("get_cos_sim_final_score", "data_model_helper.py:242-269", __name__)
+get_final_score = _oos("get_final_score", "data_model_helper.py:272-301", __name__)
+get_final_only_attention_score = _oos("get_final_only_attention_score", "data_model_helper.py:304-335", __name__)
+get_final_only_reduce_attention_score = _oos("get_final_only_reduce_attention_score", "data_model_helper.py:338-371",
+                                             __name__)

@@ -250,6 +250,25 @@ def pad_to_maxlen(grouped_items) -> dict[str, np.ndarray]:
     return {"indices": idx, "attention_mask": mask}
 
 
+def expand_items(items: np.ndarray, rev_index: np.ndarray, imp_counts: np.ndarray) -> np.ndarray:
+    """``items[rev_index]`` concatenated over the impression runs (data_utils.py:391-397).
+    The runs tile ``rev_index`` in order, so this is one gather of its first
+    ``sum(imp_counts)`` entries."""
+    n = int(np.sum(imp_counts, dtype=np.int64))
+    return np.asarray(items)[np.asarray(rev_index)[:n]]
+
+
+def final_attention_eval_collate_fn(input, news_embeddings: torch.Tensor):
+    """Padded, masked history rows of a batch of impressions (data_utils.py:784-791):
+    the host-side batch the reference feeds its pooler.  The MI355X path never
+    builds it (the pooling kernels read the CSR history directly, DESIGN §3.1);
+    it is kept for callers of the reference's DataLoader pipeline."""
+    padded = pad_to_maxlen(input)
+    indices = torch.tensor(padded["indices"])
+    attention_mask = torch.tensor(padded["attention_mask"])
+    return news_embeddings[indices] * attention_mask.unsqueeze(-1), attention_mask
+
+
 def to_csr(rev_index: np.ndarray, len_list: np.ndarray, device=None):
     """(flat int32 indices, per-row lengths) -> device (int32 idx, int64 offsets)."""
     idx = torch.as_tensor(np.ascontiguousarray(rev_index, dtype=np.int32))
@@ -265,8 +284,8 @@ def eval_collate_fn(input: Iterable[str], tokenizer, max_len: int):
     return tokenizer(list(input), max_length=max_len, padding=True, truncation=True, return_tensors="pt")
 
 
-class NewsTextDataset(Dataset):
-    """news id -> text (data_utils.py:485-487)."""
+class AbstractTextDataset(Dataset):
+    """news ids + id -> text map (data_utils.py:458-468)."""
 
     def __init__(self, text_list, news_text_dict: dict[str, str]):
         self.text_list = list(text_list)
@@ -276,7 +295,27 @@ class NewsTextDataset(Dataset):
         return len(self.text_list)
 
     def __getitem__(self, idx):
+        raise NotImplementedError
+
+
+class NewsTextDataset(AbstractTextDataset):
+    """news id -> text (data_utils.py:485-487)."""
+
+    def __getitem__(self, idx):
         return self.news_text_dict[self.text_list[idx]]
+
+
+class EmbeddingDataset(Dataset):
+    """Rows of an embedding table (data_utils.py:490-498)."""
+
+    def __init__(self, embeds):
+        self.embeds = embeds
+
+    def __len__(self):
+        return len(self.embeds)
+
+    def __getitem__(self, idx):
+        return self.embeds[idx]
 
 
 class FinalAttentionEvalDataset(Dataset):
@@ -488,3 +527,75 @@ def train_batch_csr(conn, rows, maxlen: Optional[int] = None):
     B = len(pos)
     return (last, rev[:Hs].astype(np.int32), lengths_to_offsets(lens), rev[Hs:Hs + B].astype(np.int32),
             rev[Hs + B:].astype(np.int32))
+
+
+# ----------------------------------------------------------- raw TSV -> parquet
+# The preprocessing step upstream of load_dataset (data_utils.py:125-165,
+# 418-455, 846-875): raw MIND TSVs -> the processed parquet layout load_dataset
+# reads.  Host I/O only; written for the same file names and columns.
+
+_NEWS_COLUMNS = ["NewsID", "Category", "SubCategory", "Title", "Abstract", "URL", "Title Entities",
+                 "Abstract Entities"]
+
+
+def read_data(data_dir: Path, news_dataset: NewsDataset):
+    """(behaviors, news, entity_embeds) from ``{data_dir}/raw/{split}/`` (data_utils.py:125-165)."""
+    import pandas as pd
+    raw = Path(data_dir) / "raw" / news_dataset.value
+    behaviors = pd.read_csv(raw / "behaviors.tsv", sep="\t", header=None,
+                            names=["ImpressionID", "UserID", "Time", "History", "Impressions"], parse_dates=["Time"])
+    news = pd.read_csv(raw / "news.tsv", sep="\t", header=None, names=_NEWS_COLUMNS)
+    entity = pd.read_csv(raw / "entity_embedding.vec", sep="\t", header=None)
+    return behaviors, news, entity.drop(columns=[101]).set_index(0).T.to_dict("list")
+
+
+def process_news(news_df):
+    """Adds ``news_text = "Title: {Title}"`` (data_utils.py:430-439, config.py's passage form)."""
+    news_df["news_text"] = "Title: " + news_df["Title"].astype(str)
+    return news_df
+
+
+def get_data(data_dir: Path, news_dataset: NewsDataset):
+    """read_data + process_news (data_utils.py:418-427)."""
+    behaviors, news, entity_embeds = read_data(data_dir, news_dataset)
+    return behaviors, process_news(news), entity_embeds
+
+
+def store_processed_data(data_dir: Path, news_dataset: NewsDataset) -> None:
+    """Writes ``{data_dir}/processed/{split}/{behaviors,news_text}.parquet`` and
+    ``entity_embeds.pkl`` (data_utils.py:442-455)."""
+    import joblib
+    behaviors, news_text, entity_embeds = get_data(data_dir, news_dataset)
+    out = Path(data_dir) / "processed" / news_dataset.value
+    out.mkdir(parents=True, exist_ok=True)
+    behaviors.to_parquet(out / "behaviors.parquet")
+    news_text.to_parquet(out / "news_text.parquet")
+    joblib.dump(entity_embeds, out / "entity_embeds.pkl")
+
+
+def main(argv: Optional[Sequence[str]] = None) -> None:
+    """``python -m news_rec_utils.data_utils DATA_DIR SPLIT`` (data_utils.py:846-875)."""
+    import argparse
+    parser = argparse.ArgumentParser(description="Process news dataset and store the results.")
+    parser.add_argument("data_dir", type=Path, help="Path to the directory containing data")
+    parser.add_argument("news_dataset", choices=NewsDataset._member_names_, help="Select the news dataset")
+    args = parser.parse_args(argv)
+    if not args.data_dir.is_dir():
+        parser.error(f"The path '{args.data_dir}' is not a valid directory.")
+    store_processed_data(args.data_dir, NewsDataset[args.news_dataset])
+
+
+# The InfoNCE / classification experiments' data helpers (SURVEY §8(f)4):
+# import-level placeholders only.
+from .out_of_scope import placeholder_class as _oos_cls, placeholder_function as _oos_fn  # noqa: E402
+
+split_impressions = _oos_fn("split_impressions", "data_utils.py:235-272", __name__)
+split_impressions_pos_neg_infonce = _oos_fn("split_impressions_pos_neg_infonce", "data_utils.py:275-334", __name__)
+final_attention_train_infonce_collate_fn = _oos_fn("final_attention_train_infonce_collate_fn", "data_utils.py:794-817",
+                                                   __name__)
+final_attention_train_collate_fn = _oos_fn("final_attention_train_collate_fn", "data_utils.py:820-843", __name__)
+FinalAttentionTrainInfoNCEDataset = _oos_cls("FinalAttentionTrainInfoNCEDataset", "data_utils.py:512-578", __name__,
+                                             Dataset)
+ClassificationTrainInfoNCEDataset = _oos_cls("ClassificationTrainInfoNCEDataset", "data_utils.py:648-685", __name__,
+                                             Dataset)
+ClassificationTrainDataset = _oos_cls("ClassificationTrainDataset", "data_utils.py:688-720", __name__, Dataset)

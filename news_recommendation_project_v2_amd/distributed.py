@@ -57,21 +57,56 @@ class NrComm:
     issues ncclAllGather on the current torch stream."""
 
     def __init__(self, rank: int, world: int, group=None):
+        """Collective over the group: every rank returns, or every rank raises.
+        A failure on one rank is agreed on before the next collective step (a
+        status byte travels with the id; a MIN all-reduce of a ready flag
+        precedes nr_comm_init and one of a success flag follows it), so no rank
+        is left waiting in a collective its peers have abandoned.  What this
+        cannot cover is a rank dying INSIDE ncclCommInitRank after the ready
+        check: RCCL's blocking init has no timeout."""
         import ctypes
         from . import _lib
-        self._lib = _lib.load()
         self.rank, self.world = rank, world
-        idb = (ctypes.c_ubyte * 128)()
-        if rank == 0:
-            _lib.check(self._lib.nr_comm_unique_id(idb), "nr_comm_unique_id")
-        dev = torch.device("cuda", torch.cuda.current_device())
-        staged = _host_staged(group)
-        t_id = torch.tensor(list(idb), dtype=torch.uint8, device="cpu" if staged else dev)
-        dist.broadcast(t_id, src=0, group=group)
-        idb = (ctypes.c_ubyte * 128)(*t_id.cpu().tolist())
-        self._lib.nr_init(dev.index)
         self._h = ctypes.c_void_p()
-        _lib.check(self._lib.nr_comm_init(ctypes.byref(self._h), idb, world, rank), "nr_comm_init")
+        flag_dev = "cpu" if _host_staged(group) else torch.device("cuda", torch.cuda.current_device())
+        buf = (ctypes.c_ubyte * (1 + 128))()
+        err = None
+        try:
+            self._lib = _lib.load()
+            if rank == 0:
+                _lib.check(self._lib.nr_comm_unique_id(ctypes.cast(ctypes.byref(buf, 1),
+                                                                   ctypes.POINTER(ctypes.c_ubyte))),
+                           "nr_comm_unique_id")
+                buf[0] = 1
+        except Exception as e:  # noqa: BLE001  (reported on every rank below)
+            err = e
+        t_id = torch.tensor(list(buf), dtype=torch.uint8, device=flag_dev)
+        dist.broadcast(t_id, src=0, group=group)
+        if int(t_id[0].item()) != 1:
+            raise RuntimeError(f"NrComm: rank 0 could not create the RCCL unique id ({err!r})")
+        idb = (ctypes.c_ubyte * 128)(*t_id[1:].cpu().tolist())
+        try:
+            if err is None:
+                _lib.check(self._lib.nr_init(torch.cuda.current_device()), "nr_init")
+        except Exception as e:  # noqa: BLE001
+            err = e
+        self._agree(err is None, group, flag_dev, "before nr_comm_init", err)
+        try:
+            _lib.check(self._lib.nr_comm_init(ctypes.byref(self._h), idb, world, rank), "nr_comm_init")
+        except Exception as e:  # noqa: BLE001
+            err = e
+        try:
+            self._agree(err is None, group, flag_dev, "in nr_comm_init", err)
+        except RuntimeError:
+            self.close()
+            raise
+
+    def _agree(self, ok: bool, group, flag_dev, where: str, err) -> None:
+        """MIN all-reduce of this rank's flag: raise on every rank if any failed."""
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=flag_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        if int(t.item()) != 1:
+            raise RuntimeError(f"NrComm: a rank failed {where} (this rank: {err!r})")
 
     def allgather(self, send: torch.Tensor, recv: torch.Tensor) -> None:
         from . import _lib
@@ -81,7 +116,7 @@ class NrComm:
                                           torch.cuda.current_stream().cuda_stream), "nr_allgather")
 
     def close(self) -> None:
-        if self._h:
+        if getattr(self, "_h", None):
             self._lib.nr_comm_destroy(self._h)
             self._h = None
 

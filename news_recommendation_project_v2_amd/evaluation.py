@@ -66,6 +66,17 @@ def _row_metrics(labels, ranks):
         return auc, mrr_score(y_true, y_score), ndcg_score(y_true, y_score, 5), ndcg_score(y_true, y_score, 10)
 
 
+def score_row(label_sub_rank):
+    """(auc, mrr, ndcg5, ndcg10) of one ``(labels, ranks, line index)`` triple
+    (evaluation.py:34-54), the unit ``score`` maps over impressions."""
+    labels, sub_ranks, ind = label_sub_rank
+    for rank in sub_ranks:
+        r = 1.0 / rank
+        if r < 0 or r > 1:
+            raise ValueError("Line-{}: score_rslt should be int from 0 to {}".format(ind, float(len(labels))))
+    return _row_metrics(labels, sub_ranks)
+
+
 def score_arrays(ranks: np.ndarray, labels: np.ndarray, offsets: np.ndarray):
     """Vectorised metrics over flat int ranks / 0-1 labels with CSR offsets.
 

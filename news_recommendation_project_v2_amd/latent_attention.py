@@ -342,3 +342,13 @@ class LatentAttentionModel(torch.nn.Module):
         # and F.normalize (latent_attention.py:166-170) on the [B, D] users
         u = segment_mean(self._train_items(rows), off)
         return torch.nn.functional.normalize(u, p=2, dim=-1) if self.output_normalize else u
+
+
+def exists(val):
+    """latent_attention.py:43-44."""
+    return val is not None
+
+
+def default(val, d):
+    """latent_attention.py:47-48."""
+    return val if exists(val) else d

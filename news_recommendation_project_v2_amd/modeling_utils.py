@@ -11,6 +11,8 @@ from __future__ import annotations
 from pathlib import Path
 from typing import Dict, Optional
 
+import numpy as np
+
 import torch
 import torch.nn.functional as F
 
@@ -320,3 +322,67 @@ def get_embed_from_model(model, text_dataset, text_maxlen: int, text_collate_fn,
     del text_maxlen  # applied by text_collate_fn (eval_collate_fn's max_len)
     loader = DataLoader(text_dataset, batch_size=batch_size, collate_fn=text_collate_fn, shuffle=False)
     return get_text_embed_eval(model, loader)
+
+
+def get_model_eval(dataloader, model: torch.nn.Module) -> torch.Tensor:
+    """Model outputs over a DataLoader, concatenated on the host (modeling_utils.py:402-417):
+    tuple / list batches are unpacked as positional arguments."""
+    out = []
+    model.eval()
+    with torch.no_grad():
+        for item in dataloader:
+            if isinstance(item, (tuple, list)):
+                out.append(model(*(x.to(DEVICE) for x in item)).detach().cpu())
+            else:
+                out.append(model(item.to(DEVICE)).detach().cpu())
+    return torch.cat(out)
+
+
+def store_text_embed_full_eval(model, input_dataloader, db_name) -> int:
+    """Per-token hidden states of every title into the sqlite token DB
+    (modeling_utils.py:456-473): batches are the tokenizer's right-padded
+    ``input_ids`` / ``attention_mask``; the valid tokens of each row are packed
+    and run through the HIP encoder, and each row's [L_valid, 1024] states are
+    stored fp16, ids 1.. in dataloader order (encoder.store_token_states)."""
+    from .encoder import store_token_states
+    ids, lens = [], []
+    for inputs in input_dataloader:
+        mask = torch.as_tensor(inputs["attention_mask"]).bool()
+        ii = torch.as_tensor(inputs["input_ids"])
+        ids.append(ii[mask].to(torch.int32).numpy())
+        lens.append(mask.sum(1).to(torch.int64).numpy())
+    flat = np.concatenate(ids) if ids else np.zeros(0, np.int32)
+    return store_token_states(model, flat, np.concatenate(lens) if lens else np.zeros(0, np.int64), db_name)
+
+
+def store_embed_from_model(model, text_dataset, text_maxlen: int, text_collate_fn, db_name,
+                           batch_size: int = 1024) -> int:
+    """modeling_utils.py:477-495: a sequential DataLoader over the texts, then
+    store_text_embed_full_eval (the batch only sets host tokenisation chunks)."""
+    from torch.utils.data import DataLoader
+    del text_maxlen  # applied by text_collate_fn
+    loader = DataLoader(text_dataset, batch_size=batch_size, collate_fn=text_collate_fn, shuffle=False)
+    return store_text_embed_full_eval(model, loader, db_name)
+
+
+# The classification-head / weighted-sum / reducing / NV-Embed experiments
+# (modeling_utils.py:85-89, 106-172, 326-399, 420-453) are outside the hot path
+# (SURVEY §8(f)4, DESIGN §7): import-level placeholders only.
+from .out_of_scope import placeholder_class as _oos_cls, placeholder_function as _oos_fn  # noqa: E402
+
+get_nvembed_model = _oos_fn("get_nvembed_model", "modeling_utils.py:85-89", __name__)
+get_nv_embeds = _oos_fn("get_nv_embeds", "modeling_utils.py:371-399", __name__)
+ClassificationHead = _oos_cls("ClassificationHead", "modeling_utils.py:106-116", __name__, torch.nn.Module)
+ClassificationHeadCatEmbed = _oos_cls("ClassificationHeadCatEmbed", "modeling_utils.py:119-136", __name__,
+                                      torch.nn.Module)
+get_classification_head = _oos_fn("get_classification_head", "modeling_utils.py:139-148", __name__)
+WeightedSumModel = _oos_cls("WeightedSumModel", "modeling_utils.py:158-165", __name__, torch.nn.Module)
+get_weighted_sum_model = _oos_fn("get_weighted_sum_model", "modeling_utils.py:168-172", __name__)
+EmbeddingWrapper = _oos_cls("EmbeddingWrapper", "modeling_utils.py:326-340", __name__, torch.nn.Module)
+get_embed_wrapped_model = _oos_fn("get_embed_wrapped_model", "modeling_utils.py:343-346", __name__)
+ResizeWrapperModel = _oos_cls("ResizeWrapperModel", "modeling_utils.py:349-364", __name__, torch.nn.Module)
+resize_wrap_model = _oos_fn("resize_wrap_model", "modeling_utils.py:367-368", __name__)
+get_head_model = _oos_fn("get_head_model", "modeling_utils.py:420-427", __name__)
+get_new_attention_model = _oos_fn("get_new_attention_model", "modeling_utils.py:430-435", __name__)
+ReducingModel = _oos_cls("ReducingModel", "modeling_utils.py:438-446", __name__, torch.nn.Module)
+get_reducing_model = _oos_fn("get_reducing_model", "modeling_utils.py:449-453", __name__)

@@ -143,3 +143,13 @@ class AttentionAttentionTrainer:
                     torch.save({k: v.detach().cpu() for k, v in m.state_dict().items()}, Path(d) / f"Epoch_{i + 1}.pt")
             self.train_dataset.reset()
         self.connection.close()
+
+
+# The reference's other trainers (trainer.py:47-949) belong to the experiments
+# outside the hot path: import-level placeholders only.
+from .out_of_scope import placeholder_class as _oos  # noqa: E402
+
+ClassificationModelTrainer = _oos("ClassificationModelTrainer", "trainer.py:47-214", __name__)
+AttentionWeightTrainer = _oos("AttentionWeightTrainer", "trainer.py:217-436", __name__)
+AttentionTrainer = _oos("AttentionTrainer", "trainer.py:439-713", __name__)
+AttentionReduceTrainer = _oos("AttentionReduceTrainer", "trainer.py:716-949", __name__)

@@ -15,8 +15,8 @@
  * checker is pinned to oracle/pool_ref.cos_sim_scores_per_news, itself pinned to
  * the reference's golden vectors, in tests/test_oracle_golden.py).
  *
- * Built by __graft_entry__.build() (gcc -O3 -fopenmp -shared) into
- * oracle/libfastpool.so; loaded by oracle/pool_ref.py only.
+ * Built on first use by oracle/pool_ref.py (gcc -O3 -fopenmp -shared) into
+ * oracle/libfastpool.so, and loaded by it only (test infrastructure).
  */
 #include <math.h>
 #include <stdint.h>

@@ -485,7 +485,42 @@ def gen_dataset(du):
         cat_keys=np.array(list(cat_map)), sub_keys=np.array(list(sub_map)), **out)
 
 
-GENERATORS = ("split", "rank", "final", "latent", "encoder", "token_attn", "train", "dataset")
+def gen_imports():
+    """The reference's Python API surface, read with ``ast`` (no import of the reference):
+    ``scripts``: the exact ``from news_rec_utils... import ...`` lists of its entry
+    scripts (scripts/*.py) as [module, name, line]; ``package``: every top-level
+    class / def / assigned name of each src/news_rec_utils module.
+    tests/test_api_surface.py resolves every name against the alias package."""
+    import ast
+    import json
+    scripts, package = {}, {}
+    for script in sorted((REF_SRC.parent / "scripts").glob("*.py")):
+        names = []
+        for node in ast.walk(ast.parse(script.read_text())):
+            if isinstance(node, ast.ImportFrom) and (node.module or "").split(".")[0] == "news_rec_utils":
+                names += [[node.module, a.name, node.lineno] for a in node.names]
+            elif isinstance(node, ast.Import):
+                names += [[a.name, None, node.lineno] for a in node.names if a.name.split(".")[0] == "news_rec_utils"]
+        scripts[f"scripts/{script.name}"] = names
+    for mod in sorted((REF_SRC / "news_rec_utils").glob("*.py")):
+        names = []
+        for node in ast.parse(mod.read_text()).body:
+            if isinstance(node, (ast.FunctionDef, ast.ClassDef)):
+                names.append([node.name, node.lineno])
+            elif isinstance(node, ast.Assign):
+                names += [[t.id, node.lineno] for t in node.targets if isinstance(t, ast.Name)]
+        package[mod.stem] = names
+    lines = ["{", ' "scripts": {']
+    lines.append(",\n".join(f"  {json.dumps(k)}: {json.dumps(v)}" for k, v in scripts.items()))
+    lines += [" },", ' "package": {']
+    lines.append(",\n".join(f"  {json.dumps(k)}: {json.dumps(v)}" for k, v in package.items()))
+    lines += [" }", "}"]
+    text = "\n".join(lines) + "\n"
+    json.loads(text)
+    (HERE / "api_surface.json").write_text(text)
+
+
+GENERATORS = ("split", "rank", "final", "latent", "encoder", "token_attn", "train", "dataset", "imports")
 
 
 def main():
@@ -493,6 +528,10 @@ def main():
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
     torch.set_num_threads(8)
     which = set(sys.argv[1:]) or set(GENERATORS)
+    if "imports" in which:
+        gen_imports()
+        if which == {"imports"}:
+            return
     dmh, du, ev, la, mu = import_reference()
     from news_recommendation_project_v2_amd import weights as W
     if "split" in which:

@@ -1,8 +1,11 @@
 """bench.py --gpus N without a torch.distributed launcher must start N ranks
 itself (before any GPU call) and report n_gpus = N.  The --dry-run mode runs
-that launch, the impression split (weak: a set per rank, the default; strong:
-one set partitioned), the table all-gather and the max-over-ranks reduction
-over gloo on the CPU."""
+that launch, the impression split (strong, the default: one set partitioned
+by cost = configs[3]; weak: a set per rank), the real ShardedTable
+(per-rank shard transform + all-gather), pool + score of each rank's range,
+the score gather back to impression order and its parity against one process
+scoring the whole set, and the max-over-ranks reduction, over gloo on the
+CPU, up to the driver's world size 8."""
 import json
 import os
 import subprocess
@@ -14,9 +17,9 @@ import pytest
 REPO = Path(__file__).resolve().parents[1]
 
 
-@pytest.mark.parametrize("world,scaling", [(2, "strong"), (3, "strong"), (2, None)])
+@pytest.mark.parametrize("world,scaling", [(2, "weak"), (3, "strong"), (2, None), (8, None)])
 def test_bench_spawns_ranks(world, scaling):
-    """scaling None = the default (weak: every rank its own full set)."""
+    """scaling None = the default (strong: one set partitioned over the ranks)."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     extra = ["--scaling", scaling] if scaling else []
     p = subprocess.run([sys.executable, "bench.py", "--gpus", str(world), "--dry-run", "--impressions", "1500", *extra],
@@ -24,11 +27,11 @@ def test_bench_spawns_ranks(world, scaling):
     assert p.returncode == 0, p.stderr[-2000:]
     line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
     res = json.loads(line)
-    assert res["n_gpus"] == world and res["scaling"] == (scaling or "weak")
-    if scaling == "strong":
+    assert res["n_gpus"] == world and res["scaling"] == (scaling or "strong")
+    if scaling != "weak":
         assert res["partition"][0] == 0 and res["partition"][-1] == 1500 and len(res["partition"]) == world + 1
         assert res["impressions_total"] == 1500
     else:
         assert res["partition"] is None and res["impressions_total"] == 1500 * world
     assert res["candidates_total"] == res["candidates_expected"]
-    assert res["allgather_ok"]
+    assert res["allgather_ok"] and res["scores_match_single_process"]

@@ -1,5 +1,5 @@
 # GEMM change check: GEMM / transform / encoder / training GPU tests, then the A/B timing.
-# Usage: bash tools/gpu_gemm_check.sh OUTDIR
+# Usage: bash tools/sessions/gpu_gemm_check.sh OUTDIR
 set -o pipefail
 OUT=${1:-gpurun_out/gemm}
 mkdir -p "$OUT"

@@ -1,5 +1,5 @@
 # GEMM change check + A/B (current tree vs previous commit vs round-1 base) + stamps.
-# Usage: bash tools/gpu_gemm_check2.sh OUTDIR
+# Usage: bash tools/sessions/gpu_gemm_check2.sh OUTDIR
 set -o pipefail
 OUT=${1:-gpurun_out/gemm}
 L=tools/gemm_lab

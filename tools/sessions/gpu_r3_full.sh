@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-3 full check: the whole -m gpu suite, the default bench line, then the rocprof
-# kernel-trace + PMC passes of tools/profile_round3.sh.  Usage: bash tools/gpu_r3_full.sh <tag>
+# kernel-trace + PMC passes of tools/profile_round3.sh.  Usage: bash tools/sessions/gpu_r3_full.sh <tag>
 set -o pipefail
 OUT=gpurun_out/${1:-r3full}
 mkdir -p "$OUT"

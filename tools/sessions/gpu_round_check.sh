@@ -1,5 +1,5 @@
 # Round check on the GPU box: gpu tests, smoke, bench, encoder bench, rocprof trace of the bench.
-# Usage: bash tools/gpu_round_check.sh OUTDIR
+# Usage: bash tools/sessions/gpu_round_check.sh OUTDIR
 set -o pipefail
 OUT=${1:-gpurun_out/round}
 mkdir -p "$OUT"

@@ -1,5 +1,5 @@
 # GPU check of the current tree: gpu tests, smoke, default bench, 2-rank (gloo) bench spawn.
-# Usage: bash tools/gpu_session_check.sh OUTDIR
+# Usage: bash tools/sessions/gpu_session_check.sh OUTDIR
 set -o pipefail
 OUT=${1:-gpurun_out/check}
 mkdir -p "$OUT"

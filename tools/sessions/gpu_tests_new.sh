@@ -1,5 +1,5 @@
 # GPU check of the tests added this session, then the full gpu suite and the default bench.
-# Usage: bash tools/gpu_tests_new.sh OUTDIR
+# Usage: bash tools/sessions/gpu_tests_new.sh OUTDIR
 set -o pipefail
 OUT=${1:-gpurun_out/new}
 mkdir -p "$OUT"
