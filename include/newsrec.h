@@ -183,6 +183,19 @@ int nr_gemm_grouped(int dtype_in, int dtype_out, int n, const int64_t* M, const 
                     void* const* C, const int64_t* ldc, void* stream);
 
 /*
+ * n independent C_i[M_i, N_i] = alpha_i A_i^T W_i in ONE launch, A_i [K_i][M_i]
+ * and W_i [K_i][N_i] bf16 ROW-major (the reduction index is the row: lda / ldw
+ * = row strides) -- the weight-grad GEMMs dW = dOut^T X of
+ * AttentionAttentionTrainer's backward (trainer.py:1056-1057) on the row-major
+ * activations, without transposed copies (LDS transposed reads).  C f32 or
+ * bf16 (dtype_out).  M, N multiples of 256, K of 64; K = 0 leaves C untouched.
+ * alpha nullable (all 1).
+ */
+int nr_gemm_grouped_tn(int dtype_out, int n, const int64_t* M, const int64_t* N, const int64_t* K,
+                       const void* const* A, const int64_t* lda, const void* const* W, const int64_t* ldw,
+                       void* const* C, const int64_t* ldc, const float* alpha, void* stream);
+
+/*
  * y = LayerNorm(x) * gamma + beta over rows of `dim` (biased variance).
  * Replaces nn.LayerNorm in PreNorm latent_attention.py:10-12,16-19 and
  * MyLayer attention.py:165-166,193.  dim % 256 == 0, dim <= 2048.
@@ -481,6 +494,9 @@ int nr_adamw(int64_t n, float* p, const float* g, float* m, float* v, void* p_bf
  * parameters, biases and latents in f32.  hist_idx: [Hs] indices into the U
  * rows, hist_off [B+1] CSR offsets, pos / neg [B].  users (nullable, f32
  * [B][1024]): the normalized pooled users.  ws: nr_latent_train_workspace_bytes.
+ * CSR contract (not checked on the device): hist_off[0] = 0, hist_off[B] = Hs,
+ * non-decreasing, every row non-empty; 0 <= hist_idx[i] < U.  Both the per-slot
+ * kernels (Hs valid rows) and the per-row means (hist_off) rely on it.
  */
 typedef struct nr_latent_train_args {
   int dtype;
@@ -513,6 +529,56 @@ typedef struct nr_latent_train_args {
 
 int64_t nr_latent_train_workspace_bytes(int dtype, int64_t B, int64_t U, int64_t Hs);
 int nr_latent_train_step(const nr_latent_train_args* args, void* ws, int64_t ws_bytes, void* stream);
+
+/*
+ * ---- Config-5 step with FinalAttention (the pairing scripts/train_v3.py runs:
+ * AttentionAttentionTrainer.train_one_epoch, trainer.py:1044-1066, with
+ * FinalAttention.forward, modeling_utils.py:195-228, in train mode), forward +
+ * backward of one batch as ONE call:
+ *   E  = LN_tok(tok_last)                              (g_mlp_layernorm, eps 1e-12)
+ *   per history slot: S = E[hist]; X1 = drop(relu(S W1^T + b1)); X2 = drop(relu(X1 W2^T + b2))
+ *                     X = X2 W3^T + b3; Y = drop(relu(X W4^T + b4)); P = exp(Y W5^T)
+ *   per batch row:    u = sum X P / (sum P + 1e-10)  (per dimension)
+ *                     loss = MarginRankingLoss(margin)(cos(u, E[pos]), cos(u, E[neg]))
+ * and the exact backward; every gradient is written into its f32 grad buffer.
+ * Dropout p on the three ReLU layers from the counter-hash stream of
+ * nr_gemm_relu_dropout with seed[0..2] (p = 0: the reference's eval-identical
+ * step).  The weight transposes run on an internal side stream joined back to
+ * `stream`, so the step stays ordered on `stream`.  dtype NR_F32: exact-f32 MFMA
+ * and f32 activations (the parity mode); NR_BF16: bf16 operands / activations,
+ * f32 accumulation, statistics and gradients, the bias grads summed from the
+ * f32 GEMM results before rounding, the weight grads read from the row-major
+ * activations (nr_gemm_grouped_tn's kernel).  Weights W1..W5 in `dtype` (the
+ * bf16 mirror for NR_BF16), biases and the token LN parameters f32.  CSR
+ * contract as nr_latent_train_step (hist_off[0] = 0, hist_off[B] = Hs,
+ * non-empty rows, 0 <= hist_idx < U).  users (nullable, f32 [B][1024]): the
+ * pooled users.  ws: nr_final_train_workspace_bytes, 256-byte aligned.
+ */
+typedef struct nr_final_train_args {
+  int dtype;
+  int tok_dtype; /* NR_F32 / NR_BF16 / NR_F16 */
+  int64_t B, U, Hs;
+  const void* tok_last; /* [U][1024] */
+  const int32_t* hist_idx;
+  const int64_t* hist_off;
+  const int32_t* pos;
+  const int32_t* neg;
+  float margin;
+  float p;           /* dropout probability of the three ReLU layers */
+  uint64_t seed[3];  /* their dropout streams */
+  const float *tok_g, *tok_b;
+  const void* W1; const float* b1; /* linear1 [4096][1024] */
+  const void* W2; const float* b2; /* linear2 [4096][4096] */
+  const void* W3; const float* b3; /* linear3 [1024][4096] */
+  const void* W4; const float* b4; /* linear4 [4096][1024] */
+  const void* W5;                  /* linear5 [1024][4096], no bias */
+  float *g_tok_g, *g_tok_b, *g_W1, *g_b1, *g_W2, *g_b2, *g_W3, *g_b3, *g_W4, *g_b4, *g_W5;
+  float* loss;  /* device scalar (set, not accumulated) */
+  float* users; /* nullable [B][1024] */
+} nr_final_train_args;
+
+int64_t nr_final_train_workspace_bytes(int dtype, int64_t B, int64_t U, int64_t Hs);
+int nr_final_train_step(const nr_final_train_args* args, void* ws, int64_t ws_bytes, void* stream);
 
 /*
  * ---- RCCL communicator of the multi-GPU eval (SURVEY §8(b) nr_allgather,

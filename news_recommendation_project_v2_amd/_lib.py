@@ -18,7 +18,7 @@ CSRC = Path(__file__).resolve().with_name("csrc")
 INCLUDE = Path(__file__).resolve().parent.parent / "include"
 # translation units of libnewsrec_hip.so, in link order (also the hash order)
 HIP_SOURCES = ("capi.hip", "gemm.hip", "pool_score.hip", "rowops.hip", "rank.hip", "encoder.hip", "train.hip",
-               "metrics.hip", "comm.hip", "latent_train.hip")
+               "metrics.hip", "comm.hip", "latent_train.hip", "final_train.hip")
 
 
 def hip_source_files() -> list:
@@ -80,6 +80,8 @@ SIGNATURES = {
     "nr_rccl_version": (_i, []),
     "nr_latent_train_workspace_bytes": (_l, [_i, _l, _l, _l]),
     "nr_latent_train_step": (_i, [_p, _p, _l, _p]),
+    "nr_final_train_workspace_bytes": (_l, [_i, _l, _l, _l]),
+    "nr_final_train_step": (_i, [_p, _p, _l, _p]),
     "nr_comm_unique_id": (_i, [_p]),
     "nr_comm_init": (_i, [_p, _p, _i, _i]),
     "nr_comm_destroy": (_i, [_p]),
@@ -92,6 +94,7 @@ SIGNATURES = {
     "nr_gemm_relu_dropout": (_i, [_i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _p, _l, ctypes.c_uint64, _f, _p]),
     "nr_gemm_drelu": (_i, [_i, _i, _l, _l, _l, _p, _l, _p, _l, _p, _l, _p, _l, _f, _p]),
     "nr_gemm_grouped": (_i, [_i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "nr_gemm_grouped_tn": (_i, [_i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "nr_layernorm": (_i, [_i, _i, _l, _l, _p, _l, _p, _p, _f, _p, _l, _p]),
     "nr_gather_layernorm": (_i, [_i, _l, _l, _p, _l, _p, _i, _p, _p, _f, _p, _l, _p]),
     "nr_softmax64": (_i, [_l, _l, _p, _l, _i, _p, _l, _p]),
@@ -148,6 +151,19 @@ class LatentTrainArgs(ctypes.Structure):
                 + [(n, ctypes.c_void_p) for n in ("tok_last", "hist_idx", "hist_off", "pos", "neg")]
                 + [("margin", ctypes.c_float)]
                 + [(n, ctypes.c_void_p) for n in LATENT_TRAIN_PARAMS + LATENT_TRAIN_GRADS + ("loss", "users")])
+
+
+FINAL_TRAIN_PARAMS = ("tok_g", "tok_b", "W1", "b1", "W2", "b2", "W3", "b3", "W4", "b4", "W5")
+FINAL_TRAIN_GRADS = tuple("g_" + n for n in FINAL_TRAIN_PARAMS)
+
+
+class FinalTrainArgs(ctypes.Structure):
+    """struct nr_final_train_args (include/newsrec.h)."""
+    _fields_ = ([("dtype", ctypes.c_int), ("tok_dtype", ctypes.c_int), ("B", ctypes.c_int64), ("U", ctypes.c_int64),
+                 ("Hs", ctypes.c_int64)]
+                + [(n, ctypes.c_void_p) for n in ("tok_last", "hist_idx", "hist_off", "pos", "neg")]
+                + [("margin", ctypes.c_float), ("p", ctypes.c_float), ("seed", ctypes.c_uint64 * 3)]
+                + [(n, ctypes.c_void_p) for n in FINAL_TRAIN_PARAMS + FINAL_TRAIN_GRADS + ("loss", "users")])
 
 
 class NewsRecHIPError(RuntimeError):

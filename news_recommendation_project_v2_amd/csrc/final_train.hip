@@ -1,0 +1,377 @@
+// Config-5 training step with the FinalAttention pooler -- the pairing the
+// reference's scripts/train_v3.py trains (AttentionAttentionTrainer,
+// trainer.py:1030-1117; FinalAttention.forward, modeling_utils.py:195-228) --
+// forward and backward of one batch as one C call (nr_final_train_step,
+// include/newsrec.h):
+//
+//   E  = g_mlp_LN(last token)                               token model (attention.py:193)
+//   per history slot (packed valid rows, CSR order, zero rows up to Hp = pad64(Hs)):
+//        S = E[hist];  X1 = drop(relu(S W1^T + b1));  X2 = drop(relu(X1 W2^T + b2))
+//        X = X2 W3^T + b3;  Y = drop(relu(X W4^T + b4));  P = exp(Y W5^T)
+//   per batch row: u_d = sum_i X_id P_id / (sum_i P_id + 1e-10)   (modeling_utils.py:224-228)
+//        loss = MarginRankingLoss(2)(cos(u, E[pos]), cos(u, E[neg]))   (trainer.py:1058-1066)
+//   backward: pool' -> dL (logits of linear5), dXp (X) -> dY = drop'(dL W5) -> dX = dY W4 + dXp
+//        -> dZ2 = drop'(dX W3) -> dZ1 = drop'(dZ2 W2) -> dS = dZ1 W1 -> dE[hist] += dS
+//        weight grads dW5 = dL^T Y, dW4 = dY^T X, dW3 = dX^T X2, dW2 = dZ2^T X1, dW1 = dZ1^T S
+//        bias grads = column sums of dY, dX, dZ2, dZ1; token LayerNorm parameter grads.
+//
+// FinalAttention runs once per VALID history slot (the reference's padded slots
+// carry zero pooling weight and so zero gradient).  Dropout: the counter-hash
+// stream of nr_gemm_relu_dropout (oracle/train_ref.py restates it).
+//
+// bf16 (the throughput mode): every GEMM on the persistent MFMA kernel, the
+// N = 4096 ones with the rows past the last whole tile round as split-K slices
+// (+ nr_splitk_fixup); the bias gradients as f32 column sums written by the
+// data-grad GEMMs' epilogues (no re-read of dY / dX / dZ2 / dZ1); the five
+// weight-grad GEMMs as ONE grouped TN launch that reads the row-major
+// activations through transposed LDS reads (no transposed copies); the five
+// weight transposes the data-grad GEMMs need on a side stream beside the
+// forward.  f32 (the parity mode): the same sequence on the exact-f32 MFMA tile
+// kernels, with explicit transposes for the weight grads.
+#include "nr_common.h"
+
+namespace nr {
+namespace ft {
+
+constexpr int64_t D = 1024, H = 4096;
+constexpr int kSplit = 8;  // K-slices of a split-K tail
+
+static int64_t pad64(int64_t n) { return n < 64 ? 64 : (n + 63) / 64 * 64; }
+static int64_t al(int64_t b) { return (b + 255) / 256 * 256; }
+
+// ------------------------------------------------------------------ small kernels
+struct ZList {  // zero up to 8 f32 ranges in one launch
+  float* p[8];
+  int64_t len[8];
+  int n;
+};
+__global__ __launch_bounds__(256) void zero_kernel(ZList z) {
+  for (int i = 0; i < z.n; ++i)
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < z.len[i]; j += (int64_t)gridDim.x * 256)
+      z.p[i][j] = 0.f;
+}
+
+// S[i] = E[hist[i]] for i < Hs, zero rows for Hs <= i < Hp (the packed history
+// slots); f32 -> TA, 4 columns per lane (16-B loads), one wave per row.
+template <typename TA>
+__global__ __launch_bounds__(256) void gather_slots_kernel(int64_t Hp, int64_t Hs, const float* __restrict__ E,
+                                                           const int32_t* __restrict__ hist, TA* __restrict__ S) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < Hp; i += (int64_t)gridDim.x * 4) {
+    const int64_t r = i < Hs ? (int64_t)hist[i] : -1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t c = 256 * j + 4 * lane;
+      const f32x4 v = r >= 0 ? *reinterpret_cast<const f32x4*>(E + r * D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (sizeof(TA) == 4) {
+        *reinterpret_cast<f32x4*>(S + i * D + c) = v;
+      } else {
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<bf16x4*>(S + i * D + c) = __builtin_convertvector(v, bf16x4);
+      }
+    }
+  }
+}
+
+// out[r0 / 128 + b][c] = sum of rows [r0 + 128 b, r0 + 128 (b + 1)) of src's column c
+// (rows < rows_end): the column sums of a split-K tail's rows, in the layout of
+// the persistent GEMM's CS partials.  Block = 256 columns x one 128-row block.
+template <typename TA>
+__global__ __launch_bounds__(256) void colsum_block_kernel(int64_t r0, int64_t rows_end, int64_t cols, const TA* src,
+                                                           int64_t lds, float* out) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t b0 = r0 + (int64_t)blockIdx.y * 128;
+  if (c >= cols) return;
+  float s = 0.f;
+  const int64_t e = b0 + 128 < rows_end ? b0 + 128 : rows_end;
+  for (int64_t r = b0; r < e; ++r) s += (float)src[r * lds + c];
+  out[(b0 >> 7) * cols + c] = s;
+}
+
+// g[c] = sum_r part[r][c] over up to 4 (partials, rows, cols, out) problems: the
+// bias gradients (fixed row order: deterministic).
+struct RSum {
+  const float* part[4];
+  float* out[4];
+  int64_t rows[4], cols[4];
+  int n;
+};
+__global__ __launch_bounds__(256) void rowsum_kernel(RSum r) {
+  int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int i = 0; i < r.n; ++i) {
+    if (c < r.cols[i]) {
+      float s = 0.f;
+      for (int64_t k = 0; k < r.rows[i]; ++k) s += r.part[i][k * r.cols[i] + c];
+      r.out[i][c] = s;
+      return;
+    }
+    c -= r.cols[i];
+  }
+}
+
+// ------------------------------------------------------------------ workspace
+struct Layout {
+  int64_t Hp, es, mm, csr;
+  int64_t E, S, X1, X2, XP, Y, users, z, du, dE, dXp, dL, dY, dX, dZ2, dZ1, dS;
+  int64_t W1t, W2t, W3t, W4t, W5t, skP, cs4, cs3, cs2, cs1;
+  int64_t T[10];  // f32 mode: the weight-grad operands transposed
+  int64_t total;
+};
+
+// rows of the N = 4096 GEMMs that fill whole rounds of 256x256 tiles over the
+// CUs (the rest run as kSplit K-slices + fixup); Hp when no split pays
+static int64_t main_rows(int dtype, int64_t Hp, int ncu) {
+  const int64_t ntn = H / 256;
+  if (dtype != NR_BF16 || Hp % 256 == 0 || ncu % ntn) return Hp;
+  const int64_t per = 256 * (ncu / ntn);
+  const int64_t mm = Hp / per * per;
+  const int64_t tail_tiles = (Hp - mm + 255) / 256 * ntn;
+  return mm > 0 && tail_tiles * 4 <= ncu ? mm : Hp;
+}
+
+static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs, int ncu) {
+  Layout L{};
+  L.Hp = pad64(Hs);
+  L.es = dtype == NR_F32 ? 4 : 2;
+  L.mm = main_rows(dtype, L.Hp, ncu);
+  L.csr = (L.Hp + 127) / 128;
+  const int64_t Hp = L.Hp, es = L.es, Bp = pad64(B);
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) { const int64_t r = o; o += al(bytes); return r; };
+  L.E = take(U * D * 4);
+  L.S = take(Hp * D * es); L.X1 = take(Hp * H * es); L.X2 = take(Hp * H * es); L.XP = take(Hp * 2 * D * es);
+  L.Y = take(Hp * H * es);
+  L.users = take(Bp * D * 4); L.z = take(Bp * D * 4); L.du = take(Bp * D * 4); L.dE = take(U * D * 4);
+  L.dXp = take(Hp * D * es); L.dL = take(Hp * D * es); L.dY = take(Hp * H * es); L.dX = take(Hp * D * es);
+  L.dZ2 = take(Hp * H * es); L.dZ1 = take(Hp * H * es); L.dS = take(Hp * D * es);
+  L.W1t = take(D * H * es); L.W2t = take(H * H * es); L.W3t = take(H * D * es); L.W4t = take(D * H * es);
+  L.W5t = take(H * D * es);
+  if (dtype == NR_BF16) {
+    L.skP = take((int64_t)kSplit * (Hp - L.mm) * H * 4);
+    L.cs4 = take(L.csr * H * 4); L.cs3 = take(L.csr * D * 4); L.cs2 = take(L.csr * H * 4); L.cs1 = take(L.csr * H * 4);
+  } else {
+    // dL^T, Y^T, dY^T, X^T, dX^T, X2^T, dZ2^T, X1^T, dZ1^T, S^T
+    const int64_t w[10] = {D, H, H, D, D, H, H, H, H, D};
+    for (int i = 0; i < 10; ++i) L.T[i] = take(w[i] * Hp * es);
+  }
+  L.total = o;
+  return L;
+}
+
+static int ncu_of(hipStream_t st) {
+  int dev = 0, n = 256;
+  if (hipStreamGetDevice(st, &dev) != hipSuccess ||
+      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    n = 256;
+  return n >= 8 ? n / 8 * 8 : 8;
+}
+
+#define NR_FT(x)                  \
+  do {                            \
+    const int rc_ = (x);          \
+    if (rc_ != NR_OK) return rc_; \
+  } while (0)
+#define NR_FT_EV(x, what)                                         \
+  do {                                                            \
+    if ((x) != hipSuccess) {                                      \
+      set_error("nr_final_train_step: %s failed", what);          \
+      return NR_ERR_HIP;                                          \
+    }                                                             \
+  } while (0)
+
+template <typename TA>
+int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
+  constexpr bool BF = sizeof(TA) == 2;
+  const int dt = a.dtype;
+  const int ncu = ncu_of(st);
+  const Layout L = layout(dt, a.B, a.U, a.Hs, ncu);
+  const int64_t B = a.B, U = a.U, Hs = a.Hs, Hp = L.Hp, mm = L.mm;
+  auto P_ = [&](int64_t off) { return (void*)(ws + off); };
+  float* E = (float*)P_(L.E);
+  TA *S = (TA*)P_(L.S), *X1 = (TA*)P_(L.X1), *X2 = (TA*)P_(L.X2), *XP = (TA*)P_(L.XP), *Y = (TA*)P_(L.Y);
+  float* users = a.users ? a.users : (float*)P_(L.users);
+  float *z = (float*)P_(L.z), *du = (float*)P_(L.du), *dE = (float*)P_(L.dE);
+  TA *dXp = (TA*)P_(L.dXp), *dL = (TA*)P_(L.dL), *dY = (TA*)P_(L.dY), *dX = (TA*)P_(L.dX), *dZ2 = (TA*)P_(L.dZ2);
+  TA *dZ1 = (TA*)P_(L.dZ1), *dS = (TA*)P_(L.dS);
+  TA *W1t = (TA*)P_(L.W1t), *W2t = (TA*)P_(L.W2t), *W3t = (TA*)P_(L.W3t), *W4t = (TA*)P_(L.W4t),
+     *W5t = (TA*)P_(L.W5t);
+  const TA *W1 = (const TA*)a.W1, *W2 = (const TA*)a.W2, *W3 = (const TA*)a.W3, *W4 = (const TA*)a.W4,
+           *W5 = (const TA*)a.W5;
+  TA* X = XP;           // [Hp][D] at row stride 2D
+  TA* Pexp = XP + D;    // exp(logits), same stride
+  const float scale = 1.0f / (1.0f - a.p);
+  const double tq = (double)a.p * 4294967296.0;
+  const uint32_t thr = tq >= 4294967295.0 ? 0xffffffffu : (uint32_t)tq;
+  TrainSide side;
+  NR_FT(train_side_streams(st, "nr_final_train_step", side));
+
+  // ---- fork: the weight transposes the data-grad GEMMs need, beside the forward
+  NR_FT_EV(hipEventRecord(side.fork, st), "fork record");
+  NR_FT_EV(hipStreamWaitEvent(side.s, side.fork, 0), "fork wait");
+  {
+    const TA* w[5] = {W5, W4, W3, W2, W1};
+    TA* t[5] = {W5t, W4t, W3t, W2t, W1t};
+    const int64_t r[5] = {D, H, D, H, H}, c[5] = {H, D, H, H, D};  // W5 [D][H], W4 [H][D], W3 [D][H], W2, W1 [H][D]
+    for (int i = 0; i < 5; ++i) NR_FT(nr_transpose(dt, dt, r[i], c[i], w[i], c[i], t[i], r[i], side.s));
+  }
+  NR_FT_EV(hipEventRecord(side.wt, side.s), "transpose record");
+
+  // ---- accumulators: loss, dE (cosine + history scatter), the token LN grads
+  // (and, f32 mode, the bias grads that nr_col_sum accumulates)
+  {
+    ZList zl{};
+    float* zp[8] = {a.loss, dE, a.g_tok_g, a.g_tok_b, a.g_b1, a.g_b2, a.g_b3, a.g_b4};
+    const int64_t zn[8] = {1, U * D, D, D, H, H, D, H};
+    zl.n = BF ? 4 : 8;
+    for (int i = 0; i < zl.n; ++i) { zl.p[i] = zp[i]; zl.len[i] = zn[i]; }
+    hipLaunchKernelGGL(zero_kernel, dim3(512), dim3(256), 0, st, zl);
+    NR_CHECK_LAUNCH("nr_final_train_step (zero)");
+  }
+  // ---- forward
+  NR_FT(gather_ln_dispatch(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1, a.tok_g, a.tok_b, 1e-12f, E, D, st));
+  {
+    const int64_t g = (Hp + 3) / 4;
+    hipLaunchKernelGGL((gather_slots_kernel<TA>), dim3((unsigned)(g < 2048 ? g : 2048)), dim3(256), 0, st, Hp, Hs, E,
+                       a.hist_idx, S);
+    NR_CHECK_LAUNCH("nr_final_train_step (gather)");
+  }
+  // relu(dropout) GEMM over Hp rows: main rows on the persistent kernel, the tail as K-slices + fixup
+  auto relu_gemm = [&](const TA* A, int64_t lda, const TA* W, int64_t K, const float* bias, uint64_t seed, TA* C,
+                       int64_t ldc) -> int {
+    EpiArgs ea{seed, thr, scale};
+    NR_FT(gemm_dispatch_ex(dt, dt, NR_EPI_RELU_DROPOUT, mm, H, K, A, lda, W, K, bias, nullptr, 0, C, ldc, ea, st));
+    if (mm == Hp) return NR_OK;
+    float* Pk = (float*)P_(L.skP);
+    const int64_t kk = K / kSplit, rows = Hp - mm;
+    GemmProblem p = {rows, H, kk, A + mm * lda, lda, kk, W, K, kk, Pk, H, rows * H, kSplit, 1.0f};
+    NR_FT(gemm_group_dispatch(dt, NR_F32, &p, 1, st));
+    return nr_splitk_fixup(dt, NR_EPI_RELU_DROPOUT, rows, H, kSplit, Pk, bias, nullptr, 0, C + mm * ldc, ldc, mm,
+                           seed, a.p, scale, st);
+  };
+  NR_FT(relu_gemm(S, D, W1, D, a.b1, a.seed[0], X1, H));
+  NR_FT(relu_gemm(X1, H, W2, H, a.b2, a.seed[1], X2, H));
+  NR_FT(gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, H, X2, H, W3, H, a.b3, nullptr, 0, X, 2 * D, st));
+  NR_FT(relu_gemm(X, 2 * D, W4, D, a.b4, a.seed[2], Y, H));
+  NR_FT(gemm_dispatch(dt, dt, NR_EPI_EXP, Hp, D, H, Y, H, W5, H, nullptr, nullptr, 0, Pexp, 2 * D, st));
+  NR_FT(nr_final_pool_fwd(dt, B, a.hist_off, XP, 2 * D, users, z, st));
+  // ---- loss and its gradient into the pooled users and E[pos] / E[neg]
+  NR_FT(nr_cosine_margin(B, users, E, D, a.pos, a.neg, a.margin, nullptr, a.loss, du, dE, st));
+  NR_FT(nr_final_pool_bwd(dt, B, a.hist_off, Hp, XP, 2 * D, users, z, du, dXp, D, dL, D, st));
+  // ---- data-grad chain (weights transposed on the side stream)
+  NR_FT_EV(hipStreamWaitEvent(st, side.wt, 0), "transpose wait");
+  float *cs4 = (float*)P_(L.cs4), *cs3 = (float*)P_(L.cs3), *cs2 = (float*)P_(L.cs2), *cs1 = (float*)P_(L.cs1);
+  // drop'(A W^T) against the forward output Yf; bf16: column sums into cs
+  auto drelu_gemm = [&](const TA* A, int64_t K, const TA* Wt, const TA* Yf, TA* C, float* cs, float* gbias) -> int {
+    if constexpr (!BF) {
+      NR_FT(gemm_dispatch_ex(dt, dt, NR_EPI_DRELU, Hp, H, K, A, K, Wt, K, nullptr, Yf, H, C, H,
+                             EpiArgs{0, 0, scale}, st));
+      return nr_col_sum(dt, Hp, H, C, H, gbias, st);
+    } else {
+      EpiArgs ea{0, 0, scale};
+      ea.colsum = cs;
+      NR_FT(gemm_dispatch_ex(dt, dt, NR_EPI_DRELU, mm, H, K, A, K, Wt, K, nullptr, Yf, H, C, H, ea, st));
+      if (mm == Hp) return NR_OK;
+      float* Pk = (float*)P_(L.skP);
+      const int64_t kk = K / kSplit, rows = Hp - mm;
+      GemmProblem p = {rows, H, kk, A + mm * K, K, kk, Wt, K, kk, Pk, H, rows * H, kSplit, 1.0f};
+      NR_FT(gemm_group_dispatch(dt, NR_F32, &p, 1, st));
+      NR_FT(nr_splitk_fixup(dt, NR_EPI_DRELU, rows, H, kSplit, Pk, nullptr, Yf + mm * H, H, C + mm * H, H, mm, 0,
+                            0.f, scale, st));
+      // the tail rows' column sums (of the stored bf16 values) into the CS layout
+      hipLaunchKernelGGL((colsum_block_kernel<TA>), dim3((unsigned)(H / 256), (unsigned)((rows + 127) / 128)),
+                         dim3(256), 0, st, mm, Hp, H, C, H, cs);
+      NR_CHECK_LAUNCH("nr_final_train_step (tail column sums)");
+      return NR_OK;
+    }
+  };
+  NR_FT(drelu_gemm(dL, D, W5t, Y, dY, cs4, a.g_b4));  // dY = drop'(dL W5): the grad of linear4's output
+  {
+    EpiArgs ea{0, 0, 1.f};
+    if constexpr (BF) ea.colsum = cs3;
+    NR_FT(gemm_dispatch_ex(dt, dt, NR_EPI_RESADD, Hp, D, H, dY, H, W4t, H, nullptr, dXp, D, dX, D, ea, st));
+    if constexpr (!BF) NR_FT(nr_col_sum(dt, Hp, D, dX, D, a.g_b3, st));
+  }
+  NR_FT(drelu_gemm(dX, D, W3t, X2, dZ2, cs2, a.g_b2));
+  NR_FT(drelu_gemm(dZ2, H, W2t, X1, dZ1, cs1, a.g_b1));
+  NR_FT(gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, H, dZ1, H, W1t, H, nullptr, nullptr, 0, dS, D, st));
+  // ---- weight grads: dW = dOut^T X
+  if constexpr (BF) {
+    GemmProblem p[5] = {
+        {D, H, Hp, dL, D, 0, Y, H, 0, a.g_W5, H, 0, 1, 1.0f},
+        {H, D, Hp, dY, H, 0, X, 2 * D, 0, a.g_W4, D, 0, 1, 1.0f},
+        {D, H, Hp, dX, D, 0, X2, H, 0, a.g_W3, H, 0, 1, 1.0f},
+        {H, H, Hp, dZ2, H, 0, X1, H, 0, a.g_W2, H, 0, 1, 1.0f},
+        {H, D, Hp, dZ1, H, 0, S, D, 0, a.g_W1, D, 0, 1, 1.0f},
+    };
+    NR_FT(gemm_group_tn_dispatch(NR_F32, p, 5, st));
+    RSum r{};
+    float* parts[4] = {cs1, cs2, cs3, cs4};
+    float* outs[4] = {a.g_b1, a.g_b2, a.g_b3, a.g_b4};
+    const int64_t cols[4] = {H, H, D, H};
+    r.n = 4;
+    for (int i = 0; i < 4; ++i) { r.part[i] = parts[i]; r.out[i] = outs[i]; r.rows[i] = L.csr; r.cols[i] = cols[i]; }
+    hipLaunchKernelGGL(rowsum_kernel, dim3((unsigned)((3 * H + D) / 256)), dim3(256), 0, st, r);
+    NR_CHECK_LAUNCH("nr_final_train_step (bias grads)");
+  } else {
+    TA* T[10];
+    for (int i = 0; i < 10; ++i) T[i] = (TA*)P_(L.T[i]);
+    const TA* src[10] = {dL, Y, dY, X, dX, X2, dZ2, X1, dZ1, S};
+    const int64_t cols[10] = {D, H, H, D, D, H, H, H, H, D}, ld[10] = {D, H, H, 2 * D, D, H, H, H, H, D};
+    for (int i = 0; i < 10; ++i) NR_FT(nr_transpose(dt, dt, Hp, cols[i], src[i], ld[i], T[i], Hp, st));
+    GemmProblem p[5] = {
+        {D, H, Hp, T[0], Hp, 0, T[1], Hp, 0, a.g_W5, H, 0, 1, 1.0f},
+        {H, D, Hp, T[2], Hp, 0, T[3], Hp, 0, a.g_W4, D, 0, 1, 1.0f},
+        {D, H, Hp, T[4], Hp, 0, T[5], Hp, 0, a.g_W3, H, 0, 1, 1.0f},
+        {H, H, Hp, T[6], Hp, 0, T[7], Hp, 0, a.g_W2, H, 0, 1, 1.0f},
+        {H, D, Hp, T[8], Hp, 0, T[9], Hp, 0, a.g_W1, D, 0, 1, 1.0f},
+    };
+    NR_FT(gemm_group_dispatch(dt, NR_F32, p, 5, st));
+  }
+  // ---- history gather -> unique news rows -> token LayerNorm parameter grads
+  NR_FT(nr_scatter_add_rows(dt, Hs, D, dS, D, a.hist_idx, dE, D, st));
+  NR_FT(nr_ln_param_grad(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1e-12f, dE, D, a.g_tok_g, a.g_tok_b, st));
+  return NR_OK;
+}
+#undef NR_FT
+#undef NR_FT_EV
+
+}  // namespace ft
+}  // namespace nr
+
+// (the split-K tail, and so the workspace, depends on the device's CU count:
+// sized for the CURRENT device here, checked against the stream's device by the step)
+extern "C" int64_t nr_final_train_workspace_bytes(int dtype, int64_t B, int64_t U, int64_t Hs) {
+  if ((dtype != NR_F32 && dtype != NR_BF16) || B < 0 || U < 0 || Hs < 0) return -1;
+  int dev = 0, n = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    n = 256;
+  return nr::ft::layout(dtype, B, U, Hs, n >= 8 ? n / 8 * 8 : 8).total;
+}
+
+extern "C" int nr_final_train_step(const nr_final_train_args* args, void* ws, int64_t ws_bytes, void* stream) {
+  nr::clear_error();
+  NR_CHECK_ARG(args, "nr_final_train_step: null args");
+  const nr_final_train_args& a = *args;
+  NR_CHECK_ARG(a.dtype == NR_F32 || a.dtype == NR_BF16, "nr_final_train_step: dtype must be NR_F32 or NR_BF16");
+  NR_CHECK_ARG(a.tok_dtype == NR_F32 || a.tok_dtype == NR_BF16 || a.tok_dtype == NR_F16,
+               "nr_final_train_step: bad tok_dtype");
+  NR_CHECK_ARG(a.B >= 1 && a.U >= 1 && a.Hs >= 1, "nr_final_train_step: empty batch (B=%lld U=%lld Hs=%lld)",
+               (long long)a.B, (long long)a.U, (long long)a.Hs);
+  NR_CHECK_ARG(a.Hs <= (1ll << 31) - 1024 && a.U <= (1ll << 31) && a.B <= (1ll << 24),
+               "nr_final_train_step: batch too large");
+  NR_CHECK_ARG(a.p >= 0.f && a.p < 1.f, "nr_final_train_step: dropout p outside [0, 1)");
+  NR_CHECK_DEVICE("nr_final_train_step", a.tok_last, a.hist_idx, a.hist_off, a.pos, a.neg, a.tok_g, a.tok_b, a.W1,
+                  a.b1, a.W2, a.b2, a.W3, a.b3, a.W4, a.b4, a.W5);
+  NR_CHECK_DEVICE("nr_final_train_step", a.g_tok_g, a.g_tok_b, a.g_W1, a.g_b1, a.g_W2, a.g_b2, a.g_W3, a.g_b3, a.g_W4,
+                  a.g_b4, a.g_W5, a.loss, a.users, ws);
+  NR_CHECK_ARG(a.tok_last && a.hist_idx && a.hist_off && a.pos && a.neg && a.loss && ws && a.W1 && a.W2 && a.W3 &&
+                   a.W4 && a.W5 && a.g_W1 && a.g_W2 && a.g_W3 && a.g_W4 && a.g_W5 && a.g_b1 && a.g_b2 && a.g_b3 &&
+                   a.g_b4 && a.g_tok_g && a.g_tok_b,
+               "nr_final_train_step: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t need = nr::ft::layout(a.dtype, a.B, a.U, a.Hs, nr::ft::ncu_of(s)).total;
+  NR_CHECK_ARG(ws_bytes >= need, "nr_final_train_step: workspace too small (%lld < %lld)", (long long)ws_bytes,
+               (long long)need);
+  NR_CHECK_ARG(((uintptr_t)ws & 255) == 0, "nr_final_train_step: workspace must be 256-byte aligned");
+  return a.dtype == NR_F32 ? nr::ft::step<float>(a, (char*)ws, s) : nr::ft::step<__bf16>(a, (char*)ws, s);
+}

@@ -58,15 +58,7 @@ __device__ __forceinline__ float epi_exp(float x) { return __expf(x); }
 
 // gelu_erf2x2 (the persistent bf16 kernel's GELU / GEGLU epilogues): nr_common.h.
 
-// Extra epilogue arguments (dropout of the training forward; unused otherwise).
-struct EpiArgs {
-  uint64_t seed;  // dropout stream
-  uint32_t thr;   // drop iff drop_hash(seed, row * N + col) < thr  (thr = p * 2^32)
-  float scale;    // 1 / (1 - p)
-  int group_m = 1;  // 256x256 tile order: >1 groups group_m M-tiles (see tile_of)
-  const float* ln_stats = nullptr;  // LNF epilogue: [M] (mean, rstd) pairs
-  const float* ln_uc = nullptr;     // LNF epilogue: u [N] then c [N]
-};
+// EpiArgs (dropout / LN-fold / column-sum arguments of the epilogues): nr_common.h.
 
 template <typename TO>
 __device__ __forceinline__ TO to_out(float v) {
@@ -467,16 +459,36 @@ __device__ __forceinline__ void tile_of(int wg, int nx, int ny, int gm, int& mt,
   nt = loc / gsz;
 }
 
-template <typename TI, int EPI, typename TO, bool MF16>
+// TN = true (bf16, 16x16x32 only): both operands are stored with the reduction
+// index as the ROW, A as [K][M] and W as [K][N] (lda / ldw = their row strides):
+// C[m][n] = sum_k A[k][m] W[k][n], i.e. the weight-grad GEMM dW = dOut^T X of a
+// training step read straight from the row-major activations dOut [slots][out]
+// and X [slots][in], with no transposed copies.  A stage's operand image is
+// then two halves (h = tile columns 128 h .. +127) of 64 K-rows x 256 B; the
+// 16-B chunk at position P of K-row r holds the row's global chunk
+// P ^ (hsw(r) << 1), hsw(r) = (r & 3) | ((r >> 3) & 1) << 2 (applied on the
+// DMA source: the DMA writes LDS lane-linearly).  Fragments are read with
+// ds_read_b64_tr_b16 (cdna_hip_programming.md T10): lane 4q + p of 16-lane
+// group g addresses K-row 8g + 4e + q, columns 4p .. 4p + 3 of its 16-column
+// tile and receives its own column's 4 K values, two reads (e = 0, 1) forming
+// the 8-deep operand of one 16x16x32 MFMA.  The 8 K-rows a 32-lane half reads
+// have distinct hsw, so their 32-B pieces fall in 8 distinct 32-B bank groups
+// of the 256-B row: conflict-free.  Host: M % 256 = N % 256 = K % 64 = 0.
+__device__ __forceinline__ int tn_hsw(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+template <typename TI, int EPI, typename TO, bool MF16, bool TN = false>
 __device__ __forceinline__ void gemm256p_body(unsigned char* smem, int64_t m0, int64_t n0, int64_t M, int64_t N,
                                               int64_t K, const TI* __restrict__ A, int64_t lda,
                                               const TI* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
                                               const TO* R, int64_t ldr, TO* C, int64_t ldc, const EpiArgs& ea) {
+  static_assert(!TN || (MF16 && sizeof(TI) == 2), "TN operands: bf16 16x16x32 only");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
 
   constexpr int BK = 128 / (int)sizeof(TI), CE = 16 / (int)sizeof(TI);
   // half-tile DMA sources: wave covers rows 128h + 16 wave + 8 j + lane / 8
+  // (TN: K-rows 4 (2 wave + j) + lane / 16 of column half h, 16-B position lane & 15)
   const TI* asrc[2][2];
   const TI* bsrc[2][2];
   int hoff[2][2];
@@ -484,24 +496,33 @@ __device__ __forceinline__ void gemm256p_body(unsigned char* smem, int64_t m0, i
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int r0 = 128 * h + (wave * 2 + j) * 8;
-      const int row = r0 + (lane >> 3);
-      const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-      asrc[h][j] = A + min(m0 + row, M - 1) * lda + chunk * CE;
-      bsrc[h][j] = W + (n0 + row) * ldw + chunk * CE;
-      hoff[h][j] = r0 * 128;
+      if constexpr (TN) {
+        const int r = 4 * (wave * 2 + j) + (lane >> 4);
+        const int c = (lane & 15) ^ (tn_hsw(r) << 1);
+        asrc[h][j] = A + (int64_t)r * lda + m0 + 128 * h + c * CE;
+        bsrc[h][j] = W + (int64_t)r * ldw + n0 + 128 * h + c * CE;
+        hoff[h][j] = h * 16384 + (wave * 2 + j) * 1024;
+      } else {
+        const int r0 = 128 * h + (wave * 2 + j) * 8;
+        const int row = r0 + (lane >> 3);
+        const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+        asrc[h][j] = A + min(m0 + row, M - 1) * lda + chunk * CE;
+        bsrc[h][j] = W + (n0 + row) * ldw + chunk * CE;
+        hoff[h][j] = r0 * 128;
+      }
     }
+  const int64_t astep = TN ? BK * lda : BK, bstep = TN ? BK * ldw : BK;
   auto dmaA = [&](int h, int stage, int64_t kt) {
     unsigned char* sa = smem + stage * G2_STAGE;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_global_load_lds((g_void*)(asrc[h][j] + kt * BK), (lds_void*)(sa + hoff[h][j]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((g_void*)(asrc[h][j] + kt * astep), (lds_void*)(sa + hoff[h][j]), 16, 0, 0);
   };
   auto dmaB = [&](int h, int stage, int64_t kt) {
     unsigned char* sb = smem + stage * G2_STAGE + G2BM * 128;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_global_load_lds((g_void*)(bsrc[h][j] + kt * BK), (lds_void*)(sb + hoff[h][j]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((g_void*)(bsrc[h][j] + kt * bstep), (lds_void*)(sb + hoff[h][j]), 16, 0, 0);
   };
 
   typename Acc256<MF16>::type acc;
@@ -552,21 +573,43 @@ __device__ __forceinline__ void gemm256p_body(unsigned char* smem, int64_t m0, i
   constexpr int QB = MF16 ? 2 : 1;   // B tiles per 32-column quadrant
   constexpr int NF = MF16 ? 2 : 4;   // fragments (k-steps or groups) per tile per K tile
   frag_t fa[QA][NF], fb0[QB][NF], fb1[QB][NF];
+  // TN: per-tile lane offsets of the transposed reads (K-half f adds 8192, e = 1 adds 1024)
+  int taoff[TA], tboff[TB];
+  if constexpr (TN) {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, hsw = q | ((g & 1) << 2);
+    const int lrow = (8 * g + q) * 256 + 16 * (p >> 1) + 8 * (p & 1);
+#pragma unroll
+    for (int mi = 0; mi < TA; ++mi) taoff[mi] = wm * 16384 + lrow + 32 * (mi ^ hsw);
+#pragma unroll
+    for (int ni = 0; ni < TB; ++ni) {
+      const int nrel = wn * 64 + 16 * ni;
+      tboff[ni] = G2BM * 128 + (nrel >> 7) * 16384 + lrow + 32 * (((nrel & 127) >> 4) ^ hsw);
+    }
+  }
+  auto tr_frag = [&](const unsigned char* b) {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(b));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(b + 1024));
+    return __builtin_bit_cast(frag_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
   auto readA = [&](int stage, int qm) {
     const unsigned char* s = smem + stage * G2_STAGE;
 #pragma unroll
     for (int i = 0; i < QA; ++i)
 #pragma unroll
-      for (int f = 0; f < NF; ++f)
-        fa[i][f] = *reinterpret_cast<const frag_t*>(s + aoff[QA * qm + i] + ((chunk_of(f) ^ asw[QA * qm + i]) << 4));
+      for (int f = 0; f < NF; ++f) {
+        if constexpr (TN) fa[i][f] = tr_frag(s + taoff[QA * qm + i] + f * 8192);
+        else fa[i][f] = *reinterpret_cast<const frag_t*>(s + aoff[QA * qm + i] + ((chunk_of(f) ^ asw[QA * qm + i]) << 4));
+      }
   };
   auto readB = [&](int stage, int qn, frag_t (&fb)[QB][NF]) {
     const unsigned char* s = smem + stage * G2_STAGE;
 #pragma unroll
     for (int j = 0; j < QB; ++j)
 #pragma unroll
-      for (int f = 0; f < NF; ++f)
-        fb[j][f] = *reinterpret_cast<const frag_t*>(s + boff[QB * qn + j] + ((chunk_of(f) ^ bsw[QB * qn + j]) << 4));
+      for (int f = 0; f < NF; ++f) {
+        if constexpr (TN) fb[j][f] = tr_frag(s + tboff[QB * qn + j] + f * 8192);
+        else fb[j][f] = *reinterpret_cast<const frag_t*>(s + boff[QB * qn + j] + ((chunk_of(f) ^ bsw[QB * qn + j]) << 4));
+      }
   };
   auto mma = [&](int qm, int qn, const frag_t (&fb)[QB][NF]) {
 #pragma unroll
@@ -691,7 +734,7 @@ struct GemmGroup {
   int64_t sA[kGroupMax], sW[kGroupMax], sC[kGroupMax];
 };
 
-template <typename TI, typename TO, bool MF16>
+template <typename TI, typename TO, bool MF16, bool TN = false>
 __global__ __launch_bounds__(512, 2) void gemm256p_group_kernel(GemmGroup g) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * G2_STAGE];
   const int t = xcd_remap((int)blockIdx.x, (int)gridDim.x);
@@ -700,10 +743,10 @@ __global__ __launch_bounds__(512, 2) void gemm256p_group_kernel(GemmGroup g) {
   const int local = t - (p ? g.tile_end[p - 1] : 0);
   const int b = local / g.tpb[p], lt = local - b * g.tpb[p];
   const int nx = g.ntn[p];
-  gemm256p_body<TI, NR_EPI_NONE, TO, MF16>(smem, (int64_t)(lt / nx) * G2BM, (int64_t)(lt % nx) * G2BN, g.M[p],
-                                           g.N[p], g.K[p], (const TI*)g.A[p] + b * g.sA[p], g.lda[p],
-                                           (const TI*)g.W[p] + b * g.sW[p], g.ldw[p], nullptr, nullptr, 0,
-                                           (TO*)g.C[p] + b * g.sC[p], g.ldc[p], EpiArgs{0, 0, g.alpha[p]});
+  gemm256p_body<TI, NR_EPI_NONE, TO, MF16, TN>(smem, (int64_t)(lt / nx) * G2BM, (int64_t)(lt % nx) * G2BN, g.M[p],
+                                               g.N[p], g.K[p], (const TI*)g.A[p] + b * g.sA[p], g.lda[p],
+                                               (const TI*)g.W[p] + b * g.sW[p], g.ldw[p], nullptr, nullptr, 0,
+                                               (TO*)g.C[p] + b * g.sC[p], g.ldc[p], EpiArgs{0, 0, g.alpha[p]});
 }
 
 int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, int n, hipStream_t s) {
@@ -750,6 +793,51 @@ int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, i
   else
     hipLaunchKernelGGL((gemm256p_group_kernel<__bf16, __bf16, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);
   NR_CHECK_LAUNCH("gemm_group");
+  return NR_OK;
+}
+
+// Grouped TN launch (gemm256p_body TN): problem i computes C = alpha A^T W with A
+// [K][M] (row stride lda), W [K][N] (ldw), bf16, C [M][N] f32 or bf16 -- the
+// weight-grad GEMMs dW = dOut^T X of the training steps on their row-major
+// activations.  Batches (sA / sW / sC) give split-K slices: A + b sA is K-rows
+// b kw.. of the same activation.  M, N multiples of 256, K of 64.
+int gemm_group_tn_dispatch(int dtype_out, const GemmProblem* probs, int n, hipStream_t s) {
+  NR_CHECK_ARG(dtype_out == NR_F32 || dtype_out == NR_BF16, "gemm_group_tn: bad dtype_out %d", dtype_out);
+  NR_CHECK_ARG(n >= 0 && n <= kGroupMax, "gemm_group_tn: n=%d outside [0, %d]", n, kGroupMax);
+  GemmGroup g{};
+  int64_t tiles = 0;
+  const int64_t vo = dtype_out == NR_F32 ? 4 : 8;
+  for (int i = 0; i < n; ++i) {
+    const GemmProblem& q = probs[i];
+    NR_CHECK_ARG(q.M > 0 && q.N > 0 && q.K >= 0 && q.M % G2BM == 0 && q.N % G2BN == 0 && q.K % 64 == 0 &&
+                     q.batch >= 0,
+                 "gemm_group_tn: problem %d bad shape M=%lld N=%lld K=%lld (need M, N %% 256, K %% 64)", i,
+                 (long long)q.M, (long long)q.N, (long long)q.K);
+    if (q.K == 0 || q.batch == 0) continue;
+    NR_CHECK_ARG(q.A && q.W && q.C, "gemm_group_tn: problem %d null operand", i);
+    NR_CHECK_ARG(q.lda >= q.M && q.ldw >= q.N && q.lda % 8 == 0 && q.ldw % 8 == 0 && q.ldc >= q.N &&
+                     q.ldc % vo == 0 && ((uintptr_t)q.A & 15) == 0 && ((uintptr_t)q.W & 15) == 0 &&
+                     ((uintptr_t)q.C & 15) == 0 && q.sA % 8 == 0 && q.sW % 8 == 0 && q.sC % vo == 0,
+                 "gemm_group_tn: problem %d operands must be 16-byte aligned with 16-byte row / batch strides", i);
+    const int j = g.n++;
+    g.M[j] = q.M; g.N[j] = q.N; g.K[j] = q.K;
+    g.A[j] = q.A; g.W[j] = q.W; g.C[j] = q.C;
+    g.lda[j] = q.lda; g.ldw[j] = q.ldw; g.ldc[j] = q.ldc;
+    g.sA[j] = q.sA; g.sW[j] = q.sW; g.sC[j] = q.sC;
+    g.alpha[j] = q.alpha;
+    g.ntn[j] = (int)(q.N / G2BN);
+    const int64_t tpb = (q.M / G2BM) * g.ntn[j];
+    g.tpb[j] = (int)tpb;
+    tiles += tpb * q.batch;
+    NR_CHECK_ARG(tiles <= 0x7fffffff, "gemm_group_tn: too many tiles");
+    g.tile_end[j] = (int)tiles;
+  }
+  if (g.n == 0) return NR_OK;
+  if (dtype_out == NR_F32)
+    hipLaunchKernelGGL((gemm256p_group_kernel<__bf16, float, true, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm256p_group_kernel<__bf16, __bf16, true, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);
+  NR_CHECK_LAUNCH("gemm_group_tn");
   return NR_OK;
 }
 
@@ -812,7 +900,11 @@ constexpr unsigned kVmcnt0 = 0x0F70, kVmcnt4 = 0x0F74, kVmcnt8 = 0x0F78, kVmcnt6
 // its first K step while tile t's epilogue still reads slot t.
 constexpr int kLnSlot = 8 * 512 + 256 * 8;
 
-template <int EPI, bool LNF = false>
+// CS (column sums, the training steps' bias gradients): every wave also writes
+// the f32 column sums of its 128 output rows (the epilogue values before the
+// bf16 rounding, rows past M excluded) to ea.colsum row (m0 + 128 wm) / 128,
+// so db = the sum of those ceil(M / 128) rows, with no re-read of the output.
+template <int EPI, bool LNF = false, bool CS = false>
 __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, int64_t K,
                                                           const __bf16* __restrict__ A, int64_t lda,
                                                           const __bf16* __restrict__ W, int64_t ldw,
@@ -1151,9 +1243,15 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
       for (int p = 0; p < 2; ++p) rq[mi & 3][p] = *reinterpret_cast<const uint4*>(R + row * ldr + col0 + 32 * p + qo);
       __builtin_amdgcn_sched_barrier(0);  // issue order = use order: counted waits, not vmcnt(0)
     };
-    if constexpr (EPI == NR_EPI_RESADD || EPI == NR_EPI_SOFTMAX64_BWD) {
+    constexpr bool kRes = EPI == NR_EPI_RESADD || EPI == NR_EPI_SOFTMAX64_BWD || EPI == NR_EPI_DRELU;
+    if constexpr (kRes) {
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) load_r(mi);
+    }
+    f32x4 cs[4];  // CS: this lane's column partial sums (columns 16 ni + 4 q4 .. +3)
+    if constexpr (CS) {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) cs[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
@@ -1199,6 +1297,23 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
               for (int r = 0; r < 4; ++r) {
                 const uint32_t u = w[h][r >> 1];
                 acc[mi][2 * p + h][r] += (r & 1) ? bf16_hi(u) : bf16_lo(u);
+              }
+          }
+        }
+        if constexpr (EPI == NR_EPI_DRELU) {
+          // relu / dropout backward: dZ = dY * (y > 0 ? 1 / (1 - p) : 0), y = the
+          // forward output (R) in the accumulator layout by the same swap
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const uint4 s = swap_pair16(uint2{rq[mi & 3][p].x, rq[mi & 3][p].y}, uint2{rq[mi & 3][p].z, rq[mi & 3][p].w});
+            const uint32_t w[2][2] = {{s.x, s.y}, {s.z, s.w}};
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const uint32_t u = w[h][r >> 1];
+                const float y = (r & 1) ? bf16_hi(u) : bf16_lo(u);
+                acc[mi][2 * p + h][r] = y > 0.f ? acc[mi][2 * p + h][r] * ea.scale : 0.f;
               }
           }
         }
@@ -1280,6 +1395,12 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[ni][r] *= inv;
         }
+        if constexpr (CS) {
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cs[ni][r] += live ? v[ni][r] : 0.f;
+        }
         uint2 pk[4];
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
@@ -1294,10 +1415,29 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           *reinterpret_cast<uint4*>(dst) = s0;
           *reinterpret_cast<uint4*>(dst + 32) = s1;
         }
-        if constexpr (EPI == NR_EPI_RESADD || EPI == NR_EPI_SOFTMAX64_BWD) {
+        if constexpr (kRes) {
           __builtin_amdgcn_sched_barrier(0);  // row groups in load order
           if (mi + 4 < 8) load_r(mi + 4);
         }
+      }
+    }
+    if constexpr (CS) {
+      // sum over the 16 row lanes (c16) of each column; lane c16 < 4 stores columns 16 c16 + 4 q4 .. +3
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = cs[ni][r];
+          x += __shfl_xor(x, 1, 64);
+          x += __shfl_xor(x, 2, 64);
+          x += __shfl_xor(x, 4, 64);
+          x += __shfl_xor(x, 8, 64);
+          cs[ni][r] = x;
+        }
+      if (c16 < 4) {
+        const f32x4 o = c16 == 0 ? cs[0] : c16 == 1 ? cs[1] : c16 == 2 ? cs[2] : cs[3];
+        const int64_t prow = ((int64_t)m0 + wm * 128) >> 7;
+        *reinterpret_cast<f32x4*>(ea.colsum + prow * N + col0 + 16 * c16 + 4 * q4) = o;
       }
     }
     }
@@ -1392,7 +1532,20 @@ static int launch_gemm256_t(int epi, int64_t M, int64_t N, int64_t K, const void
   const __bf16* r = (const __bf16*)R;
   __bf16* c = (__bf16*)C;
 #define NR_T(E) hipLaunchKernelGGL((gemm256t_kernel<E>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea, ntn, (int)ntm, nt, nh)
+#define NR_TC(E) hipLaunchKernelGGL((gemm256t_kernel<E, false, true>), grid, dim3(512), 0, s, M, N, K, a, lda, w, ldw, bias, r, ldr, c, ldc, ea, ntn, (int)ntm, nt, nh)
+  if (ea.colsum) {
+    switch (epi) {
+      case NR_EPI_NONE: NR_TC(NR_EPI_NONE); break;
+      case NR_EPI_RESADD: NR_TC(NR_EPI_RESADD); break;
+      case NR_EPI_DRELU: NR_TC(NR_EPI_DRELU); break;
+      default: set_error("nr_gemm: column sums with epilogue %d unsupported", epi); return NR_ERR_INVALID;
+    }
+    NR_CHECK_LAUNCH("nr_gemm");
+    return NR_OK;
+  }
+#undef NR_TC
   switch (epi) {
+    case NR_EPI_DRELU: NR_T(NR_EPI_DRELU); break;
     case NR_EPI_NONE: NR_T(NR_EPI_NONE); break;
     case NR_EPI_RELU: NR_T(NR_EPI_RELU); break;
     case NR_EPI_EXP: NR_T(NR_EPI_EXP); break;
@@ -1470,10 +1623,15 @@ static int launch_gemm256(int epi, int64_t M, int64_t N, int64_t K, const void* 
                           void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s) {
   EpiArgs eg = ea;
   eg.group_m = kGemmGroupM;
-  // persistent kernel for bf16 -> bf16 (DRELU, a training-only epilogue that needs its
-  // forward output at the END of the tile, stays on the one-tile-per-workgroup kernel)
+  if (ea.colsum && !(sizeof(TI) == 2 && sizeof(TO) == 2 && persistent_ok(M, N, K, lda, ldw) &&
+                     (epi != NR_EPI_DRELU || (((uintptr_t)R & 15) == 0 && ldr % 8 == 0)))) {
+    set_error("nr_gemm: column sums need the persistent bf16 kernel (bf16 in/out, K %% 128, 16-byte rows)");
+    return NR_ERR_UNSUPPORTED;
+  }
+  // persistent kernel for bf16 -> bf16 (DRELU reads its forward output in the
+  // epilogue's residual window, like RESADD)
   if constexpr (sizeof(TI) == 2 && sizeof(TO) == 2) {
-    if (epi != NR_EPI_DRELU && persistent_ok(M, N, K, lda, ldw))
+    if (persistent_ok(M, N, K, lda, ldw) && (epi != NR_EPI_DRELU || (((uintptr_t)R & 15) == 0 && ldr % 8 == 0)))
       return launch_gemm256_t(epi, M, N, K, A, lda, W, ldw, bias, R, ldr, C, ldc, eg, s);
     // A past the 32-bit buffer range (e.g. the title encoder's FFN2, [M x 4096]
     // at M > 512 k tokens): persistent launches over row chunks of < 4 GiB of A.
@@ -1651,6 +1809,21 @@ extern "C" int nr_gemm(int dtype_in, int dtype_out, int epilogue, int64_t M, int
   if (M > 0) NR_CHECK_DEVICE("nr_gemm", A, W, bias, R, C);
   return nr::gemm_dispatch(dtype_in, dtype_out, epilogue, M, N, K, A, lda, W, ldw, bias, R, ldr, C,
                            ldc, (hipStream_t)stream);
+}
+
+extern "C" int nr_gemm_grouped_tn(int dtype_out, int n, const int64_t* M, const int64_t* N, const int64_t* K,
+                                  const void* const* A, const int64_t* lda, const void* const* W, const int64_t* ldw,
+                                  void* const* C, const int64_t* ldc, const float* alpha, void* stream) {
+  nr::clear_error();
+  NR_CHECK_ARG(n >= 1 && n <= NR_GEMM_MAX_GROUP, "nr_gemm_grouped_tn: n=%d outside [1, %d]", n, NR_GEMM_MAX_GROUP);
+  NR_CHECK_ARG(M && N && K && A && lda && W && ldw && C && ldc, "nr_gemm_grouped_tn: null array");
+  nr::GemmProblem p[NR_GEMM_MAX_GROUP];
+  for (int i = 0; i < n; ++i) {
+    if (K[i] > 0) NR_CHECK_DEVICE("nr_gemm_grouped_tn", A[i], W[i], C[i]);
+    p[i] = nr::GemmProblem{M[i], N[i], K[i], A[i], lda[i], 0, W[i], ldw[i], 0, C[i], ldc[i], 0, 1,
+                           alpha ? alpha[i] : 1.0f};
+  }
+  return nr::gemm_group_tn_dispatch(dtype_out, p, n, (hipStream_t)stream);
 }
 
 extern "C" int nr_gemm_grouped(int dtype_in, int dtype_out, int n, const int64_t* M, const int64_t* N,

@@ -442,7 +442,7 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t n_rows, const TA
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             cdf[j] = 0.5f * (1.0f + erff(g[i][k + j] * 0.70710678118654752440f));
-            pdf[j] = 0.39894228040143267794f * __expf(-0.5f * g[i][k + j] * g[i][k + j]);
+            pdf[j] = 0.39894228040143267794f * expf(-0.5f * g[i][k + j] * g[i][k + j]);  // exact f32, as the forward
           }
         } else {
           f32x2v h, e;
@@ -941,38 +941,6 @@ static int grid_rows(int64_t rows, int cap = 1024) {
   return (int)(g < cap ? (g > 0 ? g : 1) : cap);
 }
 
-// The step's second stream (the weight-grad GEMM of W1 runs there beside the
-// data-grad chain) and its fork / join events: one set per host thread and
-// device, created on first use and kept (streams are reentrant per thread).
-struct Side {
-  hipStream_t s = nullptr, s2 = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr, fork2 = nullptr, join2 = nullptr, wt = nullptr;
-};
-static int side_stream(Side& out) {
-  thread_local Side t_side[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
-    set_error("nr_latent_train_step: no current HIP device");
-    return NR_ERR_HIP;
-  }
-  Side& sd = t_side[dev];
-  if (!sd.s) {
-    if (hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&sd.s2, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.fork2, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.join2, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&sd.wt, hipEventDisableTiming) != hipSuccess) {
-      set_error("nr_latent_train_step: cannot create the side stream / events");
-      sd = Side{};
-      return NR_ERR_HIP;
-    }
-  }
-  out = sd;
-  return NR_OK;
-}
-
 template <typename TA>
 int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   const int dt = a.dtype;
@@ -1008,9 +976,9 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   const TA *Wq = (const TA*)a.Wq, *Wkv = (const TA*)a.Wkv, *Wo = (const TA*)a.Wo, *W1 = (const TA*)a.W1,
            *W2 = (const TA*)a.W2;
   const float scale = 1.0f / sqrtf((float)DH);  // SDPA default scale (latent_attention.py:72)
-  Side side;
+  TrainSide side;
   int rc;
-  if ((rc = side_stream(side))) return rc;
+  if ((rc = train_side_streams(st, "nr_latent_train_step", side))) return rc;
 #define NR_LT_CHECK(name) NR_CHECK_LAUNCH("nr_latent_train_step (" name ")")
 
   // ---- fork 0: the weight transposes and the fold (weights only) run on the side
@@ -1257,6 +1225,41 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
 }
 
 }  // namespace lt
+
+// (nr_common.h) one set per host thread and device; the streams are created on
+// the device of `st`, so a step launched on another GPU's stream than the
+// current device forks and joins on that GPU.
+int train_side_streams(hipStream_t st, const char* fn, TrainSide& out) {
+  thread_local TrainSide t_side[64];
+  int dev = 0;
+  if (hipStreamGetDevice(st, &dev) != hipSuccess || dev < 0 || dev >= 64) {
+    set_error("%s: cannot resolve the stream's device", fn);
+    return NR_ERR_HIP;
+  }
+  TrainSide& sd = t_side[dev];
+  if (!sd.s) {
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || (cur != dev && hipSetDevice(dev) != hipSuccess)) {
+      set_error("%s: cannot select device %d", fn, dev);
+      return NR_ERR_HIP;
+    }
+    const bool ok = hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) == hipSuccess &&
+                    hipStreamCreateWithFlags(&sd.s2, hipStreamNonBlocking) == hipSuccess &&
+                    hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&sd.fork2, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&sd.join2, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&sd.wt, hipEventDisableTiming) == hipSuccess;
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!ok) {
+      set_error("%s: cannot create the side streams / events", fn);
+      sd = TrainSide{};
+      return NR_ERR_HIP;
+    }
+  }
+  out = sd;
+  return NR_OK;
+}
 }  // namespace nr
 
 extern "C" int64_t nr_latent_train_workspace_bytes(int dtype, int64_t B, int64_t U, int64_t Hs) {

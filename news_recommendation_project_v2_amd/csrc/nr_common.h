@@ -31,7 +31,18 @@ int check_device_ptrs(const char* fn, const char* names, std::initializer_list<c
 int gemm_dispatch(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, int64_t K,
                   const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
                   const void* R, int64_t ldr, void* C, int64_t ldc, hipStream_t s);
-struct EpiArgs;
+// Extra epilogue arguments of the GEMMs (gemm.hip): dropout of the training
+// forward, the LayerNorm fold, the persistent kernel's column sums.
+struct EpiArgs {
+  uint64_t seed;  // dropout stream
+  uint32_t thr;   // drop iff drop_hash(seed, row * N + col) < thr  (thr = p * 2^32)
+  float scale;    // 1 / (1 - p)
+  int group_m = 1;  // 256x256 tile order: >1 groups group_m M-tiles (see tile_of)
+  const float* ln_stats = nullptr;  // LNF epilogue: [M] (mean, rstd) pairs
+  const float* ln_uc = nullptr;     // LNF epilogue: u [N] then c [N]
+  float* colsum = nullptr;          // persistent kernel, CS: [ceil(M / 128)][N] f32 column sums of each 128-row block
+};
+
 int gemm_dispatch_ex(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, int64_t K,
                      const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
                      const void* R, int64_t ldr, void* C, int64_t ldc, const EpiArgs& ea, hipStream_t s);
@@ -50,6 +61,15 @@ int row_stats_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int6
 // NR_EPI_GEGLU): C = epi(rstd_m * (A W^T - mean_m u_n) + c_n); stats [M] (mean, rstd), uc [2][N]
 int gemm_lnfold_dispatch(int epi, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* W,
                          int64_t ldw, const float* stats, const float* uc, void* C, int64_t ldc, hipStream_t s);
+// The training steps' side streams (latent_train.hip): two non-blocking streams
+// and their fork / join events per host thread and device, created on first use
+// on the DEVICE OF `st` (not the caller's current device) and kept.
+struct TrainSide {
+  hipStream_t s = nullptr, s2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, fork2 = nullptr, join2 = nullptr, wt = nullptr;
+};
+int train_side_streams(hipStream_t st, const char* fn, TrainSide& out);
+
 // One problem of a grouped GEMM launch (gemm.hip gemm_group_dispatch): C = alpha A W^T,
 // no bias; `batch` instances at A + b sA, W + b sW, C + b sC (element strides).
 struct GemmProblem {
@@ -65,6 +85,8 @@ struct GemmProblem {
 };
 constexpr int kGroupMax = 16;
 int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, int n, hipStream_t s);
+// C = alpha A^T W per problem, A [K][M] and W [K][N] bf16 row-major (gemm.hip, TN grouped launch)
+int gemm_group_tn_dispatch(int dtype_out, const GemmProblem* probs, int n, hipStream_t s);
 int inv_norm_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps,
                       float* out, hipStream_t s);
 

@@ -470,6 +470,33 @@ def gemm_grouped(problems) -> None:
               ldw, C, ldc, _stream(dev))
 
 
+def gemm_grouped_tn(problems, alpha=None) -> None:
+    """out_i = alpha_i * a_i.T @ w_i for up to 8 (a, w, out) triples in ONE launch
+    (nr_gemm_grouped_tn): a_i [K, M], w_i [K, N] bf16 row-major (the weight grads
+    dOut^T X straight from the activations), out_i [M, N] f32 or bf16."""
+    problems = list(problems)
+    if not 1 <= len(problems) <= 8:
+        raise _lib.NewsRecHIPError("gemm_grouped_tn: 1..8 problems")
+    dev = _dev(*[t for pr in problems for t in pr])
+    n = len(problems)
+    L = ctypes.c_int64 * n
+    P = ctypes.c_void_p * n
+    M, N, K, lda, ldw, ldc = L(), L(), L(), L(), L(), L()
+    A, W, C = P(), P(), P()
+    al = (ctypes.c_float * n)(*([1.0] * n if alpha is None else alpha))
+    for i, (a, w, out) in enumerate(problems):
+        if a.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or a.shape[0] != w.shape[0] \
+                or tuple(out.shape) != (a.shape[1], w.shape[1]):
+            raise _lib.NewsRecHIPError(f"gemm_grouped_tn: problem {i} shape/dtype mismatch")
+        if out.dtype != problems[0][2].dtype:
+            raise _lib.NewsRecHIPError("gemm_grouped_tn: all outputs must share a dtype")
+        K[i], M[i], N[i] = a.shape[0], a.shape[1], w.shape[1]
+        lda[i], ldw[i], ldc[i] = _rowmajor(a, "a"), _rowmajor(w, "w"), _rowmajor(out, "out")
+        A[i], W[i], C[i] = a.data_ptr(), w.data_ptr(), out.data_ptr()
+    _lib.call("nr_gemm_grouped_tn", _dtype(problems[0][2], "out"), n, M, N, K, A, lda, W, ldw, C, ldc, al,
+              _stream(dev))
+
+
 def gemm_relu_dropout(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], seed: int, p: float,
                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = relu(a @ w.T + bias) * keep / (1 - p), keep from the (seed, row, col) hash stream."""

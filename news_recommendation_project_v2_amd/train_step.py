@@ -10,19 +10,22 @@ Replaces the body of ``AttentionAttentionTrainer.train_one_epoch``
   loss       = MarginRankingLoss(2)(res[:B], res[B:], 1)
   loss.backward(); clip_grad_norm_(0.5); AdamW(lr 1e-6).step()
 
-as a fixed kernel sequence (no autograd):
-  * the token model is ``nr_gather_layernorm`` of the U unique news' last rows;
+as ONE library call per batch (``nr_final_train_step``, csrc/final_train.hip;
+no autograd, no torch kernels inside the step):
+  * the token model is the g_mlp LayerNorm of the U unique news' last rows;
   * FinalAttention runs once per VALID history slot (Hs = sum h_i rows packed in
     CSR order, zero-padded to a multiple of 64): the reference's padded slots
     are masked to zero weight, so they carry no gradient and skipping them is
     exact; dropout is fused into the ReLU GEMM epilogues with a counter-hash
-    stream (``nr_gemm_relu_dropout``), its backward into the data-grad GEMMs
-    (``nr_gemm_drelu``: the mask is recovered from the saved outputs);
-  * data-grad GEMMs use transposed weights, weight-grad GEMMs transposed
-    activations / grads, all on the C = A·Wᵀ MFMA kernel (bf16 or exact f32);
+    stream, its backward into the data-grad GEMMs (the mask is recovered from
+    the saved outputs);
+  * bf16: the data-grad GEMMs also write the bias gradients (f32 column sums)
+    from their epilogues, and the weight-grad GEMMs read the row-major
+    activations through transposed LDS reads (no transposed copies);
   * pooling forward / backward, cosine + margin loss, scatter-add of the
-    history gradient, bias and LayerNorm-parameter reductions, the global grad
-    norm and AdamW (with the clip coefficient folded in) are HIP kernels.
+    history gradient and the LayerNorm-parameter reductions are HIP kernels;
+    the global grad norm and AdamW (clip coefficient folded in) are two more
+    launches in ``optimizer_step``.
 
 Parameters live in ONE flat f32 buffer (master weights; the torch modules'
 parameters are re-pointed at views of it, so ``state_dict()`` is always
@@ -72,6 +75,17 @@ class TrainBatch:
     @property
     def B(self) -> int:
         return self.pos.numel()
+
+
+def _refresh_mirror(step) -> None:
+    """Rewrite a step's bf16 weight mirror when its master weights changed outside
+    AdamW (load_state_dict on the wrapped modules, an edit through ``views``): the
+    parameters are views of ``step.flat``, so such writes move its version
+    counter, while AdamW (a library call) does not."""
+    if step.flat16 is not None and step.flat._version != step._mirror_version:
+        with torch.no_grad():
+            step.flat16.copy_(step.flat)
+        step._mirror_version = step.flat._version
 
 
 class FinalAttentionTrainStep:
@@ -132,7 +146,12 @@ class FinalAttentionTrainStep:
         self.sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self._ws = {}
-        self._pending = []
+        self._ws_native = None
+        self._users = None
+        self._mirror_version = self.flat._version
+        self._pmap = {"tok_g": "ln.weight", "tok_b": "ln.bias", "W5": "linear5.weight",
+                      **{f"W{i}": f"linear{i}.weight" for i in range(1, 5)},
+                      **{f"b{i}": f"linear{i}.bias" for i in range(1, 5)}}
 
     # ------------------------------------------------------------------ helpers
     def _buf(self, name: str, shape, dtype) -> torch.Tensor:
@@ -143,6 +162,9 @@ class FinalAttentionTrainStep:
             self._ws[name] = t
         return t[:n].view(shape)
 
+    # _tail_rows / _relu_gemm: the Python driver of the split-K tail the native
+    # step runs (final_train.hip main_rows / relu_gemm), kept as its test double
+    # (tests/test_train.py test_gpu_split_k_tail_matches_full_gemm).
     def _tail_rows(self, M: int, N: int, K: int) -> int:
         """Rows of a bf16 GEMM that fill whole rounds of 256x256 tiles over the CUs
         (the rest, a few tiles that would hold one CU each for a full tile time,
@@ -193,85 +215,45 @@ class FinalAttentionTrainStep:
 
     # ------------------------------------------------------------------ step
     def forward_backward(self, batch: TrainBatch):
-        """Loss (device scalar) and gradients into ``self.grad`` (zeroed first).
-        Returns (loss, users, E) for inspection."""
-        dt, dev = self.dtype, self.device
-        U = batch.tok_last.shape[0]
-        B = batch.B
-        Hs = batch.hist_idx.numel()
-        Hp = _pad64(Hs)
-        scale = 1.0 / (1.0 - self.p)
-        self.grad.zero_()
-        self.loss.zero_()
-        # ---- forward
-        gam = self.views["ln.weight"].view(1, D)
-        bet = self.views["ln.bias"].view(1, D)
-        E = ops.gather_layernorm(batch.tok_last, None, gam, bet, self.ln_eps, out=self._buf("E", (U, D), torch.float32))
-        idx = self._buf("idx", (Hp,), torch.int32)
-        idx.fill_(-1)
-        idx[:Hs].copy_(batch.hist_idx)
-        S = ops.gather_rows(E, idx, out_dtype=dt, out=self._buf("S", (Hp, D), dt))
-        X1 = self._relu_gemm(S, self.W(1), self._buf("X1", (Hp, H), dt), bias=self.b(1), seed=self.layer_seed(1))
-        X2 = self._relu_gemm(X1, self.W(2), self._buf("X2", (Hp, H), dt), bias=self.b(2), seed=self.layer_seed(2))
-        XP = self._buf("XP", (Hp, 2 * D), dt)
-        X = XP[:, :D]
-        ops.gemm(X2, self.W(3), self.b(3), out=X)
-        Y = self._relu_gemm(X, self.W(4), self._buf("Y", (Hp, H), dt), bias=self.b(4), seed=self.layer_seed(3))
-        ops.gemm(Y, self.W(5), None, epilogue="exp", out=XP[:, D:])
-        users, z = ops.final_pool_fwd(XP, batch.hist_off)
-        # ---- loss + backward
-        du = self._buf("du", (B, D), torch.float32)
-        dE = self._buf("dE", (U, D), torch.float32)
-        dE.zero_()
-        ops.cosine_margin(users, E, batch.pos, batch.neg, MARGIN, self.loss, du, dE)
-        dXp = self._buf("dXp", (Hp, D), dt)
-        dL = self._buf("dL", (Hp, D), dt)
-        ops.final_pool_bwd(XP, batch.hist_off, users, z, du, dXp, dL)
-        T = lambda src, name: ops.transpose(src, out=self._buf(name, (src.shape[1], src.shape[0]), dt))
-        # linear5 (no bias): logits = Y W5ᵀ
-        W5t = T(self.W(5), "W5t")
-        dY = self._relu_gemm(dL, W5t, self._buf("dY", (Hp, H), dt), y=Y, scale=scale)     # = dZ4
-        self._wgrad(dL, Y, "linear5.weight")
-        # linear4: Y = dropout(relu(X W4ᵀ + b4))
-        W4t = T(self.W(4), "W4t")
-        dX = ops.gemm(dY, W4t, None, epilogue="resadd", residual=dXp, out=self._buf("dX", (Hp, D), dt))
-        self._wgrad(dY, X, "linear4.weight")
-        ops.col_sum(dY, self.gviews["linear4.bias"])
-        # linear3: X = X2 W3ᵀ + b3
-        W3t = T(self.W(3), "W3t")
-        dZ2 = self._relu_gemm(dX, W3t, self._buf("dZ2", (Hp, H), dt), y=X2, scale=scale)
-        self._wgrad(dX, X2, "linear3.weight")
-        ops.col_sum(dX, self.gviews["linear3.bias"])
-        # linear2
-        W2t = T(self.W(2), "W2t")
-        dZ1 = self._relu_gemm(dZ2, W2t, self._buf("dZ1", (Hp, H), dt), y=X1, scale=scale)
-        self._wgrad(dZ2, X1, "linear2.weight")
-        ops.col_sum(dZ2, self.gviews["linear2.bias"])
-        # linear1
-        W1t = T(self.W(1), "W1t")
-        dS = ops.gemm(dZ1, W1t, None, out=self._buf("dS", (Hp, D), dt))
-        self._wgrad(dZ1, S, "linear1.weight")
-        ops.col_sum(dZ1, self.gviews["linear1.bias"])
-        # history gather -> unique news rows -> token LayerNorm params
-        self._flush_wgrads()
-        ops.scatter_add_rows(dS[:Hs], batch.hist_idx, dE)
-        ops.ln_param_grad(batch.tok_last, None, self.ln_eps, dE, self.gviews["ln.weight"], self.gviews["ln.bias"])
-        return self.loss, users, E
+        """Loss (device scalar) and gradients into ``self.grad`` (every slice
+        rewritten) as ONE library call (``nr_final_train_step``, csrc/final_train.hip):
+        the forward, the margin loss and the whole backward of the batch.
+        Returns (loss, users, None): users = the pooled users [B, D] f32.  Both
+        returned tensors are views of buffers the next call overwrites in place
+        (on the stream); clone them to keep a step's values."""
+        from . import _lib
+        U, B, Hs = batch.tok_last.shape[0], batch.B, batch.hist_idx.numel()
+        lib = _lib.load()
+        self._refresh_mirror()
+        dt = _lib.NR_BF16 if self.dtype == torch.bfloat16 else _lib.NR_F32
+        with torch.cuda.device(self.device):
+            need = int(lib.nr_final_train_workspace_bytes(dt, B, U, Hs))
+        if self._ws_native is None or self._ws_native.numel() < need:
+            self._ws_native = torch.empty(need, dtype=torch.uint8, device=self.device)
+        if self._users is None or self._users.shape[0] < B:
+            self._users = torch.empty((B, D), dtype=torch.float32, device=self.device)
+        tok = batch.tok_last.contiguous()
+        tdt = {torch.float32: _lib.NR_F32, torch.bfloat16: _lib.NR_BF16, torch.float16: _lib.NR_F16}[tok.dtype]
+        hi, ho = batch.hist_idx.to(torch.int32).contiguous(), batch.hist_off.to(torch.int64).contiguous()
+        pos, neg = batch.pos.to(torch.int32).contiguous(), batch.neg.to(torch.int32).contiguous()
+        a = _lib.FinalTrainArgs()
+        a.dtype, a.tok_dtype, a.B, a.U, a.Hs, a.margin, a.p = dt, tdt, B, U, Hs, MARGIN, self.p
+        for i in range(3):
+            a.seed[i] = self.layer_seed(i + 1)
+        a.tok_last, a.hist_idx, a.hist_off, a.pos, a.neg = (tok.data_ptr(), hi.data_ptr(), ho.data_ptr(), pos.data_ptr(),
+                                                            neg.data_ptr())
+        for f, name in self._pmap.items():
+            src = self.cviews[name] if f.startswith("W") else self.views[name]
+            setattr(a, f, src.data_ptr())
+            setattr(a, "g_" + f, self.gviews[name].data_ptr())
+        a.loss, a.users = self.loss.data_ptr(), self._users.data_ptr()
+        _lib.check(lib.nr_final_train_step(ctypes.byref(a), self._ws_native.data_ptr(), self._ws_native.numel(),
+                                           torch.cuda.current_stream(self.device).cuda_stream), "nr_final_train_step")
+        self._keep = (tok, hi, ho, pos, neg)  # alive until the stream has run the step
+        return self.loss, self._users[:B], None
 
-    def _wgrad(self, dOut: torch.Tensor, Xin: torch.Tensor, name: str) -> None:
-        """grad[name] = dOutᵀ · Xin  ([N_out, Hp] x [Hp, K_in]).  bf16: the
-        transposed operands are kept per layer and the five GEMMs run as ONE
-        grouped launch in ``_flush_wgrads`` (four of them are 64 tiles each,
-        a quarter of the chip alone)."""
-        dt = self.dtype
-        dOt = ops.transpose(dOut, out=self._buf("wg_a_" + name, (dOut.shape[1], dOut.shape[0]), dt))
-        Xt = ops.transpose(Xin, out=self._buf("wg_b_" + name, (Xin.shape[1], Xin.shape[0]), dt))
-        self._pending.append((dOt, Xt, self.gviews[name]))
-
-    def _flush_wgrads(self) -> None:
-        if self._pending:
-            ops.gemm_grouped(self._pending)
-            self._pending = []
+    def _refresh_mirror(self) -> None:
+        _refresh_mirror(self)
 
     def optimizer_step(self) -> None:
         """clip_grad_norm_(max_norm) + AdamW, one launch each (trainer.py:1067-1069)."""
@@ -368,6 +350,7 @@ class LatentAttentionTrainStep:
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self._ws = None
         self._users = None
+        self._mirror_version = self.flat._version
         b = "latent.cross_attend_blocks."
         self._pmap = {"tok_g": "ln.weight", "tok_b": "ln.bias", "latents": "latent.latents",
                       "nq_g": b + "0.norm.weight", "nq_b": b + "0.norm.bias",
@@ -382,10 +365,12 @@ class LatentAttentionTrainStep:
     def forward_backward(self, batch: TrainBatch):
         """Loss (device scalar) and gradients into ``self.grad`` (every slice
         rewritten).  Returns (loss, users, None): users = the normalized pooled
-        users [B, D]."""
+        users [B, D].  Both are views of buffers the next call overwrites in
+        place (on the stream); clone them to keep a step's values."""
         from . import _lib
         U, B, Hs = batch.tok_last.shape[0], batch.B, batch.hist_idx.numel()
         lib = _lib.load()
+        _refresh_mirror(self)
         dt = _lib.NR_BF16 if self.dtype == torch.bfloat16 else _lib.NR_F32
         need = int(lib.nr_latent_train_workspace_bytes(dt, B, U, Hs))
         if self._ws is None or self._ws.numel() < need:

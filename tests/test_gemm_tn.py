@@ -1,0 +1,68 @@
+"""The TN grouped GEMM (nr_gemm_grouped_tn, gemm.hip gemm256p_body<TN>): the
+weight-grad GEMMs dW = dOut^T X of the config-5 steps read straight from the
+row-major activations with ds_read_b64_tr_b16 (no transposed copies).  Checked
+against float64 of the same bf16 operands (the bound is f32 accumulation of
+K products: relative 2e-5 of the row-norm product scale), and bit-identical to
+the NT grouped GEMM fed explicit transposes (same per-element MFMA chain)."""
+import pytest
+import torch
+
+from news_recommendation_project_v2_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(a, w, alpha=1.0):
+    return alpha * (a.double().T @ w.double())
+
+
+@pytest.mark.parametrize("K,M,N", [(64, 256, 256), (128, 512, 256), (8320, 1024, 4096), (8320, 4096, 4096),
+                                   (576, 256, 768)])
+def test_gemm_grouped_tn_vs_float64(gpu_device, K, M, N):
+    g = torch.Generator(device=gpu_device).manual_seed(K + M + N)
+    a = torch.randn((K, M), generator=g, device=gpu_device).bfloat16()
+    w = torch.randn((K, N), generator=g, device=gpu_device).bfloat16()
+    out = torch.full((M, N), float("nan"), device=gpu_device)
+    ops.gemm_grouped_tn([(a, w, out)], alpha=[0.5])
+    torch.cuda.synchronize()
+    ref = _ref(a, w, 0.5)
+    scale = 0.5 * (a.double().norm(dim=0)[:, None] * w.double().norm(dim=0)[None, :])
+    err = ((out.double() - ref).abs() / scale).max().item()
+    assert err < 2e-5, err
+
+
+def test_gemm_grouped_tn_equals_nt_on_transposes(gpu_device):
+    """Several problems in one launch (the five FinalAttention weight grads' shapes
+    at a small K), strided row views, bf16 and f32 outputs: equal bit for bit to
+    the NT kernel on explicit transposes."""
+    g = torch.Generator(device=gpu_device).manual_seed(3)
+    K = 320
+    shapes = [(1024, 4096), (4096, 4096), (4096, 1024), (1024, 1024), (4096, 1024)]
+    probs_tn, probs_nt, outs = [], [], []
+    for M, N in shapes:
+        big = torch.randn((K, M + 64), generator=g, device=gpu_device).bfloat16()
+        a = big[:, 64:]  # row stride M + 64, 16-B aligned
+        w = torch.randn((K, N), generator=g, device=gpu_device).bfloat16()
+        o1 = torch.empty((M, N), device=gpu_device)
+        o2 = torch.empty((M, N), device=gpu_device)
+        probs_tn.append((a, w, o1))
+        probs_nt.append((a.T.contiguous(), w.T.contiguous(), o2))
+        outs.append((o1, o2))
+    ops.gemm_grouped_tn(probs_tn)
+    ops.gemm_grouped(probs_nt)
+    torch.cuda.synchronize()
+    for o1, o2 in outs:
+        assert torch.equal(o1, o2)
+    # bf16 output
+    a, w, _ = probs_tn[0]
+    ob = torch.empty((a.shape[1], w.shape[1]), device=gpu_device, dtype=torch.bfloat16)
+    ops.gemm_grouped_tn([(a, w, ob)])
+    torch.cuda.synchronize()
+    assert torch.equal(ob, outs[0][0].bfloat16())
+
+
+def test_gemm_grouped_tn_rejects_bad_shapes(gpu_device):
+    a = torch.zeros((64, 200), device=gpu_device, dtype=torch.bfloat16)
+    w = torch.zeros((64, 256), device=gpu_device, dtype=torch.bfloat16)
+    with pytest.raises(Exception, match="M, N"):
+        ops.gemm_grouped_tn([(a, w, torch.zeros((200, 256), device=gpu_device))])
