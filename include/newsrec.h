@@ -575,6 +575,8 @@ typedef struct nr_final_train_args {
   float *g_tok_g, *g_tok_b, *g_W1, *g_b1, *g_W2, *g_b2, *g_W3, *g_b3, *g_W4, *g_b4, *g_W5;
   float* loss;  /* device scalar (set, not accumulated) */
   float* users; /* nullable [B][1024] */
+  float* sumsq; /* nullable device scalar: set to the sum of squares of every gradient written (the
+                   clip_grad_norm_ input; nr_adamw's `sumsq`), summed on the fly in bf16 mode */
 } nr_final_train_args;
 
 int64_t nr_final_train_workspace_bytes(int dtype, int64_t B, int64_t U, int64_t Hs);

@@ -163,7 +163,7 @@ class FinalTrainArgs(ctypes.Structure):
                  ("Hs", ctypes.c_int64)]
                 + [(n, ctypes.c_void_p) for n in ("tok_last", "hist_idx", "hist_off", "pos", "neg")]
                 + [("margin", ctypes.c_float), ("p", ctypes.c_float), ("seed", ctypes.c_uint64 * 3)]
-                + [(n, ctypes.c_void_p) for n in FINAL_TRAIN_PARAMS + FINAL_TRAIN_GRADS + ("loss", "users")])
+                + [(n, ctypes.c_void_p) for n in FINAL_TRAIN_PARAMS + FINAL_TRAIN_GRADS + ("loss", "users", "sumsq")])
 
 
 class NewsRecHIPError(RuntimeError):

@@ -11,9 +11,15 @@
 //   per batch row: u_d = sum_i X_id P_id / (sum_i P_id + 1e-10)   (modeling_utils.py:224-228)
 //        loss = MarginRankingLoss(2)(cos(u, E[pos]), cos(u, E[neg]))   (trainer.py:1058-1066)
 //   backward: pool' -> dL (logits of linear5), dXp (X) -> dY = drop'(dL W5) -> dX = dY W4 + dXp
-//        -> dZ2 = drop'(dX W3) -> dZ1 = drop'(dZ2 W2) -> dS = dZ1 W1 -> dE[hist] += dS
+//        -> dZ2 = drop'(dX W3) -> dZ1 = drop'(dZ2 W2)
 //        weight grads dW5 = dL^T Y, dW4 = dY^T X, dW3 = dX^T X2, dW2 = dZ2^T X1, dW1 = dZ1^T S
 //        bias grads = column sums of dY, dX, dZ2, dZ1; token LayerNorm parameter grads.
+//   The history gather's gradient dS = dZ1 W1 is never formed: its only consumer is
+//   the token LayerNorm's parameters (E is the LN of the last token), and with
+//   S = xhat gamma + beta its contributions are sum_slots dS = g_b1 W1 and
+//   sum_slots dS o xhat = sum_h W1[h] o M[h], M = dZ1^T xhat -- the weight-grad GEMM
+//   of W1 run on xhat instead of S, dW1 = gamma o M + g_b1 (x) beta (w1_fold_kernel):
+//   the dS GEMM (70 GFLOP), its scatter into the U rows and their LN reduction go.
 //
 // FinalAttention runs once per VALID history slot (the reference's padded slots
 // carry zero pooling weight and so zero gradient).  Dropout: the counter-hash
@@ -35,11 +41,36 @@ namespace ft {
 
 constexpr int64_t D = 1024, H = 4096;
 constexpr int kSplit = 8;  // K-slices of a split-K tail
+// sum-of-squares partials of the bf16 step: 512 weight-grad tiles, then the W1 fold's
+// 16 x 64 blocks, the bias reduction's 208 blocks, the token LN reduction's 16
+constexpr int kSqTn = 512, kSqFold = (1024 / 64) * (4096 / 64), kSqBias = (3 * 4096 + 1024) / 64, kSqLn = 1024 / 64;
+constexpr int kSqParts = kSqTn + kSqFold + kSqBias + kSqLn;
 
 static int64_t pad64(int64_t n) { return n < 64 ? 64 : (n + 63) / 64 * 64; }
 static int64_t al(int64_t b) { return (b + 255) / 256 * 256; }
 
 // ------------------------------------------------------------------ small kernels
+template <typename T>
+__device__ __forceinline__ void ld4(const T* p, float v[4]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    v[0] = bf16_lo(u.x); v[1] = bf16_hi(u.x); v[2] = bf16_lo(u.y); v[3] = bf16_hi(u.y);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st4(T* p, const float v[4]) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
+  } else {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<b4*>(p) = __builtin_convertvector(f4{v[0], v[1], v[2], v[3]}, b4);
+  }
+}
+
 struct ZList {  // zero up to 8 f32 ranges in one launch
   float* p[8];
   int64_t len[8];
@@ -51,68 +82,306 @@ __global__ __launch_bounds__(256) void zero_kernel(ZList z) {
       z.p[i][j] = 0.f;
 }
 
-// S[i] = E[hist[i]] for i < Hs, zero rows for Hs <= i < Hp (the packed history
-// slots); f32 -> TA, 4 columns per lane (16-B loads), one wave per row.
+// From the token rows' LayerNorm xhat (f32 [U][D], gamma = 1 / beta = 0): slot rows
+// i < Hp get S[i] = xhat[hist[i]] gamma + beta and XH[i] = xhat[hist[i]] (TA; zero
+// rows past Hs), news rows u < U get E[u] = xhat[u] gamma + beta (f32, the cosine's
+// rows).  One wave per row, 4 columns per lane.
 template <typename TA>
-__global__ __launch_bounds__(256) void gather_slots_kernel(int64_t Hp, int64_t Hs, const float* __restrict__ E,
-                                                           const int32_t* __restrict__ hist, TA* __restrict__ S) {
+__global__ __launch_bounds__(256) void slots_kernel(int64_t Hp, int64_t Hs, int64_t U, const float* __restrict__ xh,
+                                                    const int32_t* __restrict__ hist, const float* __restrict__ g,
+                                                    const float* __restrict__ b, TA* __restrict__ S,
+                                                    TA* __restrict__ XH, float* __restrict__ E) {
   const int lane = threadIdx.x & 63;
-  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < Hp; i += (int64_t)gridDim.x * 4) {
-    const int64_t r = i < Hs ? (int64_t)hist[i] : -1;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < Hp + U; i += (int64_t)gridDim.x * 4) {
+    const bool slot = i < Hp;
+    const int64_t r = slot ? (i < Hs ? (int64_t)hist[i] : -1) : i - Hp;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t c = 256 * j + 4 * lane;
-      const f32x4 v = r >= 0 ? *reinterpret_cast<const f32x4*>(E + r * D + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (sizeof(TA) == 4) {
-        *reinterpret_cast<f32x4*>(S + i * D + c) = v;
+      float v[4] = {0.f, 0.f, 0.f, 0.f}, gg[4], bb[4], e[4];
+      if (r >= 0) ld4<float>(xh + r * D + c, v);
+      ld4<float>(g + c, gg);
+      ld4<float>(b + c, bb);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) e[t] = r >= 0 ? fmaf(v[t], gg[t], bb[t]) : 0.f;
+      if (slot) {
+        st4<TA>(S + i * D + c, e);
+        st4<TA>(XH + i * D + c, v);
       } else {
-        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-        *reinterpret_cast<bf16x4*>(S + i * D + c) = __builtin_convertvector(v, bf16x4);
+        st4<float>(E + (i - Hp) * D + c, e);
       }
     }
   }
 }
 
+// The token LayerNorm's part of the backward without the dS GEMM.  The history
+// gather's gradient dS = dZ1 W1 only ever reaches the token LN parameters (E is
+// the last-token LN, attention.py:193), and with S = xhat gamma + beta:
+//   sum_slots dS = g_b1 W1                         -> dbeta  += g_b1 W1
+//   sum_slots dS o xhat = sum_h W1[h] o M[h]       -> dgamma += sum_h W1[h] o M[h],  M = dZ1^T XH
+//   dW1 = dZ1^T S = gamma o M + g_b1 (x) beta      (M computed in dW1's buffer, rewritten here)
+// Block = 64 columns x 64 rows h (4 groups of 16 rows, folded in LDS); per-chunk
+// partials [H / 64][2][D] summed in chunk order by ln_reduce_kernel (deterministic).
+template <typename TA>
+__global__ __launch_bounds__(256) void w1_fold_kernel(const TA* __restrict__ W1, float* __restrict__ gW1,
+                                                      const float* __restrict__ gb1, const float* __restrict__ g,
+                                                      const float* __restrict__ b, float* __restrict__ part,
+                                                      float* __restrict__ sqp) {
+  __shared__ float red[2][4][64];
+  __shared__ float rsq[4];
+  const int grp = threadIdx.x >> 6, cl = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * 64 + cl;
+  const int64_t h0 = (int64_t)blockIdx.y * 64 + grp * 16;
+  const float gc = g[c], bc = b[c];
+  float sg = 0.f, sb = 0.f, sq = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int64_t h = h0 + k;
+    const float w = (float)W1[h * D + c], m = gW1[h * D + c], gh = gb1[h];
+    sg = fmaf(w, m, sg);
+    sb = fmaf(w, gh, sb);
+    const float dw = fmaf(gc, m, bc * gh);
+    gW1[h * D + c] = dw;
+    sq = fmaf(dw, dw, sq);
+  }
+  red[0][grp][cl] = sg;
+  red[1][grp][cl] = sb;
+  if (sqp) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    if (cl == 0) rsq[grp] = sq;
+  }
+  __syncthreads();
+  if (sqp && threadIdx.x == 0)
+    sqp[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = (rsq[0] + rsq[1]) + (rsq[2] + rsq[3]);
+  if (threadIdx.x < 128) {
+    const int w = threadIdx.x >> 6;
+    const float v = (red[w][0][cl] + red[w][1][cl]) + (red[w][2][cl] + red[w][3][cl]);
+    part[(int64_t)blockIdx.y * 2 * D + w * D + c] = v;
+  }
+}
+// dg[c] += sum_k part[k][0][c], db[c] += sum_k part[k][1][c]: 64 columns x 4 chunk groups per block
+__global__ __launch_bounds__(256) void ln_reduce_kernel(int nchunk, const float* __restrict__ part,
+                                                        float* __restrict__ dg, float* __restrict__ db,
+                                                        float* __restrict__ sqp) {
+  __shared__ float red[2][4][64];
+  const int grp = threadIdx.x >> 6, cl = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * 64 + cl;
+  float sg = 0.f, sb = 0.f;
+  for (int k = grp; k < nchunk; k += 4) {
+    sg += part[(int64_t)k * 2 * D + c];
+    sb += part[(int64_t)k * 2 * D + D + c];
+  }
+  red[0][grp][cl] = sg;
+  red[1][grp][cl] = sb;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const float vg = dg[c] + ((red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]));
+    const float vb = db[c] + ((red[1][0][cl] + red[1][1][cl]) + (red[1][2][cl] + red[1][3][cl]));
+    dg[c] = vg;
+    db[c] = vb;
+    if (sqp) {
+      float q = fmaf(vg, vg, vb * vb);
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o, 64);
+      if (cl == 0) sqp[blockIdx.x] = q;
+    }
+  }
+}
+
+// *out = the ordered sum of n partial sums of squares (the step's grad norm^2:
+// clip_grad_norm_ reads it, trainer.py:1067-1070).  One block.
+__global__ __launch_bounds__(256) void sq_total_kernel(int64_t n, const float* __restrict__ part,
+                                                       float* __restrict__ out) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 256) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < 256; ++k) t += red[k];
+    *out = t;
+  }
+}
+
+// F.cosine_similarity(u, E[pos / neg]) with the per-vector 1e-8 clamp and
+// MarginRankingLoss(margin) (trainer.py:1058-1066), as nr_cosine_margin, but the
+// gradients of E[pos[b]] / E[neg[b]] are written per pair ([2B][D]: no atomics
+// into a [U][D] dE) and the per-row loss terms kept for an ordered sum: E is
+// the token LN's output, so those rows only feed pair_ln_kernel.  One wave per row.
+__global__ __launch_bounds__(256) void cos_pairs_kernel(int64_t B, const float* __restrict__ users,
+                                                        const float* __restrict__ E, const int32_t* __restrict__ pos,
+                                                        const int32_t* __restrict__ neg, float margin,
+                                                        float* __restrict__ lrow, float* __restrict__ du,
+                                                        float* __restrict__ gpair) {
+  constexpr float EPS = 1e-8f;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float u[4][4], ep[4][4], en[4][4];
+  float uu = 0.f, pp = 0.f, nn = 0.f, up = 0.f, un = 0.f;
+  const float* pr = E + (int64_t)pos[b] * D;
+  const float* qr = E + (int64_t)neg[b] * D;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = j * 256 + lane * 4;
+    ld4<float>(users + b * D + e, u[j]);
+    ld4<float>(pr + e, ep[j]);
+    ld4<float>(qr + e, en[j]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      uu = fmaf(u[j][t], u[j][t], uu);
+      pp = fmaf(ep[j][t], ep[j][t], pp);
+      nn = fmaf(en[j][t], en[j][t], nn);
+      up = fmaf(u[j][t], ep[j][t], up);
+      un = fmaf(u[j][t], en[j][t], un);
+    }
+  }
+  auto wsum = [](float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  };
+  uu = wsum(uu); pp = wsum(pp); nn = wsum(nn); up = wsum(up); un = wsum(un);
+  const float nu = sqrtf(uu), np_ = sqrtf(pp), nq = sqrtf(nn);
+  const float iu = 1.0f / fmaxf(nu, EPS), ip = 1.0f / fmaxf(np_, EPS), iq = 1.0f / fmaxf(nq, EPS);
+  const float sp = up * iu * ip, sn = un * iu * iq;
+  const float v = margin - (sp - sn);
+  const float act = v >= 0.f ? 1.0f : 0.0f;  // clamp_min backward passes where input >= min
+  const float gsp = -act / (float)B, gsn = act / (float)B;
+  if (lane == 0) lrow[b] = fmaxf(v, 0.f) / (float)B;
+  const float cu = nu > EPS ? 1.f : 0.f, cp = np_ > EPS ? 1.f : 0.f, cq = nq > EPS ? 1.f : 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = j * 256 + lane * 4;
+    float g[4], gp[4], gn[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float uh = u[j][t] * iu, ph = ep[j][t] * ip, qh = en[j][t] * iq;
+      g[t] = gsp * (ph - cu * sp * uh) * iu + gsn * (qh - cu * sn * uh) * iu;
+      gp[t] = gsp * (uh - cp * sp * ph) * ip;
+      gn[t] = gsn * (uh - cq * sn * qh) * iq;
+    }
+    st4<float>(du + b * D + e, g);
+    st4<float>(gpair + b * D + e, gp);
+    st4<float>(gpair + (B + b) * D + e, gn);
+  }
+}
+
+// The pairs' part of the token LN parameter grads (dgamma = sum g o xhat, dbeta =
+// sum g over the 2B pair rows; SET, the W1 fold adds the history's part), and,
+// by block 0, the loss as the ordered sum of the per-row terms.  Block = 64
+// columns x 4 row groups.
+__global__ __launch_bounds__(256) void pair_ln_kernel(int64_t B, const float* __restrict__ gpair,
+                                                      const float* __restrict__ xh, const int32_t* __restrict__ pos,
+                                                      const int32_t* __restrict__ neg, const float* __restrict__ lrow,
+                                                      float* __restrict__ dg, float* __restrict__ db,
+                                                      float* __restrict__ loss) {
+  __shared__ float red[2][4][64];
+  const int grp = threadIdx.x >> 6, cl = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * 64 + cl;
+  float sg = 0.f, sb = 0.f;
+  for (int64_t r = grp; r < 2 * B; r += 4) {
+    const int64_t news = r < B ? pos[r] : neg[r - B];
+    const float gv = gpair[r * D + c];
+    sg = fmaf(gv, xh[news * D + c], sg);
+    sb += gv;
+  }
+  red[0][grp][cl] = sg;
+  red[1][grp][cl] = sb;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    dg[c] = (red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]);
+    db[c] = (red[1][0][cl] + red[1][1][cl]) + (red[1][2][cl] + red[1][3][cl]);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float l = 0.f;
+    for (int64_t r = 0; r < B; ++r) l += lrow[r];
+    *loss = l;
+  }
+}
+
 // out[r0 / 128 + b][c] = sum of rows [r0 + 128 b, r0 + 128 (b + 1)) of src's column c
 // (rows < rows_end): the column sums of a split-K tail's rows, in the layout of
-// the persistent GEMM's CS partials.  Block = 256 columns x one 128-row block.
+// the persistent GEMM's CS partials.  Block = 256 columns x one 128-row block:
+// 8 row groups of 32 lanes x 8 columns (16-B loads), folded in LDS in a fixed order.
 template <typename TA>
 __global__ __launch_bounds__(256) void colsum_block_kernel(int64_t r0, int64_t rows_end, int64_t cols, const TA* src,
                                                            int64_t lds, float* out) {
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ float red[8][256];
+  const int grp = threadIdx.x >> 5, cl = threadIdx.x & 31;
+  const int64_t c = (int64_t)blockIdx.x * 256 + 8 * cl;
   const int64_t b0 = r0 + (int64_t)blockIdx.y * 128;
-  if (c >= cols) return;
-  float s = 0.f;
   const int64_t e = b0 + 128 < rows_end ? b0 + 128 : rows_end;
-  for (int64_t r = b0; r < e; ++r) s += (float)src[r * lds + c];
-  out[(b0 >> 7) * cols + c] = s;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int64_t r = b0 + grp; r < e; r += 8) {
+    float v[4], w[4];
+    ld4<TA>(src + r * lds + c, v);
+    ld4<TA>(src + r * lds + c + 4, w);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { acc[t] += v[t]; acc[4 + t] += w[t]; }
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t) red[grp][8 * cl + t] = acc[t];
+  __syncthreads();
+  const int col = threadIdx.x;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s += red[k][col];
+  out[(b0 >> 7) * cols + (int64_t)blockIdx.x * 256 + col] = s;
 }
 
 // g[c] = sum_r part[r][c] over up to 4 (partials, rows, cols, out) problems: the
-// bias gradients (fixed row order: deterministic).
+// bias gradients.  Block = 64 columns (16 lanes x 4, 16-B loads) x 16 row groups,
+// folded in LDS in a fixed order (deterministic).
 struct RSum {
   const float* part[4];
   float* out[4];
   int64_t rows[4], cols[4];
   int n;
 };
-__global__ __launch_bounds__(256) void rowsum_kernel(RSum r) {
-  int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  for (int i = 0; i < r.n; ++i) {
-    if (c < r.cols[i]) {
-      float s = 0.f;
-      for (int64_t k = 0; k < r.rows[i]; ++k) s += r.part[i][k * r.cols[i] + c];
-      r.out[i][c] = s;
-      return;
+__global__ __launch_bounds__(256) void rowsum_kernel(RSum r, float* __restrict__ sqp) {
+  __shared__ float red[16][64];
+  int64_t c0 = (int64_t)blockIdx.x * 64;
+  int i = 0;
+  while (i < r.n && c0 >= r.cols[i]) c0 -= r.cols[i++];
+  if (i >= r.n) {  // block-uniform
+    if (sqp && threadIdx.x == 0) sqp[blockIdx.x] = 0.f;
+    return;
+  }
+  const int grp = threadIdx.x >> 4, q = threadIdx.x & 15;
+  const float* p = r.part[i];
+  const int64_t cols = r.cols[i];
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t k = grp; k < r.rows[i]; k += 16) {
+    float v[4];
+    ld4<float>(p + k * cols + c0 + 4 * q, v);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] += v[t];
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) red[grp][4 * q + t] = acc[t];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][threadIdx.x];
+    r.out[i][c0 + threadIdx.x] = s;
+    if (sqp) {
+      float q = s * s;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o, 64);
+      if (threadIdx.x == 0) sqp[blockIdx.x] = q;
     }
-    c -= r.cols[i];
   }
 }
 
 // ------------------------------------------------------------------ workspace
 struct Layout {
   int64_t Hp, es, mm, csr;
-  int64_t E, S, X1, X2, XP, Y, users, z, du, dE, dXp, dL, dY, dX, dZ2, dZ1, dS;
+  int64_t E, XHu, S, XH, X1, X2, XP, Y, users, z, du, gpair, lrow, dXp, dL, dY, dX, dZ2, dZ1, w1p, sqp;
   int64_t W1t, W2t, W3t, W4t, W5t, skP, cs4, cs3, cs2, cs1;
   int64_t T[10];  // f32 mode: the weight-grad operands transposed
   int64_t total;
@@ -138,19 +407,21 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs, int ncu) {
   const int64_t Hp = L.Hp, es = L.es, Bp = pad64(B);
   int64_t o = 0;
   auto take = [&](int64_t bytes) { const int64_t r = o; o += al(bytes); return r; };
-  L.E = take(U * D * 4);
-  L.S = take(Hp * D * es); L.X1 = take(Hp * H * es); L.X2 = take(Hp * H * es); L.XP = take(Hp * 2 * D * es);
+  L.E = take(U * D * 4); L.XHu = take(U * D * 4);
+  L.S = take(Hp * D * es); L.XH = take(Hp * D * es); L.X1 = take(Hp * H * es); L.X2 = take(Hp * H * es); L.XP = take(Hp * 2 * D * es);
   L.Y = take(Hp * H * es);
-  L.users = take(Bp * D * 4); L.z = take(Bp * D * 4); L.du = take(Bp * D * 4); L.dE = take(U * D * 4);
+  L.users = take(Bp * D * 4); L.z = take(Bp * D * 4); L.du = take(Bp * D * 4); L.gpair = take(2 * B * D * 4);
+  L.lrow = take(Bp * 4);
+  L.sqp = take(kSqParts * 4);
   L.dXp = take(Hp * D * es); L.dL = take(Hp * D * es); L.dY = take(Hp * H * es); L.dX = take(Hp * D * es);
-  L.dZ2 = take(Hp * H * es); L.dZ1 = take(Hp * H * es); L.dS = take(Hp * D * es);
+  L.dZ2 = take(Hp * H * es); L.dZ1 = take(Hp * H * es); L.w1p = take((H / 64) * 2 * D * 4);
   L.W1t = take(D * H * es); L.W2t = take(H * H * es); L.W3t = take(H * D * es); L.W4t = take(D * H * es);
   L.W5t = take(H * D * es);
   if (dtype == NR_BF16) {
     L.skP = take((int64_t)kSplit * (Hp - L.mm) * H * 4);
     L.cs4 = take(L.csr * H * 4); L.cs3 = take(L.csr * D * 4); L.cs2 = take(L.csr * H * 4); L.cs1 = take(L.csr * H * 4);
   } else {
-    // dL^T, Y^T, dY^T, X^T, dX^T, X2^T, dZ2^T, X1^T, dZ1^T, S^T
+    // dL^T, Y^T, dY^T, X^T, dX^T, X2^T, dZ2^T, X1^T, dZ1^T, XH^T
     const int64_t w[10] = {D, H, H, D, D, H, H, H, H, D};
     for (int i = 0; i < 10; ++i) L.T[i] = take(w[i] * Hp * es);
   }
@@ -187,12 +458,13 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   const Layout L = layout(dt, a.B, a.U, a.Hs, ncu);
   const int64_t B = a.B, U = a.U, Hs = a.Hs, Hp = L.Hp, mm = L.mm;
   auto P_ = [&](int64_t off) { return (void*)(ws + off); };
-  float* E = (float*)P_(L.E);
+  float *E = (float*)P_(L.E), *XHu = (float*)P_(L.XHu);
+  TA* XH = (TA*)P_(L.XH);
   TA *S = (TA*)P_(L.S), *X1 = (TA*)P_(L.X1), *X2 = (TA*)P_(L.X2), *XP = (TA*)P_(L.XP), *Y = (TA*)P_(L.Y);
   float* users = a.users ? a.users : (float*)P_(L.users);
-  float *z = (float*)P_(L.z), *du = (float*)P_(L.du), *dE = (float*)P_(L.dE);
+  float *z = (float*)P_(L.z), *du = (float*)P_(L.du), *gpair = (float*)P_(L.gpair), *lrow = (float*)P_(L.lrow);
   TA *dXp = (TA*)P_(L.dXp), *dL = (TA*)P_(L.dL), *dY = (TA*)P_(L.dY), *dX = (TA*)P_(L.dX), *dZ2 = (TA*)P_(L.dZ2);
-  TA *dZ1 = (TA*)P_(L.dZ1), *dS = (TA*)P_(L.dS);
+  TA* dZ1 = (TA*)P_(L.dZ1);
   TA *W1t = (TA*)P_(L.W1t), *W2t = (TA*)P_(L.W2t), *W3t = (TA*)P_(L.W3t), *W4t = (TA*)P_(L.W4t),
      *W5t = (TA*)P_(L.W5t);
   const TA *W1 = (const TA*)a.W1, *W2 = (const TA*)a.W2, *W3 = (const TA*)a.W3, *W4 = (const TA*)a.W4,
@@ -216,24 +488,25 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   }
   NR_FT_EV(hipEventRecord(side.wt, side.s), "transpose record");
 
-  // ---- accumulators: loss, dE (cosine + history scatter), the token LN grads
-  // (and, f32 mode, the bias grads that nr_col_sum accumulates)
-  {
+  // ---- accumulators: f32 mode's bias grads (nr_col_sum adds); everything else is
+  // written whole (the loss and token LN grads by ordered sums, no atomics)
+  if constexpr (!BF) {
     ZList zl{};
-    float* zp[8] = {a.loss, dE, a.g_tok_g, a.g_tok_b, a.g_b1, a.g_b2, a.g_b3, a.g_b4};
-    const int64_t zn[8] = {1, U * D, D, D, H, H, D, H};
-    zl.n = BF ? 4 : 8;
+    float* zp[4] = {a.g_b1, a.g_b2, a.g_b3, a.g_b4};
+    const int64_t zn[4] = {H, H, D, H};
+    zl.n = 4;
     for (int i = 0; i < zl.n; ++i) { zl.p[i] = zp[i]; zl.len[i] = zn[i]; }
-    hipLaunchKernelGGL(zero_kernel, dim3(512), dim3(256), 0, st, zl);
+    hipLaunchKernelGGL(zero_kernel, dim3(64), dim3(256), 0, st, zl);
     NR_CHECK_LAUNCH("nr_final_train_step (zero)");
   }
   // ---- forward
-  NR_FT(gather_ln_dispatch(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1, a.tok_g, a.tok_b, 1e-12f, E, D, st));
+  // xhat of the U token rows (LN without the affine), then the slots' S and XH and the news rows' E
+  NR_FT(gather_ln_dispatch(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1, nullptr, nullptr, 1e-12f, XHu, D, st));
   {
-    const int64_t g = (Hp + 3) / 4;
-    hipLaunchKernelGGL((gather_slots_kernel<TA>), dim3((unsigned)(g < 2048 ? g : 2048)), dim3(256), 0, st, Hp, Hs, E,
-                       a.hist_idx, S);
-    NR_CHECK_LAUNCH("nr_final_train_step (gather)");
+    const int64_t g = (Hp + U + 3) / 4;
+    hipLaunchKernelGGL((slots_kernel<TA>), dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, Hp, Hs, U, XHu,
+                       a.hist_idx, a.tok_g, a.tok_b, S, XH, E);
+    NR_CHECK_LAUNCH("nr_final_train_step (slots)");
   }
   // relu(dropout) GEMM over Hp rows: main rows on the persistent kernel, the tail as K-slices + fixup
   auto relu_gemm = [&](const TA* A, int64_t lda, const TA* W, int64_t K, const float* bias, uint64_t seed, TA* C,
@@ -255,7 +528,13 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   NR_FT(gemm_dispatch(dt, dt, NR_EPI_EXP, Hp, D, H, Y, H, W5, H, nullptr, nullptr, 0, Pexp, 2 * D, st));
   NR_FT(nr_final_pool_fwd(dt, B, a.hist_off, XP, 2 * D, users, z, st));
   // ---- loss and its gradient into the pooled users and E[pos] / E[neg]
-  NR_FT(nr_cosine_margin(B, users, E, D, a.pos, a.neg, a.margin, nullptr, a.loss, du, dE, st));
+  hipLaunchKernelGGL(cos_pairs_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, users, E, a.pos, a.neg,
+                     a.margin, lrow, du, gpair);
+  NR_CHECK_LAUNCH("nr_final_train_step (cosine)");
+  // the pairs' token LN grads (set) and the loss, ahead of the W1 fold that adds the history's
+  hipLaunchKernelGGL(pair_ln_kernel, dim3((unsigned)(D / 64)), dim3(256), 0, st, B, gpair, XHu, a.pos, a.neg, lrow,
+                     a.g_tok_g, a.g_tok_b, a.loss);
+  NR_CHECK_LAUNCH("nr_final_train_step (pair LN grads)");
   NR_FT(nr_final_pool_bwd(dt, B, a.hist_off, Hp, XP, 2 * D, users, z, du, dXp, D, dL, D, st));
   // ---- data-grad chain (weights transposed on the side stream)
   NR_FT_EV(hipStreamWaitEvent(st, side.wt, 0), "transpose wait");
@@ -293,7 +572,7 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   }
   NR_FT(drelu_gemm(dX, D, W3t, X2, dZ2, cs2, a.g_b2));
   NR_FT(drelu_gemm(dZ2, H, W2t, X1, dZ1, cs1, a.g_b1));
-  NR_FT(gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, H, dZ1, H, W1t, H, nullptr, nullptr, 0, dS, D, st));
+  // (no dS = dZ1 W1: its only consumer, the token LN parameters, folds into dW1 below)
   // ---- weight grads: dW = dOut^T X
   if constexpr (BF) {
     GemmProblem p[5] = {
@@ -301,21 +580,29 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
         {H, D, Hp, dY, H, 0, X, 2 * D, 0, a.g_W4, D, 0, 1, 1.0f},
         {D, H, Hp, dX, D, 0, X2, H, 0, a.g_W3, H, 0, 1, 1.0f},
         {H, H, Hp, dZ2, H, 0, X1, H, 0, a.g_W2, H, 0, 1, 1.0f},
-        {H, D, Hp, dZ1, H, 0, S, D, 0, a.g_W1, D, 0, 1, 1.0f},
+        {H, D, Hp, dZ1, H, 0, XH, D, 0, a.g_W1, D, 0, 1, 1.0f},  // M = dZ1^T XH (w1_fold_kernel)
     };
-    NR_FT(gemm_group_tn_dispatch(NR_F32, p, 5, st));
+    float* sqp = a.sumsq ? (float*)P_(L.sqp) : nullptr;
+    const bool sqf[5] = {true, true, true, true, false};  // dW1 is M here: counted by the fold
+    int ntiles = 0;
+    NR_FT(gemm_group_tn_dispatch(NR_F32, p, 5, st, sqp, sqf, &ntiles));
+    if (sqp && ntiles != kSqTn) {
+      set_error("nr_final_train_step: %d weight-grad tiles (expected %d)", ntiles, kSqTn);
+      return NR_ERR_INVALID;
+    }
     RSum r{};
     float* parts[4] = {cs1, cs2, cs3, cs4};
     float* outs[4] = {a.g_b1, a.g_b2, a.g_b3, a.g_b4};
     const int64_t cols[4] = {H, H, D, H};
     r.n = 4;
     for (int i = 0; i < 4; ++i) { r.part[i] = parts[i]; r.out[i] = outs[i]; r.rows[i] = L.csr; r.cols[i] = cols[i]; }
-    hipLaunchKernelGGL(rowsum_kernel, dim3((unsigned)((3 * H + D) / 256)), dim3(256), 0, st, r);
+    hipLaunchKernelGGL(rowsum_kernel, dim3((unsigned)((3 * H + D) / 64)), dim3(256), 0, st, r,
+                       sqp ? sqp + kSqTn + kSqFold : nullptr);
     NR_CHECK_LAUNCH("nr_final_train_step (bias grads)");
   } else {
     TA* T[10];
     for (int i = 0; i < 10; ++i) T[i] = (TA*)P_(L.T[i]);
-    const TA* src[10] = {dL, Y, dY, X, dX, X2, dZ2, X1, dZ1, S};
+    const TA* src[10] = {dL, Y, dY, X, dX, X2, dZ2, X1, dZ1, XH};
     const int64_t cols[10] = {D, H, H, D, D, H, H, H, H, D}, ld[10] = {D, H, H, 2 * D, D, H, H, H, H, D};
     for (int i = 0; i < 10; ++i) NR_FT(nr_transpose(dt, dt, Hp, cols[i], src[i], ld[i], T[i], Hp, st));
     GemmProblem p[5] = {
@@ -327,9 +614,28 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
     };
     NR_FT(gemm_group_dispatch(dt, NR_F32, p, 5, st));
   }
-  // ---- history gather -> unique news rows -> token LayerNorm parameter grads
-  NR_FT(nr_scatter_add_rows(dt, Hs, D, dS, D, a.hist_idx, dE, D, st));
-  NR_FT(nr_ln_param_grad(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1e-12f, dE, D, a.g_tok_g, a.g_tok_b, st));
+  // ---- token LayerNorm parameter grads: the history gather's part folded with dW1
+  // (w1_fold_kernel; dW1 = gamma o M + g_b1 (x) beta), added to the pairs' part
+  {
+    float* w1p = (float*)P_(L.w1p);
+    float* sqp = BF && a.sumsq ? (float*)P_(L.sqp) : nullptr;
+    hipLaunchKernelGGL((w1_fold_kernel<TA>), dim3((unsigned)(D / 64), (unsigned)(H / 64)), dim3(256), 0, st, W1,
+                       a.g_W1, a.g_b1, a.tok_g, a.tok_b, w1p, sqp ? sqp + kSqTn : nullptr);
+    NR_CHECK_LAUNCH("nr_final_train_step (W1 fold)");
+    hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)(D / 64)), dim3(256), 0, st, (int)(H / 64), w1p, a.g_tok_g,
+                       a.g_tok_b, sqp ? sqp + kSqTn + kSqFold + kSqBias : nullptr);
+    NR_CHECK_LAUNCH("nr_final_train_step (token LN grads)");
+    if (sqp) {
+      hipLaunchKernelGGL(sq_total_kernel, dim3(1), dim3(256), 0, st, (int64_t)kSqParts, sqp, a.sumsq);
+      NR_CHECK_LAUNCH("nr_final_train_step (grad norm)");
+    } else if (a.sumsq) {  // f32 mode: over the gradient arrays
+      hipLaunchKernelGGL(zero_kernel, dim3(1), dim3(256), 0, st, ZList{{a.sumsq}, {1}, 1});
+      NR_CHECK_LAUNCH("nr_final_train_step (zero)");
+      float* gs[11] = {a.g_tok_g, a.g_tok_b, a.g_W1, a.g_b1, a.g_W2, a.g_b2, a.g_W3, a.g_b3, a.g_W4, a.g_b4, a.g_W5};
+      const int64_t gn[11] = {D, D, H * D, H, H * H, H, D * H, D, H * D, H, D * H};
+      for (int i = 0; i < 11; ++i) NR_FT(nr_sumsq(gn[i], gs[i], a.sumsq, st));
+    }
+  }
   return NR_OK;
 }
 #undef NR_FT

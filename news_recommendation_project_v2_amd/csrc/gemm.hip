@@ -283,6 +283,7 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
   constexpr int RPI = 64 / LPR;                            // rows per wave instruction
   const int cl = lane & 31, rh = 4 * (lane >> 5);
   float* slab = reinterpret_cast<float*>(smem + wave * 16384);
+  float sq = 0.f;  // ea.sq_part: this thread's sum of squares of the values it stores
   // The slabs overlay the operand stages: one workgroup barrier so that no
   // wave still reads operands; after it each wave only touches its own slab,
   // so the passes order their LDS traffic wave-locally (no further workgroup
@@ -410,11 +411,31 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
 #pragma unroll
         for (int q = 0; q < VEC; ++q) o[q] = to_out<TO>(v[q]);
         *reinterpret_cast<uint4*>(C + row * ldc + ocol0 + cc) = *reinterpret_cast<const uint4*>(o);
+        if (ea.sq_part) {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) {
+            const float f = from_out<TO>(o[q]);
+            sq = fmaf(f, f, sq);
+          }
+        }
       }
     }
     NR_EPI_SYNC();
   }
 #undef NR_EPI_SYNC
+  if (ea.sq_part) {  // workgroup-uniform: the tile's sum of squares (the training step's grad norm)
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    if (lane == 0) red[wave] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+      for (int w = 0; w < 8; ++w) t += red[w];
+      ea.sq_part[blockIdx.x] = ea.sq_on ? t : 0.f;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -732,6 +753,8 @@ struct GemmGroup {
   void* C[kGroupMax];
   int64_t lda[kGroupMax], ldw[kGroupMax], ldc[kGroupMax];
   int64_t sA[kGroupMax], sW[kGroupMax], sC[kGroupMax];
+  float* sq_part;        // nullable: per-workgroup sum of squares of C (ea.sq_part)
+  bool sq[kGroupMax];    // which problems' tiles count in it
 };
 
 template <typename TI, typename TO, bool MF16, bool TN = false>
@@ -743,10 +766,13 @@ __global__ __launch_bounds__(512, 2) void gemm256p_group_kernel(GemmGroup g) {
   const int local = t - (p ? g.tile_end[p - 1] : 0);
   const int b = local / g.tpb[p], lt = local - b * g.tpb[p];
   const int nx = g.ntn[p];
+  EpiArgs ea{0, 0, g.alpha[p]};
+  ea.sq_part = g.sq_part;
+  ea.sq_on = g.sq[p];
   gemm256p_body<TI, NR_EPI_NONE, TO, MF16, TN>(smem, (int64_t)(lt / nx) * G2BM, (int64_t)(lt % nx) * G2BN, g.M[p],
                                                g.N[p], g.K[p], (const TI*)g.A[p] + b * g.sA[p], g.lda[p],
                                                (const TI*)g.W[p] + b * g.sW[p], g.ldw[p], nullptr, nullptr, 0,
-                                               (TO*)g.C[p] + b * g.sC[p], g.ldc[p], EpiArgs{0, 0, g.alpha[p]});
+                                               (TO*)g.C[p] + b * g.sC[p], g.ldc[p], ea);
 }
 
 int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, int n, hipStream_t s) {
@@ -801,10 +827,12 @@ int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, i
 // weight-grad GEMMs dW = dOut^T X of the training steps on their row-major
 // activations.  Batches (sA / sW / sC) give split-K slices: A + b sA is K-rows
 // b kw.. of the same activation.  M, N multiples of 256, K of 64.
-int gemm_group_tn_dispatch(int dtype_out, const GemmProblem* probs, int n, hipStream_t s) {
+int gemm_group_tn_dispatch(int dtype_out, const GemmProblem* probs, int n, hipStream_t s, float* sq_part,
+                           const bool* sq, int* n_tiles) {
   NR_CHECK_ARG(dtype_out == NR_F32 || dtype_out == NR_BF16, "gemm_group_tn: bad dtype_out %d", dtype_out);
   NR_CHECK_ARG(n >= 0 && n <= kGroupMax, "gemm_group_tn: n=%d outside [0, %d]", n, kGroupMax);
   GemmGroup g{};
+  g.sq_part = sq_part;
   int64_t tiles = 0;
   const int64_t vo = dtype_out == NR_F32 ? 4 : 8;
   for (int i = 0; i < n; ++i) {
@@ -825,6 +853,7 @@ int gemm_group_tn_dispatch(int dtype_out, const GemmProblem* probs, int n, hipSt
     g.lda[j] = q.lda; g.ldw[j] = q.ldw; g.ldc[j] = q.ldc;
     g.sA[j] = q.sA; g.sW[j] = q.sW; g.sC[j] = q.sC;
     g.alpha[j] = q.alpha;
+    g.sq[j] = sq ? sq[i] : false;
     g.ntn[j] = (int)(q.N / G2BN);
     const int64_t tpb = (q.M / G2BM) * g.ntn[j];
     g.tpb[j] = (int)tpb;
@@ -832,6 +861,7 @@ int gemm_group_tn_dispatch(int dtype_out, const GemmProblem* probs, int n, hipSt
     NR_CHECK_ARG(tiles <= 0x7fffffff, "gemm_group_tn: too many tiles");
     g.tile_end[j] = (int)tiles;
   }
+  if (n_tiles) *n_tiles = (int)tiles;
   if (g.n == 0) return NR_OK;
   if (dtype_out == NR_F32)
     hipLaunchKernelGGL((gemm256p_group_kernel<__bf16, float, true, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);

@@ -303,7 +303,11 @@ __global__ __launch_bounds__(512) void segmean_kernel(int64_t B, int64_t Bp, con
 // the per-vector 1e-8 clamp and MarginRankingLoss(margin), mean over B
 // (trainer.py:1058-1066); backward: du as nr_cosine_margin, dm = (du - u (u .
 // du)) / |m| (normalize backward; du / 1e-12 below the clamp).  Writes users = u,
-// dmA = dm, dmc = dm / h_b (rows b in [B, Bp): zero), gb2 += dm, dE[pos / neg]
+// dmA = dm, dmc = dm / h_b (rows b in [B, Bp): zero; dmc32 = the same in f32: the
+// residual of LN_f's backward, where the bf16 dmc -- one rounding shared by all
+// h_b slots of the row -- gave the token LN bias grad, whose dominant term is
+// sum_b dm_b, a correlated 2^-9 error the bf16 numerics model does not have),
+// gb2 += dm, dE[pos / neg]
 // += their cosine grads (lane-contiguous atomics: 256 B per wave instruction).
 template <typename TA>
 __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int nparts, const float* __restrict__ parts,
@@ -312,7 +316,8 @@ __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int np
                                                    int64_t lde, const int32_t* __restrict__ pos,
                                                    const int32_t* __restrict__ neg, float margin,
                                                    float* __restrict__ loss, float* __restrict__ users,
-                                                   TA* __restrict__ dmA, TA* __restrict__ dmc, float* __restrict__ dE,
+                                                   TA* __restrict__ dmA, TA* __restrict__ dmc,
+                                                   float* __restrict__ dmc32, float* __restrict__ dE,
                                                    float* __restrict__ gb2) {
   constexpr float EPS = 1e-8f, NEPS = 1e-12f;
   __shared__ float red[4];
@@ -323,6 +328,7 @@ __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int np
     for (int j = 0; j < 4; ++j) {
       dmA[b * D + j * 256 + tid] = (TA)0.f;
       dmc[b * D + j * 256 + tid] = (TA)0.f;
+      dmc32[b * D + j * 256 + tid] = 0.f;
     }
     return;
   }
@@ -387,6 +393,7 @@ __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int np
     if (users) users[b * D + c] = u[j];
     dmA[b * D + c] = (TA)dm;
     dmc[b * D + c] = (TA)(dm * icnt);
+    dmc32[b * D + c] = dm * icnt;
   }
 }
 
@@ -489,16 +496,20 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t n_rows, const TA
 // arithmetic) plus a residual gradient, and the LN parameter grads:
 //   dx = rstd (dxh - mean(dxh) - xhat mean(dxh xhat)) + res,  dxh = dy gamma
 //   dgamma += dy xhat, dbeta += dy (per-lane registers, one atomic per column per block)
-// MODE 0 (LN_f of H1): res = dmc[row_seg[row]] (the broadcast dH of the mean),
+// MODE 0 (LN_f of H1): res = dmc32[row_seg[row]] (f32: the broadcast dH of the mean),
 //   dx -> out rows (TA); padding slots (row_seg < 0) -> zero rows.
-// MODE 1 (LN_q of S):  res = dH1 row (TA); dx scattered into dE[idx[row]]
+// MODE 1 (LN_q of S):  x = the f32 row E[idx[row]] the forward normalised (xf, not
+//   the bf16-stored S: the statistics of the rounded row moved the token LN
+//   bias grad ~10x past the bf16 numerics model's drift, test_train_bf16_drift),
+//   res = dH1 row (TA); dx scattered into dE[idx[row]]
 //   (the gradient of the history gather): the row is staged in the wave's LDS
 //   and added with lane-contiguous f32 atomics (256 B per wave instruction, the
 //   full-rate shape of MI355X_MICROARCH.md "Global float atomics"); idx < 0 skipped.
 template <typename TA, int MODE>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, const TA* __restrict__ x,
-                                                     const float* __restrict__ gamma, float eps,
-                                                     const TA* __restrict__ dy, const TA* __restrict__ res,
+                                                     const float* __restrict__ xf, const float* __restrict__ gamma,
+                                                     float eps,
+                                                     const TA* __restrict__ dy, const void* __restrict__ res_,
                                                      const int32_t* __restrict__ sel, TA* __restrict__ out,
                                                      float* __restrict__ dE, int64_t lde, float* __restrict__ dgamma,
                                                      float* __restrict__ dbeta) {
@@ -527,9 +538,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int c = j * 256 + lane * 4;
-      ld4<TA>(x + row * D + c, v[j]);
+      if constexpr (MODE == 1) ld4<float>(xf + (int64_t)s * lde + c, v[j]);
+      else ld4<TA>(x + row * D + c, v[j]);
       ld4<TA>(dy + row * D + c, dyv[j]);
-      ld4<TA>(res + (MODE == 0 ? (int64_t)s : row) * D + c, rv[j]);
+      if constexpr (MODE == 0) ld4<float>(static_cast<const float*>(res_) + (int64_t)s * D + c, rv[j]);
+      else ld4<TA>(static_cast<const TA*>(res_) + row * D + c, rv[j]);
     }
     float sum = 0.f;
 #pragma unroll
@@ -892,7 +905,7 @@ constexpr int kLatParts = 32;  // split-K slices of dlatents' GEMM (K = 8192 -> 
 // Workspace layout (byte offsets), shared by the size query and the step.
 struct Layout {
   int64_t Hp, Hpp, kw, Bp, es;
-  int64_t E, Sx, X, P, H1, Y, G, zbar, h1bar, row_seg, hparts, hsum, dmA, dmc, dZ, dZs, gpart, dG, dY, dH1, dP,
+  int64_t E, Sx, X, P, H1, Y, G, zbar, h1bar, row_seg, hparts, hsum, dmA, dmc, dmc32, dZ, dZs, gpart, dG, dY, dH1, dP,
       dS, dX, dE;
   int64_t dGT, YT, dH1T, PT, dST, XT, dmT, zbarT;
   int64_t WqT, W1T, W2T, WoT, WkvT, latn, latnT, KVp, KV, KVT, A, AT, BtT, Bt;
@@ -916,7 +929,7 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs) {
   L.Y = take(Hp * D * es); L.G = take(Hp * 2 * F * es);
   L.zbar = take(Bp * F * es); L.h1bar = take(Bp * D * 4); L.row_seg = take(Hp * 4);
   L.hparts = take((int64_t)kHParts * Bp * D * 4); L.hsum = take(Bp * D * 4);
-  L.dmA = take(Bp * D * es); L.dmc = take(Bp * D * es); L.dZ = take((int64_t)kZParts * Bp * F * 4);
+  L.dmA = take(Bp * D * es); L.dmc = take(Bp * D * es); L.dmc32 = take(Bp * D * 4); L.dZ = take((int64_t)kZParts * Bp * F * 4);
   L.dZs = take(Bp * F * 4);
   L.gpart = take((Hp + kGRows - 1) / kGRows * 2 * F * 4);
   L.dG = take(Hp * 2 * F * es); L.dY = take(Hp * D * es); L.dH1 = take(Hp * D * es);
@@ -956,6 +969,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   float* hsum = (float*)P_(L.hsum);
   float* dZs = (float*)P_(L.dZs);
   TA *dmA = (TA*)P_(L.dmA), *dmc = (TA*)P_(L.dmc);
+  float* dmc32 = (float*)P_(L.dmc32);
   float* dZ = (float*)P_(L.dZ);
   float* gpart = (float*)P_(L.gpart);
   TA *dG = (TA*)P_(L.dG), *dY = (TA*)P_(L.dY), *dH1 = (TA*)P_(L.dH1), *dP = (TA*)P_(L.dP), *dS = (TA*)P_(L.dS);
@@ -1079,7 +1093,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     if ((rc = sum_parts(hparts, kHParts, Bp * D, hsum, Bp * D, st))) return rc;
   }
   hipLaunchKernelGGL((head_kernel<TA>), dim3((unsigned)Bp), dim3(256), 0, st, B, Bp, 1, hsum, a.b2, h1bar,
-                     a.hist_off, E, (int64_t)D, a.pos, a.neg, a.margin, a.loss, a.users, dmA, dmc, dE, a.g_b2);
+                     a.hist_off, E, (int64_t)D, a.pos, a.neg, a.margin, a.loss, a.users, dmA, dmc, dmc32, dE, a.g_b2);
   NR_LT_CHECK("head");
   // ---- backward
   // dZ_b = (dm_b / h_b) W2 (f32, split-K partials [kZParts, Bp, 4096]): C = dmc . W2T^T
@@ -1123,8 +1137,8 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   }
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, 2 * F, dG, 2 * F, W1T, 2 * F, nullptr, nullptr, 0, dY, D, st)))
     return rc;
-  hipLaunchKernelGGL((ln_bwd_kernel<TA, 0>), dim3(grid_rows(Hp, 512)), dim3(256), 0, st, Hp, Hp, H1, a.nf_g, 1e-5f, dY,
-                     dmc, row_seg, dH1, nullptr, (int64_t)0, a.g_nf_g, a.g_nf_b);
+  hipLaunchKernelGGL((ln_bwd_kernel<TA, 0>), dim3(grid_rows(Hp, 512)), dim3(256), 0, st, Hp, Hp, H1, nullptr, a.nf_g, 1e-5f, dY,
+                     dmc32, row_seg, dH1, nullptr, (int64_t)0, a.g_nf_g, a.g_nf_b);
   NR_LT_CHECK("ln_f_bwd");
   if (dt == NR_BF16) {
     // dS = P (dP - sum_group P dP) in the dP GEMM's epilogue (NR_EPI_SOFTMAX64_BWD, R = P)
@@ -1147,7 +1161,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     return NR_ERR_HIP;
   }
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, S, dS, S, AT, S, nullptr, nullptr, 0, dX, D, st))) return rc;
-  hipLaunchKernelGGL((ln_bwd_kernel<TA, 1>), dim3(grid_rows(Hp, 512)), dim3(256), 0, st, Hp, a.Hs, Sx, a.nq_g, 1e-5f,
+  hipLaunchKernelGGL((ln_bwd_kernel<TA, 1>), dim3(grid_rows(Hp, 512)), dim3(256), 0, st, Hp, a.Hs, Sx, E, a.nq_g, 1e-5f,
                      dX, dH1, a.hist_idx, nullptr, dE, (int64_t)D, a.g_nq_g, a.g_nq_b);
   NR_LT_CHECK("ln_q_bwd");
   // token LayerNorm parameter grads from dE (history scatter + cosine grads)

@@ -41,6 +41,8 @@ struct EpiArgs {
   const float* ln_stats = nullptr;  // LNF epilogue: [M] (mean, rstd) pairs
   const float* ln_uc = nullptr;     // LNF epilogue: u [N] then c [N]
   float* colsum = nullptr;          // persistent kernel, CS: [ceil(M / 128)][N] f32 column sums of each 128-row block
+  float* sq_part = nullptr;         // 256x256 tile kernels: per-workgroup sum of squares of the stored values
+  bool sq_on = false;               //   (written at sq_part[blockIdx.x]; 0 when !sq_on)
 };
 
 int gemm_dispatch_ex(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, int64_t K,
@@ -86,7 +88,10 @@ struct GemmProblem {
 constexpr int kGroupMax = 16;
 int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, int n, hipStream_t s);
 // C = alpha A^T W per problem, A [K][M] and W [K][N] bf16 row-major (gemm.hip, TN grouped launch)
-int gemm_group_tn_dispatch(int dtype_out, const GemmProblem* probs, int n, hipStream_t s);
+// sq_part (nullable): per-workgroup sums of squares of the problems flagged in sq
+// (0 for the others), one per workgroup; *n_tiles (nullable) = the workgroup count.
+int gemm_group_tn_dispatch(int dtype_out, const GemmProblem* probs, int n, hipStream_t s, float* sq_part = nullptr,
+                           const bool* sq = nullptr, int* n_tiles = nullptr);
 int inv_norm_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps,
                       float* out, hipStream_t s);
 

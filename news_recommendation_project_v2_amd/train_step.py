@@ -246,7 +246,7 @@ class FinalAttentionTrainStep:
             src = self.cviews[name] if f.startswith("W") else self.views[name]
             setattr(a, f, src.data_ptr())
             setattr(a, "g_" + f, self.gviews[name].data_ptr())
-        a.loss, a.users = self.loss.data_ptr(), self._users.data_ptr()
+        a.loss, a.users, a.sumsq = self.loss.data_ptr(), self._users.data_ptr(), self.sumsq.data_ptr()
         _lib.check(lib.nr_final_train_step(ctypes.byref(a), self._ws_native.data_ptr(), self._ws_native.numel(),
                                            torch.cuda.current_stream(self.device).cuda_stream), "nr_final_train_step")
         self._keep = (tok, hi, ho, pos, neg)  # alive until the stream has run the step
@@ -256,10 +256,9 @@ class FinalAttentionTrainStep:
         _refresh_mirror(self)
 
     def optimizer_step(self) -> None:
-        """clip_grad_norm_(max_norm) + AdamW, one launch each (trainer.py:1067-1069)."""
+        """clip_grad_norm_(max_norm) + AdamW (trainer.py:1067-1069): one launch; the
+        squared grad norm was summed by the step itself (``sumsq``)."""
         self.step_count += 1
-        self.sumsq.zero_()
-        ops.sumsq(self.grad, self.sumsq)
         ops.adamw(self.flat, self.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps, self.wd,
                   self.max_norm, self.sumsq if self.max_norm > 0 else None, self.flat16)
 

@@ -17,6 +17,8 @@ masks; p = 0 reproduces the reference exactly (tests/golden/train_step.npz).
 """
 from __future__ import annotations
 
+import math
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -64,7 +66,112 @@ def final_attention_train(sd, emb, mask, seeds, p, slot_rows):
     return (x * w).sum(dim=1)
 
 
-def _loss(P, tok_last, hist_groups, pos, neg, p, seeds, ln_eps, margin, pooler="final"):
+class _BF16(torch.autograd.Function):
+    """Round to bf16 (RNE) in the forward; the incoming gradient rounded the same
+    way in the backward (a bf16-stored activation and its bf16-stored gradient)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+def _bf16_weight(w):
+    """bf16 copy of an f32 master weight; the gradient reaches the master unrounded."""
+    return w + (w.detach().to(torch.bfloat16).float() - w.detach())
+
+
+class _Split(torch.autograd.Function):
+    """hi + lo bf16 pair of an f32 value in the forward (the split-bf16 operand of
+    a bf16x3 GEMM); the gradient rounded to bf16 in the backward."""
+
+    @staticmethod
+    def forward(ctx, x):
+        hi = x.to(torch.bfloat16).float()
+        return hi + (x - hi).to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+def _split_weight(w):
+    hi = w.detach().to(torch.bfloat16).float()
+    return w + (hi + (w.detach() - hi).to(torch.bfloat16).float() - w.detach())
+
+
+def final_attention_train_bf16x3(sd, emb, mask):
+    """BF16x3 NUMERICS MODEL (not the reference): the precise-forward variant of the
+    bf16 step -- every forward GEMM operand split into a hi + lo bf16 pair (f32 to
+    16 mantissa bits; the A_lo W_lo product dropped is below that), the backward
+    as the bf16 model (bf16 weights, activations and gradients)."""
+    r, sp = _BF16.apply, _Split.apply
+    Wf = {i: _split_weight(sd[f"linear{i}.weight"]) for i in range(1, 6)}
+    x = F.relu(F.linear(sp(emb), Wf[1], sd["linear1.bias"]))
+    x = F.relu(F.linear(sp(x), Wf[2], sd["linear2.bias"]))
+    x = F.linear(sp(x), Wf[3], sd["linear3.bias"])
+    w = F.relu(F.linear(sp(x), Wf[4], sd["linear4.bias"]))
+    w = torch.exp(F.linear(sp(w), Wf[5])) * mask.unsqueeze(-1)
+    w = w / (w.sum(dim=1, keepdim=True) + 1e-10)
+    return (x * w).sum(dim=1)
+
+
+def final_attention_train_bf16(sd, emb, mask):
+    """BF16 NUMERICS MODEL (not the reference): FinalAttention.forward
+    (modeling_utils.py:218-228) with the HIP bf16 step's rounding points --
+    bf16 weights, every activation the step stores (S, X1, X2, X, Y, P) rounded
+    to bf16 and so their gradients; products exact, sums in f32, pooling in f32.
+    What an ideal RNE bf16 implementation of the step computes (dropout off)."""
+    r = _BF16.apply
+    W = {i: _bf16_weight(sd[f"linear{i}.weight"]) for i in range(1, 6)}
+    x = r(F.relu(F.linear(r(emb), W[1], sd["linear1.bias"])))
+    x = r(F.relu(F.linear(x, W[2], sd["linear2.bias"])))
+    x = r(F.linear(x, W[3], sd["linear3.bias"]))
+    w = r(F.relu(F.linear(x, W[4], sd["linear4.bias"])))
+    w = r(torch.exp(F.linear(w, W[5]))) * mask.unsqueeze(-1)
+    w = w / (w.sum(dim=1, keepdim=True) + 1e-10)
+    return (x * w).sum(dim=1)
+
+
+def latent_attention_train_bf16(sd, emb, mask, heads=8):
+    """BF16 NUMERICS MODEL (not the reference) of the latent bf16 step
+    (csrc/latent_train.hip): the K/V fold A_h = K_h Wq_h / sqrt(512), Bt_h^T =
+    V_h Wo_h^T from bf16 LN_c(latents) and bf16 weights; per slot S, X = LN_q(E[hist]),
+    P = softmax64(X A^T), H1 = P Bt^T + S, Y = LN_f(H1), G = Y W1^T + b1 stored bf16;
+    per batch row m = bf16(mean GEGLU(G)) W2^T + b2 + mean(H1) (f32), u = normalize(m).
+    Same math as latent_attention.py:134-171 (the last layer commuted with the mean)."""
+    r = _BF16.apply
+    p, q_ = "cross_attend_blocks.0.", "cross_attend_blocks.1."
+    d = emb.shape[-1]
+    latn = r(F.layer_norm(sd["latents"], (d,), sd[p + "norm_context.weight"], sd[p + "norm_context.bias"], 1e-5))
+    kv = r(F.linear(latn, _bf16_weight(sd[p + "fn.to_kv.weight"])))          # [64, 8192]
+    k, v = kv.chunk(2, dim=-1)                                                 # [64, 4096] each
+    wq, wo = _bf16_weight(sd[p + "fn.to_q.weight"]), _bf16_weight(sd[p + "fn.to_out.weight"])
+    dh = k.shape[1] // heads
+    A = r(torch.cat([k[:, h * dh:(h + 1) * dh] @ wq[h * dh:(h + 1) * dh] for h in range(heads)]) / math.sqrt(dh))
+    BtT = r(torch.cat([v[:, h * dh:(h + 1) * dh] @ wo[:, h * dh:(h + 1) * dh].T for h in range(heads)]))  # [512, 1024]
+    m = mask.bool()
+    e = emb[m]                                                                 # [Hs, d] valid slots, CSR order
+    S = r(e)
+    X = r(F.layer_norm(e, (d,), sd[p + "norm.weight"], sd[p + "norm.bias"], 1e-5))
+    Pm = r(torch.softmax((X @ A.T).reshape(-1, heads, 64), dim=-1).reshape(-1, heads * 64))
+    H1 = r(Pm @ BtT + S)
+    Y = r(F.layer_norm(H1, (d,), sd[q_ + "norm.weight"], sd[q_ + "norm.bias"], 1e-5))
+    G = r(F.linear(Y, _bf16_weight(sd[q_ + "fn.net.0.weight"]), sd[q_ + "fn.net.0.bias"]))
+    a, g = G.chunk(2, dim=-1)
+    Z = a * F.gelu(g)
+    lens = m.sum(dim=1)
+    seg = torch.repeat_interleave(torch.arange(len(lens)), lens)
+    zbar = r(torch.zeros((len(lens), Z.shape[1])).index_add(0, seg, Z) / lens[:, None])
+    h1bar = torch.zeros((len(lens), d)).index_add(0, seg, H1) / lens[:, None]
+    out = F.linear(zbar, _bf16_weight(sd[q_ + "fn.net.2.weight"]), sd[q_ + "fn.net.2.bias"]) + h1bar
+    return F.normalize(out, p=2, dim=-1)
+
+
+def _loss(P, tok_last, hist_groups, pos, neg, p, seeds, ln_eps, margin, pooler="final", numerics="f32"):
     E = F.layer_norm(tok_last.float(), (tok_last.shape[1],), P["ln.weight"], P["ln.bias"], ln_eps)
     B = len(hist_groups)
     L = max(len(h) for h in hist_groups)
@@ -80,8 +187,13 @@ def _loss(P, tok_last, hist_groups, pos, neg, p, seeds, ln_eps, margin, pooler="
     second = E[idx] * mask.unsqueeze(-1)
     if pooler == "latent":  # LatentAttentionModel in FinalAttention's slot (no dropout in that module)
         from oracle import pool_ref
-        out = pool_ref.latent_attention_forward({k[7:]: v for k, v in P.items() if k.startswith("latent.")},
-                                                second, mask)
+        lsd = {k[7:]: v for k, v in P.items() if k.startswith("latent.")}
+        out = (latent_attention_train_bf16(lsd, second, mask) if numerics == "bf16" else
+               pool_ref.latent_attention_forward(lsd, second, mask))
+    elif numerics == "bf16":
+        out = final_attention_train_bf16(P, second, mask)
+    elif numerics == "bf16x3":
+        out = final_attention_train_bf16x3(P, second, mask)
     else:
         out = final_attention_train(P, second, mask, seeds, p, slot_rows)
     pn = torch.as_tensor(np.concatenate([pos, neg]).astype(np.int64))
@@ -132,12 +244,14 @@ def train_epoch(params: dict, batches, *, lr=1e-6, max_norm=0.5, weight_decay=0.
 
 
 def train_steps(params: dict, batches, *, pooler="final", lr=1e-6, max_norm=0.5, weight_decay=0.01, ln_eps=1e-12,
-                margin=2.0):
+                margin=2.0, numerics="f32"):
     """The train_one_epoch loop (trainer.py:1044-1069: zero_grad, forward, loss,
     backward, clip_grad_norm_, AdamW.step with ONE persistent optimizer) over
     `batches` = list of (tok_last, hist_groups, pos, neg), dropout off, with
     FinalAttention (params "ln.*", "linear*") or the latent pooler (params
-    "ln.*", "latent.<LatentAttentionModel name>").  Returns (per-step losses,
+    "ln.*", "latent.<LatentAttentionModel name>").  numerics="bf16" (FinalAttention
+    only): the bf16 numerics model above instead of f32 -- the drift an ideal bf16
+    implementation shows against the f32 loop.  Returns (per-step losses,
     per-step clipped-grad total norms, params after)."""
     P = _leaf(params)
     plist = list(P.values())
@@ -145,7 +259,7 @@ def train_steps(params: dict, batches, *, pooler="final", lr=1e-6, max_norm=0.5,
     losses, norms = [], []
     for tok_last, groups, pos, neg in batches:
         opt.zero_grad()
-        loss = _loss(P, tok_last, groups, pos, neg, 0.0, (0, 0, 0), ln_eps, margin, pooler)
+        loss = _loss(P, tok_last, groups, pos, neg, 0.0, (0, 0, 0), ln_eps, margin, pooler, numerics)
         loss.backward()
         norms.append(float(torch.nn.utils.clip_grad_norm_(plist, max_norm=max_norm)))
         opt.step()

@@ -1,5 +1,5 @@
 """Config 5 in bf16 (BASELINE configs[4]: "bf16 MFMA backward") held to the f32
-ORACLE over many steps, not to the HIP f32 path (VERDICT r3 #1).
+ORACLE over many steps, not to the HIP f32 path (VERDICT r3 #1, r4 #1).
 
 Both config-5 engines (FinalAttentionTrainStep, LatentAttentionTrainStep) run
 22 bf16 steps -- two epochs of the reference trainer's golden batching
@@ -10,20 +10,28 @@ the CPU (FinalAttention: pinned to the reference's own step and epoch golden in
 test_train.py; latent: torch autograd of the reference module's forward,
 pool_ref.latent_attention_forward, pinned to the reference golden).
 
-Bounds, at the reference's lr = 1e-6 and at a 100x lr (1e-4)
-that makes the parameters actually move, so bf16 drift accumulates:
-  per-step loss    |l_bf16 - l_oracle| <= loss_rel * |l_oracle| at every step
-  update           per parameter tensor, d = p_22 - p_0 (the trained change):
-                   cos(d_bf16, d_oracle) >= upd_cos and
-                   ||d_bf16 - d_oracle|| <= upd_rel * ||d_oracle||   (BOUNDS)
-  trained model    (lr 1e-6) eval AUC of the bf16-trained pooler vs the
-                   oracle-trained pooler (oracle eval) on 20,000 held-out
-                   impressions over 4,096 held-out news, clicks ~ logistic of
-                   the oracle score: through the f32 HIP eval path equal to 4
-                   decimal places (|dAUC| < 5e-5: what bf16 TRAINING moves);
-                   through the bf16 eval path within 1e-4 (bf16 inference adds
-                   its own rounding of the table and users, gated at full size
-                   by tests/test_auc_gate.py)
+Where the bounds come from (no number here is fitted to a box).  The same 22
+steps also run through the oracle's BF16 NUMERICS MODEL
+(train_ref.train_steps(numerics="bf16"): the reference math with the HIP step's
+rounding points -- bf16 weights, every stored activation and its gradient
+rounded to nearest-even bf16, f32 sums).  Its drift from the f32 loop is what
+ideal bf16 arithmetic costs on these batches, and it is large for
+FinalAttention: the linear4 gradient is ill-conditioned against the FORWARD's
+rounding (a CPU ablation of the rounding points, DESIGN.md §4: bf16 gradients
+add nothing, an exact forward with a bf16 backward brings every gradient to
+<= 0.3 %, keeping only the w-branch in f32 does not help).  So the HIP bf16 step
+is held to the model, per parameter tensor, d = p_22 - p_0 (the trained change):
+  update     ||d_hip - d_f32|| / ||d_f32||  <=  1.25 * (the model's) + 0.01
+             1 - cos(d_hip, d_f32)          <=  1.5 * (the model's) + 2e-3
+  loss       |l_hip - l_f32| <= 2 * (the model's max over the steps) + 1e-5 |l_f32|, every step
+  (margins: two bf16 realisations of the same arithmetic, summed in different
+  orders, differ by a few % of their drift; 25-50 % slack and the absolute
+  floors keep the check about the level, not the noise)
+and, at the reference's lr = 1e-6, the trained model itself: the bf16-trained
+pooler against the oracle-trained one (oracle eval) on 200,000 held-out
+impressions over 8,192 held-out news, clicks ~ logistic of the oracle score,
+through the f32 AND the bf16 HIP eval paths: |dAUC| < 5e-5 (AUC equal to 4
+decimal places, the north star's contract).
 """
 import os
 
@@ -34,13 +42,26 @@ import torch
 from news_recommendation_project_v2_amd import weights as W
 
 STEPS_EPOCHS = 2
-# (pooler, lr) -> (max per-step loss rel err, min update cosine, max update rel err); measured on
-# the box (round 4): final 4.2e-5 / 0.992 / 0.125 at 1e-6 and 5.3e-4 / 0.968 / 0.254 at 1e-4,
-# latent 6.6e-5 / 0.9999 / 0.017 and 7.7e-5 / 0.9999 / 0.015 (profiles/round4/drift.log)
-BOUNDS = {("final", 1e-6): (1e-3, 0.98, 0.2), ("final", 1e-4): (2e-3, 0.95, 0.35),
-          ("latent", 1e-6): (1e-3, 0.999, 0.05), ("latent", 1e-4): (2e-3, 0.999, 0.05)}
-AUC_BF16_EVAL = 1e-4  # the bf16 eval path's own shift on this 20k-impression set (see below)
-AUC_4DP = 5e-5
+LRS = (1e-6, 1e-4)          # the reference's lr, and 100x (the parameters move: drift accumulates)
+UPD_REL = (1.25, 0.01)      # HIP update rel err <= a * model + b
+UPD_COS = (1.5, 2e-3)       # 1 - HIP update cosine <= a * (1 - model cosine) + b
+LOSS = (2.0, 1e-5)          # per-step |l_hip - l_f32| <= a * model max + b |l_f32|
+AUC_4DP = 5e-5              # |dAUC| < half a unit in the 4th decimal
+HELD_NEWS, HELD_IMPS = 8192, 200_000
+
+
+_MODEL = {}
+
+
+def _model_drift(pooler, lr, obatches):
+    """(f32 losses, f32 params, bf16-model losses, bf16-model params) of the 22 steps (cached)."""
+    from oracle import train_ref
+    key = (pooler, lr)
+    if key not in _MODEL:
+        l32, _, p32 = train_ref.train_steps(_params(pooler), obatches, pooler=pooler, lr=lr)
+        l16, _, p16 = train_ref.train_steps(_params(pooler), obatches, pooler=pooler, lr=lr, numerics="bf16")
+        _MODEL[key] = (l32, p32, l16, p16)
+    return _MODEL[key]
 
 
 def _params(pooler):
@@ -87,14 +108,14 @@ def _scores_gpu(pooler, sd, E, imps, dev, dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.timeout(900)
-@pytest.mark.parametrize("lr", [1e-6, 1e-4])
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("lr", LRS)
 @pytest.mark.parametrize("pooler", ["final", "latent"])
 def test_bf16_training_tracks_f32_oracle(gpu_device, tmp_path, pooler, lr):
     import torch.nn.functional as F
     from test_train import _dataset, _device_batch, _oracle_batch, _setup
     from news_recommendation_project_v2_amd import evaluation, synthetic
-    from oracle import data_ref, pool_ref, train_ref
+    from oracle import data_ref, pool_ref
     torch.set_num_threads(min(16, os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS") or 16)))
     g, states, labels = _setup()
     ds = _dataset(g, labels)
@@ -108,30 +129,40 @@ def test_bf16_training_tracks_f32_oracle(gpu_device, tmp_path, pooler, lr):
     p_gpu = {k: v.detach().cpu().clone() for k, v in eng.views.items()}
 
     obatches = [_oracle_batch(ds, states, lo, hi)[:4] for lo, hi in ranges]
-    ref_losses, _, p_ref = train_ref.train_steps(_params(pooler), obatches, pooler=pooler, lr=lr)
-    assert set(p_ref) == set(p_gpu)
+    ref_losses, p_ref, mod_losses, p_mod = _model_drift(pooler, lr, obatches)
+    assert set(p_ref) == set(p_gpu) == set(p_mod)
 
-    loss_rel, upd_cos, upd_rel = BOUNDS[(pooler, lr)]
-    rel = [abs(a - b) / abs(b) for a, b in zip(losses, ref_losses)]
-    print(f"\n[bf16 drift] {pooler} lr={lr:g}: steps {len(losses)}, loss rel err max {max(rel):.2e} "
-          f"(first {rel[0]:.2e}, last {rel[-1]:.2e}); loss {ref_losses[0]:.5f} -> {ref_losses[-1]:.5f}")
-    assert max(rel) <= loss_rel, (pooler, lr, rel)
-    worst_cos, worst_rel = 1.0, 0.0
-    for k in p_ref:
-        d_ref = p_ref[k] - p0[k]
-        d_gpu = p_gpu[k] - p0[k]
-        c = _cos(d_gpu, d_ref)
-        r = float((d_gpu - d_ref).double().norm() / (d_ref.double().norm() + 1e-300))
-        worst_cos, worst_rel = min(worst_cos, c), max(worst_rel, r)
-        assert c >= upd_cos and r <= upd_rel, (pooler, lr, k, c, r)
-    print(f"[bf16 drift] {pooler} lr={lr:g}: update cosine min {worst_cos:.4f}, update rel err max {worst_rel:.3f}")
-    if lr != 1e-6:
+    hip_l = [abs(a - b) for a, b in zip(losses, ref_losses)]
+    mod_l = max(abs(a - b) for a, b in zip(mod_losses, ref_losses))
+    print(f"\n[bf16 drift] {pooler} lr={lr:g}: steps {len(losses)}, |loss - f32| max {max(hip_l):.2e} "
+          f"(bf16 model {mod_l:.2e}); loss {ref_losses[0]:.5f} -> {ref_losses[-1]:.5f}")
+    for a, b in zip(hip_l, ref_losses):
+        assert a <= LOSS[0] * mod_l + LOSS[1] * abs(b), (pooler, lr, a, mod_l)
+
+    def drift(p):
+        out = {}
+        for k in p_ref:
+            d_ref, d = p_ref[k] - p0[k], p[k] - p0[k]
+            out[k] = (_cos(d, d_ref), float((d - d_ref).double().norm() / (d_ref.double().norm() + 1e-300)))
+        return out
+
+    hip, mod = drift(p_gpu), drift(p_mod)
+    for k in sorted(hip, key=lambda k: hip[k][0]):
+        print(f"[bf16 drift] {pooler} lr={lr:g}   {k:58s} update cosine {hip[k][0]:.5f} (model {mod[k][0]:.5f})"
+              f"  rel err {hip[k][1]:.4f} (model {mod[k][1]:.4f})")
+    worst = min(hip, key=lambda k: hip[k][0])
+    print(f"[bf16 drift] {pooler} lr={lr:g}: worst tensor {worst}: update cosine {hip[worst][0]:.4f} "
+          f"(bf16 model {mod[worst][0]:.4f}), rel err {hip[worst][1]:.3f} (model {mod[worst][1]:.3f})")
+    for k in hip:
+        assert hip[k][1] <= UPD_REL[0] * mod[k][1] + UPD_REL[1], (pooler, lr, k, hip[k], mod[k])
+        assert 1 - hip[k][0] <= UPD_COS[0] * (1 - mod[k][0]) + UPD_COS[1], (pooler, lr, k, hip[k], mod[k])
+    if lr != LRS[0]:
         return
 
     # the trained poolers on held-out impressions, clicks ~ logistic of the oracle score
-    n_news, n_imp = 4096, 20000
-    tok = torch.stack([W.normal_tensor(97, f"heldout_tok_{i}", (1024,)) * 2.0 + 0.3 for i in range(n_news)]).half()
-    imps = synthetic.mind_impressions(n_news, n_imp, seed=21)
+    tok = torch.stack([W.normal_tensor(97, f"heldout_tok_{i}", (1024,)) * 2.0 + 0.3
+                       for i in range(HELD_NEWS)]).half()
+    imps = synthetic.mind_impressions(HELD_NEWS, HELD_IMPS, seed=21)
     E_ref = F.layer_norm(tok.float(), (1024,), p_ref["ln.weight"], p_ref["ln.bias"], 1e-12)
     strip = (lambda d: {k: v for k, v in d.items() if not k.startswith("ln.")}) if pooler == "final" else \
         (lambda d: {k[7:]: v for k, v in d.items() if k.startswith("latent.")})
@@ -143,11 +174,11 @@ def test_bf16_training_tracks_f32_oracle(gpu_device, tmp_path, pooler, lr):
     E_gpu = ops.gather_layernorm(tok.to(gpu_device), None, eng.views["ln.weight"].view(1, 1024),
                                  eng.views["ln.bias"].view(1, 1024), 1e-12)
     sd_gpu = {k: v.to(gpu_device) for k, v in strip(p_gpu).items()}
+    assert auc_ref > 0.7
     for dt in (torch.float32, torch.bfloat16):
-        e, s = _scores_gpu(pooler, sd_gpu, E_gpu, imps, gpu_device, dt)
-        auc = evaluation.score_device(e.rank(s), lab, imps.cand_off())["auc"]
-        print(f"[bf16 drift] {pooler}: held-out AUC oracle-trained (oracle eval) {auc_ref:.6f}, bf16-trained "
-              f"({'bf16' if dt == torch.bfloat16 else 'f32'} HIP eval) {auc:.6f}, |d| {abs(auc - auc_ref):.2e}")
-        assert auc_ref > 0.7
-        tol = AUC_4DP if dt == torch.float32 else AUC_BF16_EVAL
-        assert abs(auc - auc_ref) < tol, (pooler, dt, auc, auc_ref)
+        e, s_ = _scores_gpu(pooler, sd_gpu, E_gpu, imps, gpu_device, dt)
+        auc = evaluation.score_device(e.rank(s_), lab, imps.cand_off())["auc"]
+        print(f"[bf16 drift] {pooler}: held-out AUC ({HELD_IMPS} impressions) oracle-trained (oracle eval) "
+              f"{auc_ref:.7f}, bf16-trained ({'bf16' if dt == torch.bfloat16 else 'f32'} HIP eval) {auc:.7f}, "
+              f"|d| {abs(auc - auc_ref):.2e}")
+        assert abs(auc - auc_ref) < AUC_4DP, (pooler, dt, auc, auc_ref)

@@ -44,6 +44,20 @@ for step in "$@"; do
           python tools/train_bench.py --pooler $p --dtype bf16 --steps 10 > "$OUT/train_${p}_prof.json" 2> "$OUT/train_${p}_prof.err" )
         rc=$?; echo "trainprof $p rc=$rc" >> "$OUT/status.txt"; [ $rc -eq 0 ] || exit $rc
       done ;;
+    drifttest)
+      timeout -k 10 1500 python -u -m pytest -v --timeout 1400 --timeout-method thread -m gpu -s \
+        tests/test_train_bf16_drift.py > "$OUT/pytest_drift.log" 2>&1
+      rc=$?; echo "drifttest rc=$rc" >> "$OUT/status.txt"; ok $rc || exit $rc ;;
+    traintests)
+      timeout -k 10 600 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_train.py tests/test_gemm_tn.py tests/test_latent_attention_autograd.py > "$OUT/pytest_train.log" 2>&1
+      rc=$?; echo "traintests rc=$rc" >> "$OUT/status.txt"; ok $rc || exit $rc ;;
+    trainpmc)
+      ( cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && \
+        timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
+        --kernel-include-regex gemm256 -d "$OUT/pmc_train_final" -o pmc --output-format csv -- \
+        python tools/train_bench.py --pooler final --dtype bf16 --steps 4 > "$OUT/pmc_train_final.log" 2>&1 )
+      rc=$?; echo "trainpmc rc=$rc" >> "$OUT/status.txt"; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $step" >> "$OUT/status.txt"; exit 2 ;;
   esac
 done
