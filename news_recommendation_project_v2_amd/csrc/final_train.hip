@@ -160,7 +160,8 @@ __global__ __launch_bounds__(256) void w1_fold_kernel(const TA* __restrict__ W1,
     part[(int64_t)blockIdx.y * 2 * D + w * D + c] = v;
   }
 }
-// dg[c] += sum_k part[k][0][c], db[c] += sum_k part[k][1][c]: 64 columns x 4 chunk groups per block
+// dg[c] = sum_k part[k][0][c], db[c] = sum_k part[k][1][c] over the W1 fold's and the
+// pairs' chunks: 64 columns x 4 chunk groups per block
 __global__ __launch_bounds__(256) void ln_reduce_kernel(int nchunk, const float* __restrict__ part,
                                                         float* __restrict__ dg, float* __restrict__ db,
                                                         float* __restrict__ sqp) {
@@ -176,8 +177,8 @@ __global__ __launch_bounds__(256) void ln_reduce_kernel(int nchunk, const float*
   red[1][grp][cl] = sb;
   __syncthreads();
   if (threadIdx.x < 64) {
-    const float vg = dg[c] + ((red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]));
-    const float vb = db[c] + ((red[1][0][cl] + red[1][1][cl]) + (red[1][2][cl] + red[1][3][cl]));
+    const float vg = (red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]);
+    const float vb = (red[1][0][cl] + red[1][1][cl]) + (red[1][2][cl] + red[1][3][cl]);
     dg[c] = vg;
     db[c] = vb;
     if (sqp) {
@@ -193,16 +194,14 @@ __global__ __launch_bounds__(256) void ln_reduce_kernel(int nchunk, const float*
 // clip_grad_norm_ reads it, trainer.py:1067-1070).  One block.
 __global__ __launch_bounds__(256) void sq_total_kernel(int64_t n, const float* __restrict__ part,
                                                        float* __restrict__ out) {
-  __shared__ float red[256];
+  __shared__ float red[4];
   float s = 0.f;
   for (int64_t i = threadIdx.x; i < n; i += 256) s += part[i];
-  red[threadIdx.x] = s;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int k = 0; k < 256; ++k) t += red[k];
-    *out = t;
-  }
+  if (threadIdx.x == 0) *out = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // F.cosine_similarity(u, E[pos / neg]) with the per-vector 1e-8 clamp and
@@ -269,20 +268,24 @@ __global__ __launch_bounds__(256) void cos_pairs_kernel(int64_t B, const float* 
   }
 }
 
-// The pairs' part of the token LN parameter grads (dgamma = sum g o xhat, dbeta =
-// sum g over the 2B pair rows; SET, the W1 fold adds the history's part), and,
-// by block 0, the loss as the ordered sum of the per-row terms.  Block = 64
-// columns x 4 row groups.
+// The pairs' part of the token LN parameter grads: chunk k of the 2B pair rows
+// (rows k, k + kPairChunks, ...) -> partials part[k][0][c] = sum g o xhat,
+// part[k][1][c] = sum g, in the layout of the W1 fold's chunk partials (placed
+// after them, ln_reduce_kernel sums both).  Block = 64 columns x 4 row groups;
+// grid (D / 64, kPairChunks).  Block (0, 0)'s first wave also writes the loss as
+// the ordered (fixed tree) sum of the per-row terms.
+constexpr int kPairChunks = 8;
 __global__ __launch_bounds__(256) void pair_ln_kernel(int64_t B, const float* __restrict__ gpair,
                                                       const float* __restrict__ xh, const int32_t* __restrict__ pos,
                                                       const int32_t* __restrict__ neg, const float* __restrict__ lrow,
-                                                      float* __restrict__ dg, float* __restrict__ db,
-                                                      float* __restrict__ loss) {
+                                                      float* __restrict__ part, float* __restrict__ loss) {
   __shared__ float red[2][4][64];
   const int grp = threadIdx.x >> 6, cl = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * 64 + cl;
+  const int64_t step = (int64_t)kPairChunks * 4;
   float sg = 0.f, sb = 0.f;
-  for (int64_t r = grp; r < 2 * B; r += 4) {
+#pragma unroll 4
+  for (int64_t r = (int64_t)blockIdx.y + kPairChunks * grp; r < 2 * B; r += step) {
     const int64_t news = r < B ? pos[r] : neg[r - B];
     const float gv = gpair[r * D + c];
     sg = fmaf(gv, xh[news * D + c], sg);
@@ -292,13 +295,15 @@ __global__ __launch_bounds__(256) void pair_ln_kernel(int64_t B, const float* __
   red[1][grp][cl] = sb;
   __syncthreads();
   if (threadIdx.x < 64) {
-    dg[c] = (red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]);
-    db[c] = (red[1][0][cl] + red[1][1][cl]) + (red[1][2][cl] + red[1][3][cl]);
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float l = 0.f;
-    for (int64_t r = 0; r < B; ++r) l += lrow[r];
-    *loss = l;
+    part[(int64_t)blockIdx.y * 2 * D + c] = (red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]);
+    part[(int64_t)blockIdx.y * 2 * D + D + c] = (red[1][0][cl] + red[1][1][cl]) + (red[1][2][cl] + red[1][3][cl]);
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+      float l = 0.f;
+      for (int64_t r = threadIdx.x; r < B; r += 64) l += lrow[r];
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) l += __shfl_xor(l, o, 64);
+      if (threadIdx.x == 0) *loss = l;
+    }
   }
 }
 
@@ -414,7 +419,7 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs, int ncu) {
   L.lrow = take(Bp * 4);
   L.sqp = take(kSqParts * 4);
   L.dXp = take(Hp * D * es); L.dL = take(Hp * D * es); L.dY = take(Hp * H * es); L.dX = take(Hp * D * es);
-  L.dZ2 = take(Hp * H * es); L.dZ1 = take(Hp * H * es); L.w1p = take((H / 64) * 2 * D * 4);
+  L.dZ2 = take(Hp * H * es); L.dZ1 = take(Hp * H * es); L.w1p = take((H / 64 + kPairChunks) * 2 * D * 4);
   L.W1t = take(D * H * es); L.W2t = take(H * H * es); L.W3t = take(H * D * es); L.W4t = take(D * H * es);
   L.W5t = take(H * D * es);
   if (dtype == NR_BF16) {
@@ -531,9 +536,9 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   hipLaunchKernelGGL(cos_pairs_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, users, E, a.pos, a.neg,
                      a.margin, lrow, du, gpair);
   NR_CHECK_LAUNCH("nr_final_train_step (cosine)");
-  // the pairs' token LN grads (set) and the loss, ahead of the W1 fold that adds the history's
-  hipLaunchKernelGGL(pair_ln_kernel, dim3((unsigned)(D / 64)), dim3(256), 0, st, B, gpair, XHu, a.pos, a.neg, lrow,
-                     a.g_tok_g, a.g_tok_b, a.loss);
+  // the pairs' token LN grad partials (after the W1 fold's chunks) and the loss
+  hipLaunchKernelGGL(pair_ln_kernel, dim3((unsigned)(D / 64), kPairChunks), dim3(256), 0, st, B, gpair, XHu, a.pos,
+                     a.neg, lrow, (float*)P_(L.w1p) + (H / 64) * 2 * D, a.loss);
   NR_CHECK_LAUNCH("nr_final_train_step (pair LN grads)");
   NR_FT(nr_final_pool_bwd(dt, B, a.hist_off, Hp, XP, 2 * D, users, z, du, dXp, D, dL, D, st));
   // ---- data-grad chain (weights transposed on the side stream)
@@ -615,14 +620,15 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
     NR_FT(gemm_group_dispatch(dt, NR_F32, p, 5, st));
   }
   // ---- token LayerNorm parameter grads: the history gather's part folded with dW1
-  // (w1_fold_kernel; dW1 = gamma o M + g_b1 (x) beta), added to the pairs' part
+  // (w1_fold_kernel; dW1 = gamma o M + g_b1 (x) beta), summed with the pairs' part
   {
     float* w1p = (float*)P_(L.w1p);
     float* sqp = BF && a.sumsq ? (float*)P_(L.sqp) : nullptr;
     hipLaunchKernelGGL((w1_fold_kernel<TA>), dim3((unsigned)(D / 64), (unsigned)(H / 64)), dim3(256), 0, st, W1,
                        a.g_W1, a.g_b1, a.tok_g, a.tok_b, w1p, sqp ? sqp + kSqTn : nullptr);
     NR_CHECK_LAUNCH("nr_final_train_step (W1 fold)");
-    hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)(D / 64)), dim3(256), 0, st, (int)(H / 64), w1p, a.g_tok_g,
+    hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)(D / 64)), dim3(256), 0, st, (int)(H / 64) + kPairChunks, w1p,
+                       a.g_tok_g,
                        a.g_tok_b, sqp ? sqp + kSqTn + kSqFold + kSqBias : nullptr);
     NR_CHECK_LAUNCH("nr_final_train_step (token LN grads)");
     if (sqp) {

@@ -925,15 +925,17 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs) {
   int64_t o = 0;
   auto take = [&](int64_t bytes) { const int64_t r = o; o += al(bytes); return r; };
   L.E = take(U * D * 4);
-  L.Sx = take(Hp * D * es); L.X = take(Hp * D * es); L.P = take(Hp * S * es); L.H1 = take(Hp * D * es);
+  // X, P, dH1, dS hold Hpp rows: the dA / dBt K-slices read them directly (bf16: TN
+  // weight-grad GEMMs), rows [Hp, Hpp) zeroed by the step
+  L.Sx = take(Hp * D * es); L.X = take(Hpp * D * es); L.P = take(Hpp * S * es); L.H1 = take(Hp * D * es);
   L.Y = take(Hp * D * es); L.G = take(Hp * 2 * F * es);
   L.zbar = take(Bp * F * es); L.h1bar = take(Bp * D * 4); L.row_seg = take(Hp * 4);
   L.hparts = take((int64_t)kHParts * Bp * D * 4); L.hsum = take(Bp * D * 4);
   L.dmA = take(Bp * D * es); L.dmc = take(Bp * D * es); L.dmc32 = take(Bp * D * 4); L.dZ = take((int64_t)kZParts * Bp * F * 4);
   L.dZs = take(Bp * F * 4);
   L.gpart = take((Hp + kGRows - 1) / kGRows * 2 * F * 4);
-  L.dG = take(Hp * 2 * F * es); L.dY = take(Hp * D * es); L.dH1 = take(Hp * D * es);
-  L.dP = take(Hp * S * es); L.dS = take(Hp * S * es); L.dX = take(Hp * D * es); L.dE = take(U * D * 4);
+  L.dG = take(Hp * 2 * F * es); L.dY = take(Hp * D * es); L.dH1 = take(Hpp * D * es);
+  L.dP = take(Hp * S * es); L.dS = take(Hpp * S * es); L.dX = take(Hp * D * es); L.dE = take(U * D * 4);
   L.dGT = take(2 * F * Hp * es); L.YT = take(D * Hp * es); L.dH1T = take(D * Hpp * es); L.PT = take(S * Hpp * es);
   L.dST = take(S * Hpp * es); L.XT = take(D * Hpp * es); L.dmT = take(D * Bp * es); L.zbarT = take(F * Bp * es);
   L.WqT = take(D * F * es); L.W1T = take(D * 2 * F * es); L.W2T = take(F * D * es); L.WoT = take(F * D * es);
@@ -1011,7 +1013,13 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     const int64_t zn[] = {D, D, D, D, D, D, D, D, D, 2 * F, 1};
     for (int i = 0; i < 11; ++i) { z.p[i] = zp[i]; z.len[i] = zn[i]; }
     z.p[11] = dE; z.len[11] = U * D;
-    z.n = 12;
+    // rows [Hp, Hpp) of the dA / dBt operands (read as the K-slices' zero tail)
+    const int64_t tail = (Hpp - Hp) * L.es / 4;  // in f32 words (Hpp - Hp is a multiple of 64 rows)
+    z.p[12] = (float*)(X + Hp * D); z.len[12] = tail * D;
+    z.p[13] = (float*)(Pm + Hp * S); z.len[13] = tail * S;
+    z.p[14] = (float*)(dH1 + Hp * D); z.len[14] = tail * D;
+    z.p[15] = (float*)(dS + Hp * S); z.len[15] = tail * S;
+    z.n = 16;
     hipLaunchKernelGGL(zero_kernel, dim3(1024), dim3(256), 0, st, z);
     NR_LT_CHECK("zero");
   }
@@ -1118,7 +1126,14 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     set_error("nr_latent_train_step: fork failed");
     return NR_ERR_HIP;
   }
-  {
+  if constexpr (sizeof(TA) == 2) {
+    // bf16: the weight grads read dG, Y, dm, zbar row-major (TN grouped GEMM, no transposes)
+    GemmProblem p[2] = {
+        {2 * F, D, Hp, dG, 2 * F, 0, Y, D, 0, a.g_W1, D, 0, 1, 1.0f},
+        {D, F, Bp, dmA, D, 0, zbar, F, 0, a.g_W2, F, 0, 1, 1.0f},
+    };
+    if ((rc = gemm_group_tn_dispatch(NR_F32, p, 2, side.s))) return rc;
+  } else {
     TList t;
     t.add(dG, 2 * F, dGT, Hp, Hp, 2 * F, true);
     t.add(Y, D, YT, Hp, Hp, D, true);
@@ -1130,6 +1145,8 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
         {D, F, Bp, dmT, Bp, 0, zbarT, Bp, 0, a.g_W2, F, 0, 1, 1.0f},
     };
     if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, side.s))) return rc;
+  }
+  {
     if (hipEventRecord(side.join, side.s) != hipSuccess) {
       set_error("nr_latent_train_step: join record failed");
       return NR_ERR_HIP;
@@ -1170,7 +1187,15 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   hipStream_t s2 = side.s2;
   // ---- dA = dS^T X and dBt = dH1^T P as kWParts K-slices (16 + 16 tiles alone would hold 32 CUs
   // for a K = Hp tile time), summed while converting to the fold backward's operands
-  {
+  if constexpr (sizeof(TA) == 2) {
+    // bf16: K-slices of the row-major dS / X / dH1 / P (TN grouped GEMM; rows past Hp are zero)
+    const int64_t kw = L.kw;
+    GemmProblem p[2] = {
+        {S, D, kw, dS, S, kw * S, X, D, kw * D, gA, D, (int64_t)S * D, kWParts, 1.0f},
+        {D, S, kw, dH1, D, kw * D, Pm, S, kw * S, gBt, S, (int64_t)D * S, kWParts, 1.0f},
+    };
+    if ((rc = gemm_group_tn_dispatch(NR_F32, p, 2, s2))) return rc;
+  } else {
     TList t;
     t.add(dH1, D, dH1T, Hpp, Hp, D, true, Hpp);
     t.add(Pm, S, PT, Hpp, Hp, S, true, Hpp);
