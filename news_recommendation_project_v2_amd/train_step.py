@@ -77,6 +77,14 @@ class TrainBatch:
         return self.pos.numel()
 
 
+def _check_loss_out(t: torch.Tensor, dev) -> torch.Tensor:
+    d = torch.device(dev)
+    if (t.dtype != torch.float32 or t.numel() < 1 or not t.is_contiguous() or t.device.type != d.type
+            or (d.index is not None and t.device.index != d.index)):
+        raise NewsRecHIPError("loss_out must be a contiguous float32 tensor with >= 1 element on the step's device")
+    return t
+
+
 def _refresh_mirror(step) -> None:
     """Rewrite a step's bf16 weight mirror when its master weights changed outside
     AdamW (load_state_dict on the wrapped modules, an edit through ``views``): the
@@ -214,9 +222,9 @@ class FinalAttentionTrainStep:
         return (self.seed * 1_000_003 + self.step_count * 7919 + layer * 104_729) & (2**64 - 1)
 
     # ------------------------------------------------------------------ step
-    def forward_backward(self, batch: TrainBatch):
-        """Loss (device scalar) and gradients into ``self.grad`` (every slice
-        rewritten) as ONE library call (``nr_final_train_step``, csrc/final_train.hip):
+    def forward_backward(self, batch: TrainBatch, loss_out: torch.Tensor | None = None):
+        """Loss (device scalar, written to ``loss_out`` when given) and gradients
+        into ``self.grad`` (every slice rewritten) as ONE library call (``nr_final_train_step``, csrc/final_train.hip):
         the forward, the margin loss and the whole backward of the batch.
         Returns (loss, users, None): users = the pooled users [B, D] f32.  Both
         returned tensors are views of buffers the next call overwrites in place
@@ -246,11 +254,12 @@ class FinalAttentionTrainStep:
             src = self.cviews[name] if f.startswith("W") else self.views[name]
             setattr(a, f, src.data_ptr())
             setattr(a, "g_" + f, self.gviews[name].data_ptr())
-        a.loss, a.users, a.sumsq = self.loss.data_ptr(), self._users.data_ptr(), self.sumsq.data_ptr()
+        loss = self.loss if loss_out is None else _check_loss_out(loss_out, self.device)
+        a.loss, a.users, a.sumsq = loss.data_ptr(), self._users.data_ptr(), self.sumsq.data_ptr()
         _lib.check(lib.nr_final_train_step(ctypes.byref(a), self._ws_native.data_ptr(), self._ws_native.numel(),
                                            torch.cuda.current_stream(self.device).cuda_stream), "nr_final_train_step")
         self._keep = (tok, hi, ho, pos, neg)  # alive until the stream has run the step
-        return self.loss, self._users[:B], None
+        return loss, self._users[:B], None
 
     def _refresh_mirror(self) -> None:
         _refresh_mirror(self)
@@ -263,9 +272,10 @@ class FinalAttentionTrainStep:
                   self.max_norm, self.sumsq if self.max_norm > 0 else None, self.flat16)
 
     def step(self, batch: TrainBatch) -> torch.Tensor:
-        """One full step; returns this step's loss as its own device scalar."""
-        loss, _, _ = self.forward_backward(batch)
-        out = loss.clone()
+        """One full step; returns this step's loss as its own device scalar (a
+        fresh allocation the step writes, so no copy launch)."""
+        out = torch.empty(1, dtype=torch.float32, device=self.device)
+        self.forward_backward(batch, loss_out=out)
         self.optimizer_step()
         return out
 
@@ -361,9 +371,9 @@ class LatentAttentionTrainStep:
         if set(self._pmap.values()) != set(self.names):
             raise NewsRecHIPError(f"unexpected LatentAttentionModel parameters: {sorted(self.names)}")
 
-    def forward_backward(self, batch: TrainBatch):
-        """Loss (device scalar) and gradients into ``self.grad`` (every slice
-        rewritten).  Returns (loss, users, None): users = the normalized pooled
+    def forward_backward(self, batch: TrainBatch, loss_out: torch.Tensor | None = None):
+        """Loss (device scalar, written to ``loss_out`` when given) and gradients
+        into ``self.grad`` (every slice rewritten).  Returns (loss, users, None): users = the normalized pooled
         users [B, D].  Both are views of buffers the next call overwrites in
         place (on the stream); clone them to keep a step's values."""
         from . import _lib
@@ -388,14 +398,15 @@ class LatentAttentionTrainStep:
             src = self.cviews[name] if f in ("Wq", "Wkv", "Wo", "W1", "W2") else self.views[name]
             setattr(a, f, src.data_ptr())
             setattr(a, "g_" + f, self.gviews[name].data_ptr())
-        a.loss, a.users = self.loss.data_ptr(), self._users.data_ptr()
+        loss = self.loss if loss_out is None else _check_loss_out(loss_out, self.device)
+        a.loss, a.users = loss.data_ptr(), self._users.data_ptr()
         # (no grad.zero_(): the step writes every gradient and zeroes its own accumulators;
         # the flat buffer's alignment gaps were zeroed at construction and are never written)
         _lib.check(lib.nr_latent_train_step(ctypes.byref(a), self._ws.data_ptr(), self._ws.numel(),
                                             torch.cuda.current_stream(self.device).cuda_stream),
                    "nr_latent_train_step")
         self._keep = (tok, hi, ho, pos, neg)  # alive until the stream has run the step
-        return self.loss, self._users[:B], None
+        return loss, self._users[:B], None
 
     def optimizer_step(self) -> None:
         """clip_grad_norm_(max_norm) + AdamW, one launch each (trainer.py:1067-1069);
@@ -409,8 +420,8 @@ class LatentAttentionTrainStep:
             self.model._hip_cache = {}  # the eval path's folded weights are stale now
 
     def step(self, batch: TrainBatch) -> torch.Tensor:
-        loss, _, _ = self.forward_backward(batch)
-        out = loss.clone()
+        out = torch.empty(1, dtype=torch.float32, device=self.device)
+        self.forward_backward(batch, loss_out=out)
         self.optimizer_step()
         return out
 
