@@ -137,10 +137,12 @@ int nr_gemm(int dtype_in, int dtype_out, int epilogue, int64_t M, int64_t N, int
  * nr_gemm with the training-forward epilogue of FinalAttention
  * (modeling_utils.py:218-221: dropout(relu(linear(x))), p = 0.1 in train mode):
  *   C = relu(A·Wᵀ + bias) * keep(row, col) / (1 - p)
- * keep = drop_hash(seed, row * N + col) >= p * 2^32, drop_hash = the splitmix64
- * finaliser of seed + (idx + 1) * 0x9E3779B97F4A7C15, upper 32 bits (restated
- * in oracle/train_ref.py).  Replaces nn.Dropout's Philox stream: the masks are
- * a different (equally distributed) draw, reproducible from (seed, row, col).
+ * keep(idx = row * N + col) = field (idx & 3) of h >= round(p * 2^16), where h =
+ * the splitmix64 finaliser of seed + (idx / 4 + 1) * 0x9E3779B97F4A7C15 and
+ * field k = bits [16 k, 16 k + 16) (one hash per 4 consecutive elements;
+ * restated in oracle/train_ref.py).  Replaces nn.Dropout's Philox stream: the
+ * masks are a different (equally distributed; p quantised to 1/65536) draw,
+ * reproducible from (seed, row, col).
  */
 int nr_gemm_relu_dropout(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K, const void* A,
                          int64_t lda, const void* W, int64_t ldw, const float* bias, void* C, int64_t ldc,

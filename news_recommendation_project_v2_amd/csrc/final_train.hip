@@ -477,8 +477,7 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   TA* X = XP;           // [Hp][D] at row stride 2D
   TA* Pexp = XP + D;    // exp(logits), same stride
   const float scale = 1.0f / (1.0f - a.p);
-  const double tq = (double)a.p * 4294967296.0;
-  const uint32_t thr = tq >= 4294967295.0 ? 0xffffffffu : (uint32_t)tq;
+  const uint32_t thr = dropout_threshold(a.p);
   TrainSide side;
   NR_FT(train_side_streams(st, "nr_final_train_step", side));
 

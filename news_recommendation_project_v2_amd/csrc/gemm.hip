@@ -110,7 +110,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[2][2], int64_t
             float v = acc[mi][ni][reg] + b;
             if constexpr (EPI == NR_EPI_RELU) v = fmaxf(v, 0.f);
             if constexpr (EPI == NR_EPI_RELU_DROPOUT)
-              v = drop_hash(ea.seed, (uint64_t)(row * N + col)) < ea.thr ? 0.f : fmaxf(v, 0.f) * ea.scale;
+              v = drop_at(ea.seed, (uint64_t)(row * N + col), ea.thr) ? 0.f : fmaxf(v, 0.f) * ea.scale;
             if constexpr (EPI == NR_EPI_EXP) v = expf(v);
             if constexpr (EPI == NR_EPI_GELU) v = gelu_erf(v);
             if constexpr (EPI == NR_EPI_RESADD) v += from_out<TO>(R[row * ldr + col]);
@@ -326,7 +326,7 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
               if constexpr (EPI == NR_EPI_RELU) v = fmaxf(v, 0.f);
               if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
                 const uint64_t gi = (uint64_t)((m0 + wm * 128 + pass * 64 + lr) * N + wcol + 16 * ni + c16);
-                v = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(v, 0.f) * ea.scale;
+                v = drop_at(ea.seed, gi, ea.thr) ? 0.f : fmaxf(v, 0.f) * ea.scale;
               }
               if constexpr (EPI == NR_EPI_EXP) v = expf(v);
               if constexpr (EPI == NR_EPI_GELU) v = gelu_erf(v);
@@ -350,8 +350,8 @@ __device__ __forceinline__ void gemm256_store(const typename Acc256<MF16>::type&
           if constexpr (EPI == NR_EPI_RELU) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); }
           if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
             const uint64_t gi = (uint64_t)((m0 + wm * 128 + pass * 64 + lr) * N + wcol + cl);
-            v0 = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(v0, 0.f) * ea.scale;
-            v1 = drop_hash(ea.seed, gi + 32) < ea.thr ? 0.f : fmaxf(v1, 0.f) * ea.scale;
+            v0 = drop_at(ea.seed, gi, ea.thr) ? 0.f : fmaxf(v0, 0.f) * ea.scale;
+            v1 = drop_at(ea.seed, gi + 32, ea.thr) ? 0.f : fmaxf(v1, 0.f) * ea.scale;
           }
           if constexpr (EPI == NR_EPI_EXP) { v0 = expf(v0); v1 = expf(v1); }
           if constexpr (EPI == NR_EPI_GELU) { v0 = gelu_erf(v0); v1 = gelu_erf(v1); }
@@ -1377,17 +1377,19 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
             for (int r = 0; r < 4; ++r) acc[mi][ni][r] = pv[ni][r] * (acc[mi][ni][r] - dot);
         }
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
+        for (int ni = 0; ni < 4; ++ni) {
+          // the lane's 4 consecutive columns col0 + 16 ni + 4 q4 .. +3 are one group
+          // of the dropout stream: one hash for the four
+          uint64_t dh = 0;
+          if constexpr (EPI == NR_EPI_RELU_DROPOUT) dh = drop_hash4(ea.seed, (uint64_t)(row * N + col0 + 16 * ni + 4 * q4) >> 2);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float x = acc[mi][ni][r];
-            if constexpr (EPI == NR_EPI_RELU_DROPOUT) {
-              const uint64_t gi = (uint64_t)(row * N + col0 + 16 * ni + 4 * q4 + r);
-              x = drop_hash(ea.seed, gi) < ea.thr ? 0.f : fmaxf(x, 0.f) * ea.scale;
-            }
+            if constexpr (EPI == NR_EPI_RELU_DROPOUT) x = drop_field(dh, r, ea.thr) ? 0.f : fmaxf(x, 0.f) * ea.scale;
             if constexpr (EPI == NR_EPI_EXP) x = epi_exp(x);
             v[ni][r] = x;
           }
+        }
         if constexpr (EPI == NR_EPI_GELU) {
 #pragma unroll
           for (int ni = 0; ni < 4; ++ni) {
@@ -1817,8 +1819,7 @@ extern "C" int nr_gemm_relu_dropout(int dtype_in, int dtype_out, int64_t M, int6
   nr::clear_error();
   NR_CHECK_ARG(p >= 0.f && p < 1.f, "nr_gemm_relu_dropout: p must be in [0, 1)");
   if (M > 0) NR_CHECK_DEVICE("nr_gemm_relu_dropout", A, W, bias, C);
-  const double t = (double)p * 4294967296.0;
-  const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  const uint32_t thr = nr::dropout_threshold(p);
   return nr::gemm_dispatch_ex(dtype_in, dtype_out, NR_EPI_RELU_DROPOUT, M, N, K, A, lda, W, ldw, bias, nullptr, 0,
                               C, ldc, nr::EpiArgs{seed, thr, 1.0f / (1.0f - p)}, (hipStream_t)stream);
 }

@@ -35,7 +35,7 @@ int gemm_dispatch(int dtype_in, int dtype_out, int epi, int64_t M, int64_t N, in
 // forward, the LayerNorm fold, the persistent kernel's column sums.
 struct EpiArgs {
   uint64_t seed;  // dropout stream
-  uint32_t thr;   // drop iff drop_hash(seed, row * N + col) < thr  (thr = p * 2^32)
+  uint32_t thr;   // drop iff drop_at(seed, row * N + col, thr)  (thr = round(p * 2^16), dropout_threshold)
   float scale;    // 1 / (1 - p)
   int group_m = 1;  // 256x256 tile order: >1 groups group_m M-tiles (see tile_of)
   const float* ln_stats = nullptr;  // LNF epilogue: [M] (mean, rstd) pairs
@@ -102,15 +102,31 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 
-// Counter-based dropout stream (splitmix64 finaliser of seed + (idx+1) * golden
-// ratio, upper 32 bits).  oracle/train_ref.py restates it in numpy so the CPU
-// checker draws exactly the same masks.
-__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
+// Counter-based dropout stream: one splitmix64 finaliser output of seed + (g+1) *
+// golden ratio per group g of 4 consecutive elements of a row (element idx = row
+// * N + col, N % 4 == 0, is in group idx >> 2); element idx is dropped iff the
+// 16-bit field idx & 3 of its group's hash is < thr = round(p * 2^16).  (One
+// hash per 4 elements: the RELU_DROPOUT epilogues spent more time in per-element
+// 64-bit hashes than in the ReLU GEMM's epilogue itself.)  oracle/train_ref.py
+// restates it in numpy so the CPU checker draws exactly the same masks.
+__device__ __forceinline__ uint64_t drop_hash4(uint64_t seed, uint64_t g) {
+  uint64_t z = seed + (g + 1) * 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ bool drop_field(uint64_t h, int k, uint32_t thr) {
+  return ((uint32_t)(h >> (16 * k)) & 0xffffu) < thr;
+}
+// host: the 16-bit drop threshold of probability p (p quantised to 1/65536; the
+// keep scale stays 1 / (1 - p))
+static inline uint32_t dropout_threshold(float p) {
+  const double t = __builtin_nearbyint((double)p * 65536.0);
+  return t <= 0.0 ? 0u : t >= 65536.0 ? 65536u : (uint32_t)t;
+}
+// the per-element form (tile kernels): element idx of the stream
+__device__ __forceinline__ bool drop_at(uint64_t seed, uint64_t idx, uint32_t thr) {
+  return drop_field(drop_hash4(seed, idx >> 2), (int)(idx & 3), thr);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

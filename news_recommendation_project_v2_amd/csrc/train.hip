@@ -628,7 +628,7 @@ using namespace nr;
 // C[r][c] = epi(sum_s P[s][r][c] + bias[c]) for the rows of a GEMM that were
 // computed as `parts` K-slices (nr_gemm_grouped, f32 partials), with the
 // epilogues of the training GEMMs: ReLU + dropout (same counter-hash mask as
-// the GEMM kernels: drop_hash(seed, (row0 + r) * N + c)) and the relu/dropout
+// the GEMM kernels: drop_at(seed, (row0 + r) * N + c, thr)) and the relu/dropout
 // backward (R > 0 ? v * scale : 0).  4 columns per thread.
 template <int EPI, typename TO>
 __global__ __launch_bounds__(256) void splitk_fixup_kernel(int64_t rows, int64_t N, int parts, const float* __restrict__ P,
@@ -641,11 +641,12 @@ __global__ __launch_bounds__(256) void splitk_fixup_kernel(int64_t rows, int64_t
   const int64_t r = q / nq, c = (q % nq) * 4;
   f32x4 v = *reinterpret_cast<const f32x4*>(P + r * N + c);
   for (int s = 1; s < parts; ++s) v += *reinterpret_cast<const f32x4*>(P + ((int64_t)s * rows + r) * N + c);
+  uint64_t dh = 0;  // c % 4 == 0: the 4 columns are one group of the dropout stream
+  if constexpr (EPI == NR_EPI_RELU_DROPOUT) dh = drop_hash4(seed, (uint64_t)((row0 + r) * N + c) >> 2);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     float x = v[k] + (bias ? bias[c + k] : 0.f);
-    if constexpr (EPI == NR_EPI_RELU_DROPOUT)
-      x = drop_hash(seed, (uint64_t)((row0 + r) * N + c + k)) < thr ? 0.f : fmaxf(x, 0.f) * scale;
+    if constexpr (EPI == NR_EPI_RELU_DROPOUT) x = drop_field(dh, k, thr) ? 0.f : fmaxf(x, 0.f) * scale;
     if constexpr (EPI == NR_EPI_DRELU) x = ldf(R + r * ldr + c + k) > 0.f ? x * scale : 0.f;
     stf(C + r * ldc + c + k, x);
   }
@@ -850,8 +851,7 @@ extern "C" int nr_splitk_fixup(int dtype_out, int epilogue, int64_t rows, int64_
   NR_CHECK_ARG(((uintptr_t)partials & 15) == 0, "nr_splitk_fixup: partials must be 16-byte aligned");
   NR_CHECK_DEVICE("nr_splitk_fixup", partials, bias, R, C);
   // dropout threshold and scale exactly as nr_gemm_relu_dropout forms them
-  const double t = (double)p * 4294967296.0;
-  const uint32_t thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  const uint32_t thr = dropout_threshold(p);
   if (epilogue == NR_EPI_RELU_DROPOUT) scale = 1.0f / (1.0f - p);
   const int64_t quads = rows * (N / 4);
   NR_CHECK_ARG((quads + 255) / 256 <= 0x7fffffff, "nr_splitk_fixup: too many rows");

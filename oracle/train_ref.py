@@ -11,7 +11,7 @@ Restates the body of AttentionAttentionTrainer.train_one_epoch
   loss       = MarginRankingLoss(2)(*res.chunk(2), 1)
   backward; clip_grad_norm_(params, 0.5); AdamW(lr, wd 0.01).step()
 Dropout (nn.Dropout p in the reference) is drawn from the counter-hash stream
-the HIP path uses (drop_hash below = nr_common.h drop_hash), indexed by the
+the HIP path uses (drop_hash4 / keep_mask below = nr_common.h drop_at), indexed by the
 packed valid-slot row (CSR order) and the column, so both sides see the same
 masks; p = 0 reproduces the reference exactly (tests/golden/train_step.npz).
 """
@@ -26,21 +26,28 @@ import torch.nn.functional as F
 _M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
 
 
-def drop_hash(seed: int, idx: np.ndarray) -> np.ndarray:
-    """splitmix64 finaliser of seed + (idx + 1) * golden, upper 32 bits (uint32)."""
+def drop_hash4(seed: int, g: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser of seed + (g + 1) * golden (uint64): the hash of
+    dropout group g = 4 consecutive elements (nr_common.h drop_hash4)."""
     with np.errstate(over="ignore"):
-        z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + (idx.astype(np.uint64) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + (g.astype(np.uint64) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        z = z ^ (z >> np.uint64(31))
-    return (z >> np.uint64(32)).astype(np.uint32)
+        return z ^ (z >> np.uint64(31))
+
+
+def dropout_threshold(p: float) -> int:
+    """round(p * 2^16), clamped to [0, 65536] (nr_common.h dropout_threshold)."""
+    return int(min(max(round(p * 65536.0), 0), 65536))
 
 
 def keep_mask(seed: int, rows: np.ndarray, ncols: int, p: float) -> torch.Tensor:
-    """keep[r, c] for packed slot rows `rows`: drop iff hash < p * 2^32."""
-    thr = min(int(p * 4294967296.0), 0xFFFFFFFF)
+    """keep[r, c] for packed slot rows `rows`: element idx = row * ncols + c is
+    dropped iff 16-bit field idx & 3 of drop_hash4(seed, idx >> 2) < round(p * 2^16)."""
+    thr = np.uint64(dropout_threshold(p))
     idx = rows.astype(np.uint64)[:, None] * np.uint64(ncols) + np.arange(ncols, dtype=np.uint64)[None, :]
-    return torch.from_numpy((drop_hash(seed, idx) >= np.uint32(thr)).astype(np.float32))
+    field = (drop_hash4(seed, idx >> np.uint64(2)) >> ((idx & np.uint64(3)) * np.uint64(16))) & np.uint64(0xFFFF)
+    return torch.from_numpy((field >= thr).astype(np.float32))
 
 
 def final_attention_train(sd, emb, mask, seeds, p, slot_rows):
