@@ -769,7 +769,11 @@ __global__ __launch_bounds__(512, 2) void gemm256p_group_kernel(GemmGroup g) {
   EpiArgs ea{0, 0, g.alpha[p]};
   ea.sq_part = g.sq_part;
   ea.sq_on = g.sq[p];
-  gemm256p_body<TI, NR_EPI_NONE, TO, MF16, TN>(smem, (int64_t)(lt / nx) * G2BM, (int64_t)(lt % nx) * G2BN, g.M[p],
+  // an XCD runs ~32 consecutive ids at a time: grouped 4 M-tiles x 8 N-tiles
+  // (tile_of), so its L2 holds 12 operand panels per K step, not 2 + 16
+  int mt, nt;
+  tile_of(lt, nx, (int)((g.M[p] + G2BM - 1) / G2BM), 4, mt, nt);
+  gemm256p_body<TI, NR_EPI_NONE, TO, MF16, TN>(smem, (int64_t)mt * G2BM, (int64_t)nt * G2BN, g.M[p],
                                                g.N[p], g.K[p], (const TI*)g.A[p] + b * g.sA[p], g.lda[p],
                                                (const TI*)g.W[p] + b * g.sW[p], g.ldw[p], nullptr, nullptr, 0,
                                                (TO*)g.C[p] + b * g.sC[p], g.ldc[p], ea);
