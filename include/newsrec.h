@@ -163,8 +163,9 @@ int nr_gemm_drelu(int dtype_in, int dtype_out, int64_t M, int64_t N, int64_t K, 
  * last, partial round of 256x256 tiles of a GEMM (config-5 training at M % 4096
  * small): those rows run as `parts` K-slices side by side instead of one tile
  * per CU.  epilogue NR_EPI_NONE, NR_EPI_RELU_DROPOUT (mask of row row0 + r, p as
- * nr_gemm_relu_dropout, `scale` ignored) or NR_EPI_DRELU (R = forward output,
- * C = R > 0 ? v * scale : 0).  bias nullable.
+ * nr_gemm_relu_dropout, `scale` ignored), NR_EPI_DRELU (R = forward output,
+ * C = R > 0 ? v * scale : 0), NR_EPI_RESADD (C = v + R) or NR_EPI_EXP
+ * (C = exp(v)).  bias nullable.
  */
 int nr_splitk_fixup(int dtype_out, int epilogue, int64_t rows, int64_t N, int parts, const float* partials,
                     const float* bias, const void* R, int64_t ldr, void* C, int64_t ldc, int64_t row0,

@@ -1470,7 +1470,8 @@ __global__ __launch_bounds__(512, 2) void gemm256t_kernel(int64_t M, int64_t N, 
           x += __shfl_xor(x, 8, 64);
           cs[ni][r] = x;
         }
-      if (c16 < 4) {
+      // (a 128-row block wholly past M has no column-sum row: ceil(M / 128) rows)
+      if (c16 < 4 && (int64_t)m0 + wm * 128 < M) {
         const f32x4 o = c16 == 0 ? cs[0] : c16 == 1 ? cs[1] : c16 == 2 ? cs[2] : cs[3];
         const int64_t prow = ((int64_t)m0 + wm * 128) >> 7;
         *reinterpret_cast<f32x4*>(ea.colsum + prow * N + col0 + 16 * c16 + 4 * q4) = o;

@@ -648,6 +648,8 @@ __global__ __launch_bounds__(256) void splitk_fixup_kernel(int64_t rows, int64_t
     float x = v[k] + (bias ? bias[c + k] : 0.f);
     if constexpr (EPI == NR_EPI_RELU_DROPOUT) x = drop_field(dh, k, thr) ? 0.f : fmaxf(x, 0.f) * scale;
     if constexpr (EPI == NR_EPI_DRELU) x = ldf(R + r * ldr + c + k) > 0.f ? x * scale : 0.f;
+    if constexpr (EPI == NR_EPI_RESADD) x += ldf(R + r * ldr + c + k);
+    if constexpr (EPI == NR_EPI_EXP) x = __expf(x);  // as the bf16 GEMM epilogue (gemm.hip epi_exp)
     stf(C + r * ldc + c + k, x);
   }
 }
@@ -843,11 +845,13 @@ extern "C" int nr_splitk_fixup(int dtype_out, int epilogue, int64_t rows, int64_
   clear_error();
   NR_CHECK_ARG(NR_OKDT(dtype_out) && rows >= 0 && N > 0 && N % 4 == 0 && parts >= 1 && ldc >= N && row0 >= 0,
                "nr_splitk_fixup: bad args");
-  NR_CHECK_ARG(epilogue == NR_EPI_NONE || epilogue == NR_EPI_RELU_DROPOUT || epilogue == NR_EPI_DRELU,
+  NR_CHECK_ARG(epilogue == NR_EPI_NONE || epilogue == NR_EPI_RELU_DROPOUT || epilogue == NR_EPI_DRELU ||
+                   epilogue == NR_EPI_RESADD || epilogue == NR_EPI_EXP,
                "nr_splitk_fixup: epilogue %d unsupported", epilogue);
   NR_CHECK_ARG(p >= 0.f && p < 1.f, "nr_splitk_fixup: dropout p outside [0, 1)");
   if (rows == 0) return NR_OK;
-  NR_CHECK_ARG(partials && C && (epilogue != NR_EPI_DRELU || (R && ldr >= N)), "nr_splitk_fixup: null pointer");
+  NR_CHECK_ARG(partials && C && ((epilogue != NR_EPI_DRELU && epilogue != NR_EPI_RESADD) || (R && ldr >= N)),
+               "nr_splitk_fixup: null pointer");
   NR_CHECK_ARG(((uintptr_t)partials & 15) == 0, "nr_splitk_fixup: partials must be 16-byte aligned");
   NR_CHECK_DEVICE("nr_splitk_fixup", partials, bias, R, C);
   // dropout threshold and scale exactly as nr_gemm_relu_dropout forms them
@@ -862,6 +866,8 @@ extern "C" int nr_splitk_fixup(int dtype_out, int epilogue, int64_t rows, int64_
                                        bias, (const T*)R, ldr, (T*)C, ldc, row0, seed, thr, scale))
   if (epilogue == NR_EPI_RELU_DROPOUT) NR_FIX(NR_EPI_RELU_DROPOUT);
   else if (epilogue == NR_EPI_DRELU) NR_FIX(NR_EPI_DRELU);
+  else if (epilogue == NR_EPI_RESADD) NR_FIX(NR_EPI_RESADD);
+  else if (epilogue == NR_EPI_EXP) NR_FIX(NR_EPI_EXP);
   else NR_FIX(NR_EPI_NONE);
 #undef NR_FIX
   NR_CHECK_LAUNCH("nr_splitk_fixup");

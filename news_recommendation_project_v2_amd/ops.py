@@ -529,10 +529,11 @@ def splitk_fixup(partials: torch.Tensor, out: torch.Tensor, epilogue: str = "non
                  residual: Optional[torch.Tensor] = None, row0: int = 0, seed: int = 0, p: float = 0.0,
                  scale: float = 1.0) -> torch.Tensor:
     """out = epi(partials.sum(0) + bias) for K-slice partials [parts, rows, N] f32
-    (nr_splitk_fixup): epilogue "none", "relu_dropout" (mask rows row0..) or
-    "drelu" (residual = the forward output)."""
+    (nr_splitk_fixup): epilogue "none", "relu_dropout" (mask rows row0..), "drelu"
+    (residual = the forward output), "resadd" (+ residual) or "exp"."""
     dev = _dev(partials, out, bias, residual)
-    epi = {"none": _lib.NR_EPI_NONE, "relu_dropout": _lib.NR_EPI_RELU_DROPOUT, "drelu": _lib.NR_EPI_DRELU}[epilogue]
+    epi = {"none": _lib.NR_EPI_NONE, "relu_dropout": _lib.NR_EPI_RELU_DROPOUT, "drelu": _lib.NR_EPI_DRELU,
+           "resadd": _lib.NR_EPI_RESADD, "exp": _lib.NR_EPI_EXP}[epilogue]
     if partials.dtype != torch.float32 or not partials.is_contiguous() or partials.dim() != 3:
         raise _lib.NewsRecHIPError("splitk_fixup: partials must be contiguous f32 [parts, rows, N]")
     parts, rows, N = partials.shape

@@ -398,3 +398,22 @@ def test_gpu_split_k_tail_matches_full_gemm(gpu_device, K):
         assert torch.equal(got[:4096], ref[:4096])                  # the whole-round rows: the same kernel
         assert torch.equal(got[4096:] == 0, ref[4096:] == 0)        # same mask / relu / drelu zeros
         torch.testing.assert_close(got[4096:].float(), ref[4096:].float(), rtol=1.6e-2, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_gpu_splitk_fixup_resadd_exp(gpu_device):
+    """nr_splitk_fixup's RESADD (C = sum + bias + R) and EXP (C = exp(sum + bias))
+    epilogues against torch on the same f32 partials (bf16 output: to its rounding)."""
+    from news_recommendation_project_v2_amd import ops
+    g = torch.Generator(device=gpu_device).manual_seed(3)
+    parts = torch.randn(8, 128, 1024, device=gpu_device, generator=g) * 0.1
+    b = torch.randn(1024, device=gpu_device, generator=g) * 0.1
+    r = torch.randn(128, 1024, device=gpu_device, generator=g).bfloat16()
+    out = torch.empty(128, 1024, device=gpu_device, dtype=torch.bfloat16)
+    ops.splitk_fixup(parts, out, "resadd", bias=b, residual=r)
+    torch.cuda.synchronize()
+    ref = parts.sum(0) + b + r.float()
+    torch.testing.assert_close(out.float(), ref, rtol=8e-3, atol=1e-5)
+    ops.splitk_fixup(parts, out, "exp", bias=b)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.float(), (parts.sum(0) + b).exp(), rtol=8e-3, atol=1e-6)
