@@ -44,6 +44,8 @@ def _calls(P):
         "nr_gemm_drelu": (BF16, BF16, 4, 256, 64, P, 64, P, 64, P, 256, P, 256, f(1.0), None),
         "nr_gemm_grouped": (BF16, F32, 1, (L * 1)(256), (L * 1)(256), (L * 1)(64), ptrs, (L * 1)(64), ptrs,
                             (L * 1)(64), ptrs, (L * 1)(256), None),
+        "nr_gemm_grouped_tn": (F32, 1, (L * 1)(256), (L * 1)(256), (L * 1)(64), ptrs, (L * 1)(256), ptrs,
+                               (L * 1)(256), ptrs, (L * 1)(256), None, None),
         "nr_layernorm": (F32, F32, 2, 1024, P, 1024, P, P, f(1e-5), P, 1024, None),
         "nr_gather_layernorm": (F32, 2, 1024, P, 1024, P, 1, P, P, f(1e-12), P, 1024, None),
         "nr_softmax64": (2, 2, P, 128, F32, P, 128, None),
@@ -85,8 +87,9 @@ def test_every_entry_with_pointers_is_covered():
               "nr_encoder_workspace_bytes", "nr_residency_flush", "nr_is_device_pointer",
               # communicator handles (tests/test_comm.py)
               "nr_rccl_version", "nr_comm_unique_id", "nr_comm_init", "nr_comm_destroy", "nr_allgather",
-              # one struct of pointers (test_latent_train_step_refuses_host_pointers below)
-              "nr_latent_train_workspace_bytes", "nr_latent_train_step"}
+              # one struct of pointers (the train-step tests below)
+              "nr_latent_train_workspace_bytes", "nr_latent_train_step",
+              "nr_final_train_workspace_bytes", "nr_final_train_step"}
     assert set(_calls(ctypes.c_void_p(256))) == set(_lib.SIGNATURES) - no_ptr
 
 
@@ -122,3 +125,17 @@ def test_latent_train_step_refuses_host_pointers(lib, H):
     assert "empty batch" in lib.nr_last_error().decode()
     assert lib.nr_latent_train_workspace_bytes(_lib.NR_BF16, 256, 8000, 8310) > 0
     assert lib.nr_latent_train_workspace_bytes(7, 1, 1, 1) == -1
+
+
+def test_final_train_step_refuses_host_pointers(lib, H):
+    """nr_final_train_step (one struct of pointers) checks every one before any
+    launch; its workspace query rejects a bad dtype."""
+    _, P = H
+    a = _lib.FinalTrainArgs()
+    a.dtype, a.tok_dtype, a.B, a.U, a.Hs, a.margin, a.p = _lib.NR_BF16, _lib.NR_F16, 4, 8, 16, 2.0, 0.1
+    for f, _ in a._fields_:
+        if f not in ("dtype", "tok_dtype", "B", "U", "Hs", "margin", "p", "seed"):
+            setattr(a, f, P.value)
+    rc = lib.nr_final_train_step(ctypes.byref(a), P, 1 << 26, None)
+    assert rc == -1 and "not device memory" in lib.nr_last_error().decode()
+    assert lib.nr_final_train_workspace_bytes(7, 1, 1, 1) == -1
