@@ -85,15 +85,25 @@ def _check_loss_out(t: torch.Tensor, dev) -> torch.Tensor:
     return t
 
 
+def _weights_version(step) -> tuple:
+    """Version counters of everything that can write the master weights outside
+    AdamW: the flat buffer and its views (``views``), and the modules' Parameters,
+    whose ``.data`` was pointed at those views -- a Parameter keeps its own version
+    counter through ``.data =``, so load_state_dict on a wrapped module moves only
+    the Parameter's, not the flat buffer's.  AdamW (a library call through raw
+    pointers) moves neither."""
+    return (step.flat._version,) + tuple(p._version for p in step._mod_params)
+
+
 def _refresh_mirror(step) -> None:
     """Rewrite a step's bf16 weight mirror when its master weights changed outside
-    AdamW (load_state_dict on the wrapped modules, an edit through ``views``): the
-    parameters are views of ``step.flat``, so such writes move its version
-    counter, while AdamW (a library call) does not."""
-    if step.flat16 is not None and step.flat._version != step._mirror_version:
+    AdamW (load_state_dict on the wrapped modules, an edit through ``views``;
+    ADVICE r4)."""
+    v = _weights_version(step)
+    if step.flat16 is not None and v != step._mirror_version:
         with torch.no_grad():
             step.flat16.copy_(step.flat)
-        step._mirror_version = step.flat._version
+    step._mirror_version = v
 
 
 class FinalAttentionTrainStep:
@@ -156,7 +166,8 @@ class FinalAttentionTrainStep:
         self._ws = {}
         self._ws_native = None
         self._users = None
-        self._mirror_version = self.flat._version
+        self._mod_params = list(params)  # the modules' Parameters (now views of flat)
+        self._mirror_version = _weights_version(self)
         self._pmap = {"tok_g": "ln.weight", "tok_b": "ln.bias", "W5": "linear5.weight",
                       **{f"W{i}": f"linear{i}.weight" for i in range(1, 5)},
                       **{f"b{i}": f"linear{i}.bias" for i in range(1, 5)}}
@@ -359,7 +370,8 @@ class LatentAttentionTrainStep:
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self._ws = None
         self._users = None
-        self._mirror_version = self.flat._version
+        self._mod_params = list(params)  # the modules' Parameters (now views of flat)
+        self._mirror_version = _weights_version(self)
         b = "latent.cross_attend_blocks."
         self._pmap = {"tok_g": "ln.weight", "tok_b": "ln.bias", "latents": "latent.latents",
                       "nq_g": b + "0.norm.weight", "nq_b": b + "0.norm.bias",
