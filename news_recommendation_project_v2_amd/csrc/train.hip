@@ -132,40 +132,83 @@ __global__ __launch_bounds__(256) void transpose_f32_bf16_kernel(int64_t rows, i
 // FinalAttention pooling (modeling_utils.py:224-228) over consecutive slot rows:
 // xp row = [x | p] (p = exp(w)); u_d = sum x p / (sum p + 1e-10), z_d = sum p + 1e-10.
 // One workgroup (4 waves x 256 dims) per segment.
+// 4 consecutive elements as one 8-B (bf16) / 16-B (f32) access (host: 16-B aligned
+// base, row strides and column offsets multiples of 4 elements)
 template <typename T>
-__global__ __launch_bounds__(256) void final_pool_fwd_kernel(int64_t n_seg, const int64_t* __restrict__ off,
-                                                             const T* __restrict__ xp, int64_t ld,
-                                                             float* __restrict__ users, float* __restrict__ z) {
-  // block = (segment, 256-dim quarter); the 4 waves stride the segment's rows,
-  // 4 dims per lane, partial sums folded through LDS (fixed order).
+__device__ __forceinline__ void ld4v(const T* p, float (&v)[4]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 q = *reinterpret_cast<const float4*>(p);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+    const uint2 q = *reinterpret_cast<const uint2*>(p);
+    v[0] = bf16_lo(q.x); v[1] = bf16_hi(q.x); v[2] = bf16_lo(q.y); v[3] = bf16_hi(q.y);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st4v(T* p, const float (&v)[4]) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
+  } else {
+    const __bf16 h[4] = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(h);
+  }
+}
+
+// ----------------------------------------------------------------- pooling fwd
+// u[b, d] = sum_i x[i, d] p[i, d] / (sum_i p[i, d] + 1e-10) over the rows of
+// segment b (FinalAttention's per-dimension softmax pooling, modeling_utils.py:224-228,
+// with p = exp(logit) from the GEMM epilogue); z = the denominator (saved for bwd).
+// Block = (segment, 256-dim quarter) with kPoolWaves waves striding the segment's
+// rows (4 dims per lane, one 8-B load of x and of p per row), partial sums folded
+// through LDS in a fixed order.  16 waves: the history lengths are geometric up to
+// 600 and the longest segment's block sets the kernel time (4 waves: 26 us).
+constexpr int kPoolWaves = 16;
+template <typename T>
+__global__ __launch_bounds__(64 * kPoolWaves) void final_pool_fwd_kernel(int64_t n_seg, const int64_t* __restrict__ off,
+                                                                        const T* __restrict__ xp, int64_t ld,
+                                                                        float* __restrict__ users,
+                                                                        float* __restrict__ z) {
   constexpr int D = 1024;
-  __shared__ float sn[4][256], sd[4][256];
+  __shared__ float sn[kPoolWaves][256], sd[kPoolWaves][256];
   const int64_t b = blockIdx.x;
   if (b >= n_seg) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int d = (int)blockIdx.y * 256 + lane * 4;
   float num[4] = {0.f, 0.f, 0.f, 0.f}, den[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t i = off[b] + wave; i < off[b + 1]; i += 4) {
+#pragma unroll 2
+  for (int64_t i = off[b] + wave; i < off[b + 1]; i += kPoolWaves) {
     const T* row = xp + i * ld;
+    float x[4], p[4];
+    ld4v<T>(row + d, x);
+    ld4v<T>(row + D + d, p);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float x = ldf<T>(row + d + t), p = ldf<T>(row + D + d + t);
-      num[t] = fmaf(x, p, num[t]);
-      den[t] += p;
+      num[t] = fmaf(x[t], p[t], num[t]);
+      den[t] += p[t];
     }
   }
 #pragma unroll
   for (int t = 0; t < 4; ++t) { sn[wave][lane * 4 + t] = num[t]; sd[wave][lane * 4 + t] = den[t]; }
   __syncthreads();
-  const int c = threadIdx.x, dc = (int)blockIdx.y * 256 + c;
-  const float zz = ((sd[0][c] + sd[1][c]) + (sd[2][c] + sd[3][c])) + 1e-10f;
-  z[b * D + dc] = zz;
-  users[b * D + dc] = ((sn[0][c] + sn[1][c]) + (sn[2][c] + sn[3][c])) / zz;
+  if (threadIdx.x < 256) {
+    const int c = threadIdx.x, dc = (int)blockIdx.y * 256 + c;
+    float sdn = 0.f, snn = 0.f;
+#pragma unroll
+    for (int w = 0; w < kPoolWaves; ++w) { sdn += sd[w][c]; snn += sn[w][c]; }
+    const float zz = sdn + 1e-10f;
+    z[b * D + dc] = zz;
+    users[b * D + dc] = snn / zz;
+  }
 }
 
 // ----------------------------------------------------------------- pooling bwd
 // dx_i = du * p_i / z ;  dlogit_i = du * (x_i - u) / z * p_i  (d p_i / d w_i = p_i).
-// Rows of no segment (padding up to n_rows) get zeros.
+// Rows of no segment (padding up to n_rows) get zeros.  Every row is independent
+// given its segment's (du, u, z), so the grid runs over ROWS, not segments: block =
+// 16 rows x one 256-dim quarter, wave w rows 4 w .. 4 w + 3, 4 dims per lane, the
+// row's segment found by a binary search of off for the wave's first row and
+// stepped after (rows are in segment order).  Per-segment blocks waited on the
+// longest history (geometric lengths up to 600): 31 us at 4 waves, 22 at 16.
 template <typename T>
 __global__ __launch_bounds__(256) void final_pool_bwd_kernel(int64_t n_seg, const int64_t* __restrict__ off,
                                                              int64_t n_rows, const T* __restrict__ xp, int64_t ld,
@@ -173,33 +216,53 @@ __global__ __launch_bounds__(256) void final_pool_bwd_kernel(int64_t n_seg, cons
                                                              const float* __restrict__ z,
                                                              const float* __restrict__ du, T* __restrict__ dx,
                                                              int64_t lddx, T* __restrict__ dl, int64_t lddl) {
-  // block = (segment, 256-dim quarter), waves stride the rows (as the forward)
   constexpr int D = 1024;
-  const int64_t b = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int d = (int)blockIdx.y * 256 + lane * 4;
-  if (b >= n_seg) {  // trailing blocks zero the padding rows
-    for (int64_t i = off[n_seg] + (b - n_seg) * 4 + wave; i < n_rows; i += (int64_t)(gridDim.x - n_seg) * 4)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) { stf<T>(dx + i * lddx + d + t, 0.f); stf<T>(dl + i * lddl + d + t, 0.f); }
-    return;
-  }
+  const int64_t r0 = (int64_t)blockIdx.x * 16 + wave * 4;
+  const int64_t nvalid = off[n_seg];
+  int64_t b = -1, bend = 0;  // current segment and its end row
   float g[4], u[4], iz[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    g[t] = du[b * D + d + t];
-    u[t] = users[b * D + d + t];
-    iz[t] = 1.0f / z[b * D + d + t];
-  }
-  for (int64_t i = off[b] + wave; i < off[b + 1]; i += 4) {
+  for (int k = 0; k < 4; ++k) {
+    const int64_t i = r0 + k;
+    if (i >= n_rows) break;
+    if (i >= nvalid) {
+      const float zero[4] = {0.f, 0.f, 0.f, 0.f};
+      st4v<T>(dx + i * lddx + d, zero);
+      st4v<T>(dl + i * lddl + d, zero);
+      continue;
+    }
+    if (i >= bend) {
+      if (b < 0) {  // largest b with off[b] <= i (off[0] = 0 <= i < off[n_seg])
+        int64_t lo = 0, hi = n_seg - 1;
+        while (lo < hi) {
+          const int64_t mid = (lo + hi + 1) >> 1;
+          if (off[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        b = lo;
+      } else {
+        do { ++b; } while (off[b + 1] <= i);  // (empty segments are stepped over)
+      }
+      bend = off[b + 1];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        g[t] = du[b * D + d + t];
+        u[t] = users[b * D + d + t];
+        iz[t] = 1.0f / z[b * D + d + t];
+      }
+    }
     const T* row = xp + i * ld;
+    float x[4], p[4], gx[4], gl[4];
+    ld4v<T>(row + d, x);
+    ld4v<T>(row + D + d, p);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const float x = ldf<T>(row + d + t), p = ldf<T>(row + D + d + t);
-      const float gp = g[t] * p * iz[t];
-      stf<T>(dx + i * lddx + d + t, gp);
-      stf<T>(dl + i * lddl + d + t, gp * (x - u[t]));
+      gx[t] = g[t] * p[t] * iz[t];
+      gl[t] = gx[t] * (x[t] - u[t]);
     }
+    st4v<T>(dx + i * lddx + d, gx);
+    st4v<T>(dl + i * lddl + d, gl);
   }
 }
 
@@ -715,7 +778,8 @@ extern "C" int nr_final_pool_fwd(int dtype, int64_t n_seg, const int64_t* off, c
   if (n_seg == 0) return NR_OK;
   NR_CHECK_ARG(off && xp && users && z, "nr_final_pool_fwd: null pointer");
   NR_CHECK_DEVICE("nr_final_pool_fwd", off, xp, users, z);
-  NR_DT1(dtype, hipLaunchKernelGGL((final_pool_fwd_kernel<T>), dim3((unsigned)n_seg, 4), dim3(256), 0,
+  NR_CHECK_ARG(((uintptr_t)xp & 15) == 0 && ld % 4 == 0, "nr_final_pool_fwd: xp must be 16-byte aligned, ld %% 4 == 0");
+  NR_DT1(dtype, hipLaunchKernelGGL((final_pool_fwd_kernel<T>), dim3((unsigned)n_seg, 4), dim3(64 * kPoolWaves), 0,
                                    (hipStream_t)stream, n_seg, off, (const T*)xp, ld, users, z));
   NR_CHECK_LAUNCH("nr_final_pool_fwd");
   return NR_OK;
@@ -730,7 +794,12 @@ extern "C" int nr_final_pool_bwd(int dtype, int64_t n_seg, const int64_t* off, i
   if (n_seg == 0 && n_rows == 0) return NR_OK;
   NR_CHECK_ARG(off && xp && users && z && du && dx && dl, "nr_final_pool_bwd: null pointer");
   NR_CHECK_DEVICE("nr_final_pool_bwd", off, xp, users, z, du, dx, dl);
-  const unsigned grid = (unsigned)(n_seg + 64);  // 64 trailing blocks zero the padding rows
+  NR_CHECK_ARG(((uintptr_t)xp & 15) == 0 && ((uintptr_t)dx & 15) == 0 && ((uintptr_t)dl & 15) == 0 && ld % 4 == 0 &&
+                   lddx % 4 == 0 && lddl % 4 == 0,
+               "nr_final_pool_bwd: xp / dx / dl must be 16-byte aligned with row strides %% 4 == 0");
+  if (n_rows == 0) return NR_OK;
+  NR_CHECK_ARG((n_rows + 15) / 16 <= 0x7fffffff, "nr_final_pool_bwd: too many rows");
+  const unsigned grid = (unsigned)((n_rows + 15) / 16);  // 16 rows per block
   NR_DT1(dtype, hipLaunchKernelGGL((final_pool_bwd_kernel<T>), dim3(grid, 4), dim3(256), 0, (hipStream_t)stream,
                                    n_seg, off, n_rows, (const T*)xp, ld, users, z, du, (T*)dx, lddx, (T*)dl, lddl));
   NR_CHECK_LAUNCH("nr_final_pool_bwd");
