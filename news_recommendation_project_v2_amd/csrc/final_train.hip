@@ -84,17 +84,17 @@ __global__ __launch_bounds__(256) void zero_kernel(ZList z) {
 
 // From the token rows' LayerNorm xhat (f32 [U][D], gamma = 1 / beta = 0): slot rows
 // i < Hp get S[i] = xhat[hist[i]] gamma + beta and XH[i] = xhat[hist[i]] (TA; zero
-// rows past Hs), news rows u < U get E[u] = xhat[u] gamma + beta (f32, the cosine's
-// rows).  One wave per row, 4 columns per lane.
+// rows past Hs).  (The news rows' E = xhat gamma + beta is formed where it is read,
+// by cos_pairs_kernel for the 2B pos / neg rows, not stored for all U.)  One wave per
+// row, 4 columns per lane.
 template <typename TA>
-__global__ __launch_bounds__(256) void slots_kernel(int64_t Hp, int64_t Hs, int64_t U, const float* __restrict__ xh,
+__global__ __launch_bounds__(256) void slots_kernel(int64_t Hp, int64_t Hs, const float* __restrict__ xh,
                                                     const int32_t* __restrict__ hist, const float* __restrict__ g,
                                                     const float* __restrict__ b, TA* __restrict__ S,
-                                                    TA* __restrict__ XH, float* __restrict__ E) {
+                                                    TA* __restrict__ XH) {
   const int lane = threadIdx.x & 63;
-  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < Hp + U; i += (int64_t)gridDim.x * 4) {
-    const bool slot = i < Hp;
-    const int64_t r = slot ? (i < Hs ? (int64_t)hist[i] : -1) : i - Hp;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < Hp; i += (int64_t)gridDim.x * 4) {
+    const int64_t r = i < Hs ? (int64_t)hist[i] : -1;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t c = 256 * j + 4 * lane;
@@ -104,12 +104,8 @@ __global__ __launch_bounds__(256) void slots_kernel(int64_t Hp, int64_t Hs, int6
       ld4<float>(b + c, bb);
 #pragma unroll
       for (int t = 0; t < 4; ++t) e[t] = r >= 0 ? fmaf(v[t], gg[t], bb[t]) : 0.f;
-      if (slot) {
-        st4<TA>(S + i * D + c, e);
-        st4<TA>(XH + i * D + c, v);
-      } else {
-        st4<float>(E + (i - Hp) * D + c, e);
-      }
+      st4<TA>(S + i * D + c, e);
+      st4<TA>(XH + i * D + c, v);
     }
   }
 }
@@ -210,7 +206,8 @@ __global__ __launch_bounds__(256) void sq_total_kernel(int64_t n, const float* _
 // into a [U][D] dE) and the per-row loss terms kept for an ordered sum: E is
 // the token LN's output, so those rows only feed pair_ln_kernel.  One wave per row.
 __global__ __launch_bounds__(256) void cos_pairs_kernel(int64_t B, const float* __restrict__ users,
-                                                        const float* __restrict__ E, const int32_t* __restrict__ pos,
+                                                        const float* __restrict__ xh, const float* __restrict__ tg,
+                                                        const float* __restrict__ tb, const int32_t* __restrict__ pos,
                                                         const int32_t* __restrict__ neg, float margin,
                                                         float* __restrict__ lrow, float* __restrict__ du,
                                                         float* __restrict__ gpair) {
@@ -220,14 +217,23 @@ __global__ __launch_bounds__(256) void cos_pairs_kernel(int64_t B, const float* 
   if (b >= B) return;
   float u[4][4], ep[4][4], en[4][4];
   float uu = 0.f, pp = 0.f, nn = 0.f, up = 0.f, un = 0.f;
-  const float* pr = E + (int64_t)pos[b] * D;
-  const float* qr = E + (int64_t)neg[b] * D;
+  // E[n] = xhat[n] gamma + beta (the token LN's output), as slots_kernel forms S
+  const float* pr = xh + (int64_t)pos[b] * D;
+  const float* qr = xh + (int64_t)neg[b] * D;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int e = j * 256 + lane * 4;
+    float gg[4], bb[4];
     ld4<float>(users + b * D + e, u[j]);
     ld4<float>(pr + e, ep[j]);
     ld4<float>(qr + e, en[j]);
+    ld4<float>(tg + e, gg);
+    ld4<float>(tb + e, bb);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      ep[j][t] = fmaf(ep[j][t], gg[t], bb[t]);
+      en[j][t] = fmaf(en[j][t], gg[t], bb[t]);
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       uu = fmaf(u[j][t], u[j][t], uu);
@@ -386,7 +392,7 @@ __global__ __launch_bounds__(256) void rowsum_kernel(RSum r, float* __restrict__
 // ------------------------------------------------------------------ workspace
 struct Layout {
   int64_t Hp, es, mm, csr;
-  int64_t E, XHu, S, XH, X1, X2, XP, Y, users, z, du, gpair, lrow, dXp, dL, dY, dX, dZ2, dZ1, w1p, sqp;
+  int64_t XHu, S, XH, X1, X2, XP, Y, users, z, du, gpair, lrow, dXp, dL, dY, dX, dZ2, dZ1, w1p, sqp;
   int64_t W1t, W2t, W3t, W4t, W5t, skP, cs4, cs3, cs2, cs1;
   int64_t T[10];  // f32 mode: the weight-grad operands transposed
   int64_t total;
@@ -412,7 +418,7 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs, int ncu) {
   const int64_t Hp = L.Hp, es = L.es, Bp = pad64(B);
   int64_t o = 0;
   auto take = [&](int64_t bytes) { const int64_t r = o; o += al(bytes); return r; };
-  L.E = take(U * D * 4); L.XHu = take(U * D * 4);
+  L.XHu = take(U * D * 4);
   L.S = take(Hp * D * es); L.XH = take(Hp * D * es); L.X1 = take(Hp * H * es); L.X2 = take(Hp * H * es); L.XP = take(Hp * 2 * D * es);
   L.Y = take(Hp * H * es);
   L.users = take(Bp * D * 4); L.z = take(Bp * D * 4); L.du = take(Bp * D * 4); L.gpair = take(2 * B * D * 4);
@@ -463,7 +469,7 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   const Layout L = layout(dt, a.B, a.U, a.Hs, ncu);
   const int64_t B = a.B, U = a.U, Hs = a.Hs, Hp = L.Hp, mm = L.mm;
   auto P_ = [&](int64_t off) { return (void*)(ws + off); };
-  float *E = (float*)P_(L.E), *XHu = (float*)P_(L.XHu);
+  float* XHu = (float*)P_(L.XHu);
   TA* XH = (TA*)P_(L.XH);
   TA *S = (TA*)P_(L.S), *X1 = (TA*)P_(L.X1), *X2 = (TA*)P_(L.X2), *XP = (TA*)P_(L.XP), *Y = (TA*)P_(L.Y);
   float* users = a.users ? a.users : (float*)P_(L.users);
@@ -504,12 +510,12 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
     NR_CHECK_LAUNCH("nr_final_train_step (zero)");
   }
   // ---- forward
-  // xhat of the U token rows (LN without the affine), then the slots' S and XH and the news rows' E
+  // xhat of the U token rows (LN without the affine), then the slots' S and XH
   NR_FT(gather_ln_dispatch(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1, nullptr, nullptr, 1e-12f, XHu, D, st));
   {
-    const int64_t g = (Hp + U + 3) / 4;
-    hipLaunchKernelGGL((slots_kernel<TA>), dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, Hp, Hs, U, XHu,
-                       a.hist_idx, a.tok_g, a.tok_b, S, XH, E);
+    const int64_t g = (Hp + 3) / 4;
+    hipLaunchKernelGGL((slots_kernel<TA>), dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, Hp, Hs, XHu,
+                       a.hist_idx, a.tok_g, a.tok_b, S, XH);
     NR_CHECK_LAUNCH("nr_final_train_step (slots)");
   }
   // relu(dropout) GEMM over Hp rows: main rows on the persistent kernel, the tail as K-slices + fixup
@@ -532,8 +538,8 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   NR_FT(gemm_dispatch(dt, dt, NR_EPI_EXP, Hp, D, H, Y, H, W5, H, nullptr, nullptr, 0, Pexp, 2 * D, st));
   NR_FT(nr_final_pool_fwd(dt, B, a.hist_off, XP, 2 * D, users, z, st));
   // ---- loss and its gradient into the pooled users and E[pos] / E[neg]
-  hipLaunchKernelGGL(cos_pairs_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, users, E, a.pos, a.neg,
-                     a.margin, lrow, du, gpair);
+  hipLaunchKernelGGL(cos_pairs_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, users, XHu, a.tok_g,
+                     a.tok_b, a.pos, a.neg, a.margin, lrow, du, gpair);
   NR_CHECK_LAUNCH("nr_final_train_step (cosine)");
   // the pairs' token LN grad partials (after the W1 fold's chunks) and the loss
   hipLaunchKernelGGL(pair_ln_kernel, dim3((unsigned)(D / 64), kPairChunks), dim3(256), 0, st, B, gpair, XHu, a.pos,
