@@ -71,6 +71,44 @@ __device__ __forceinline__ void st4(T* p, const float v[4]) {
   }
 }
 
+// The token model's output row of news n (g_mlp_layernorm without its affine, eps
+// 1e-12: the arithmetic of gather_ln_kernel, rowops.hip, so the bits are those of
+// nr_gather_layernorm): lane's 4 x 4 columns 256 j + 4 lane .. +3 of xhat.  TT =
+// the token states' type (f32 / bf16 / f16).
+template <typename TT>
+__device__ __forceinline__ void tok_xhat(const TT* row, int lane, float (&v)[4][4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const TT* p = row + j * 256 + lane * 4;
+    if constexpr (sizeof(TT) == 4) {
+      ld4<float>((const float*)p, v[j]);
+    } else if constexpr (std::is_same<TT, _Float16>::value) {
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      const h4 h = *reinterpret_cast<const h4*>(p);
+      v[j][0] = (float)h[0]; v[j][1] = (float)h[1]; v[j][2] = (float)h[2]; v[j][3] = (float)h[3];
+    } else {
+      ld4<__bf16>((const __bf16*)p, v[j]);
+    }
+  }
+  float sm = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sm += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+  const float mean = wave_sum(sm) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float d = v[j][t] - mean;
+      q = fmaf(d, d, q);
+    }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + 1e-12f);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) v[j][t] = (v[j][t] - mean) * rstd;
+}
+
 struct ZList {  // zero up to 8 f32 ranges in one launch
   float* p[8];
   int64_t len[8];
@@ -82,30 +120,31 @@ __global__ __launch_bounds__(256) void zero_kernel(ZList z) {
       z.p[i][j] = 0.f;
 }
 
-// From the token rows' LayerNorm xhat (f32 [U][D], gamma = 1 / beta = 0): slot rows
-// i < Hp get S[i] = xhat[hist[i]] gamma + beta and XH[i] = xhat[hist[i]] (TA; zero
-// rows past Hs).  (The news rows' E = xhat gamma + beta is formed where it is read,
-// by cos_pairs_kernel for the 2B pos / neg rows, not stored for all U.)  One wave per
-// row, 4 columns per lane.
-template <typename TA>
-__global__ __launch_bounds__(256) void slots_kernel(int64_t Hp, int64_t Hs, const float* __restrict__ xh,
+// Slot rows i < Hp: xhat = the token LN (no affine) of the last token of news
+// hist[i], computed here per slot from the token states (no [U][D] LN table:
+// Hs ~ U at the benchmark batch, and the token rows are half the bytes),
+// S[i] = xhat gamma + beta and XH[i] = xhat (TA; zero rows past Hs).  The pos / neg
+// rows' LN is formed by cos_pairs_kernel.  One wave per row, 4 columns per lane.
+template <typename TA, typename TT>
+__global__ __launch_bounds__(256) void slots_kernel(int64_t Hp, int64_t Hs, const TT* __restrict__ tok,
                                                     const int32_t* __restrict__ hist, const float* __restrict__ g,
                                                     const float* __restrict__ b, TA* __restrict__ S,
                                                     TA* __restrict__ XH) {
   const int lane = threadIdx.x & 63;
   for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < Hp; i += (int64_t)gridDim.x * 4) {
-    const int64_t r = i < Hs ? (int64_t)hist[i] : -1;
+    const int64_t r = i < Hs ? (int64_t)hist[i] : -1;  // wave-uniform
+    float v[4][4] = {};
+    if (r >= 0) tok_xhat<TT>(tok + r * D, lane, v);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t c = 256 * j + 4 * lane;
-      float v[4] = {0.f, 0.f, 0.f, 0.f}, gg[4], bb[4], e[4];
-      if (r >= 0) ld4<float>(xh + r * D + c, v);
+      float gg[4], bb[4], e[4];
       ld4<float>(g + c, gg);
       ld4<float>(b + c, bb);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) e[t] = r >= 0 ? fmaf(v[t], gg[t], bb[t]) : 0.f;
+      for (int t = 0; t < 4; ++t) e[t] = r >= 0 ? fmaf(v[j][t], gg[t], bb[t]) : 0.f;
       st4<TA>(S + i * D + c, e);
-      st4<TA>(XH + i * D + c, v);
+      st4<TA>(XH + i * D + c, v[j]);
     }
   }
 }
@@ -205,8 +244,10 @@ __global__ __launch_bounds__(256) void sq_total_kernel(int64_t n, const float* _
 // gradients of E[pos[b]] / E[neg[b]] are written per pair ([2B][D]: no atomics
 // into a [U][D] dE) and the per-row loss terms kept for an ordered sum: E is
 // the token LN's output, so those rows only feed pair_ln_kernel.  One wave per row.
+template <typename TT>
 __global__ __launch_bounds__(256) void cos_pairs_kernel(int64_t B, const float* __restrict__ users,
-                                                        const float* __restrict__ xh, const float* __restrict__ tg,
+                                                        const TT* __restrict__ tok, float* __restrict__ xpair,
+                                                        const float* __restrict__ tg,
                                                         const float* __restrict__ tb, const int32_t* __restrict__ pos,
                                                         const int32_t* __restrict__ neg, float margin,
                                                         float* __restrict__ lrow, float* __restrict__ du,
@@ -217,16 +258,17 @@ __global__ __launch_bounds__(256) void cos_pairs_kernel(int64_t B, const float* 
   if (b >= B) return;
   float u[4][4], ep[4][4], en[4][4];
   float uu = 0.f, pp = 0.f, nn = 0.f, up = 0.f, un = 0.f;
-  // E[n] = xhat[n] gamma + beta (the token LN's output), as slots_kernel forms S
-  const float* pr = xh + (int64_t)pos[b] * D;
-  const float* qr = xh + (int64_t)neg[b] * D;
+  // E[n] = xhat[n] gamma + beta (the token LN's output), as slots_kernel forms S;
+  // the pairs' xhat rows kept for pair_ln_kernel (xpair [2B][D]: pos rows, then neg)
+  tok_xhat<TT>(tok + (int64_t)pos[b] * D, lane, ep);
+  tok_xhat<TT>(tok + (int64_t)neg[b] * D, lane, en);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int e = j * 256 + lane * 4;
     float gg[4], bb[4];
+    st4<float>(xpair + b * D + e, ep[j]);
+    st4<float>(xpair + (B + b) * D + e, en[j]);
     ld4<float>(users + b * D + e, u[j]);
-    ld4<float>(pr + e, ep[j]);
-    ld4<float>(qr + e, en[j]);
     ld4<float>(tg + e, gg);
     ld4<float>(tb + e, bb);
 #pragma unroll
@@ -282,8 +324,7 @@ __global__ __launch_bounds__(256) void cos_pairs_kernel(int64_t B, const float* 
 // the ordered (fixed tree) sum of the per-row terms.
 constexpr int kPairChunks = 8;
 __global__ __launch_bounds__(256) void pair_ln_kernel(int64_t B, const float* __restrict__ gpair,
-                                                      const float* __restrict__ xh, const int32_t* __restrict__ pos,
-                                                      const int32_t* __restrict__ neg, const float* __restrict__ lrow,
+                                                      const float* __restrict__ xpair, const float* __restrict__ lrow,
                                                       float* __restrict__ part, float* __restrict__ loss) {
   __shared__ float red[2][4][64];
   const int grp = threadIdx.x >> 6, cl = threadIdx.x & 63;
@@ -292,9 +333,8 @@ __global__ __launch_bounds__(256) void pair_ln_kernel(int64_t B, const float* __
   float sg = 0.f, sb = 0.f;
 #pragma unroll 4
   for (int64_t r = (int64_t)blockIdx.y + kPairChunks * grp; r < 2 * B; r += step) {
-    const int64_t news = r < B ? pos[r] : neg[r - B];
     const float gv = gpair[r * D + c];
-    sg = fmaf(gv, xh[news * D + c], sg);
+    sg = fmaf(gv, xpair[r * D + c], sg);
     sb += gv;
   }
   red[0][grp][cl] = sg;
@@ -392,7 +432,7 @@ __global__ __launch_bounds__(256) void rowsum_kernel(RSum r, float* __restrict__
 // ------------------------------------------------------------------ workspace
 struct Layout {
   int64_t Hp, es, mm, csr;
-  int64_t XHu, S, XH, X1, X2, XP, Y, users, z, du, gpair, lrow, dXp, dL, dY, dX, dZ2, dZ1, w1p, sqp;
+  int64_t xpair, S, XH, X1, X2, XP, Y, users, z, du, gpair, lrow, dXp, dL, dY, dX, dZ2, dZ1, w1p, sqp;
   int64_t W1t, W2t, W3t, W4t, W5t, skP, cs4, cs3, cs2, cs1;
   int64_t T[10];  // f32 mode: the weight-grad operands transposed
   int64_t total;
@@ -418,7 +458,7 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs, int ncu) {
   const int64_t Hp = L.Hp, es = L.es, Bp = pad64(B);
   int64_t o = 0;
   auto take = [&](int64_t bytes) { const int64_t r = o; o += al(bytes); return r; };
-  L.XHu = take(U * D * 4);
+  L.xpair = take(2 * B * D * 4);
   L.S = take(Hp * D * es); L.XH = take(Hp * D * es); L.X1 = take(Hp * H * es); L.X2 = take(Hp * H * es); L.XP = take(Hp * 2 * D * es);
   L.Y = take(Hp * H * es);
   L.users = take(Bp * D * 4); L.z = take(Bp * D * 4); L.du = take(Bp * D * 4); L.gpair = take(2 * B * D * 4);
@@ -467,9 +507,9 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   const int dt = a.dtype;
   const int ncu = ncu_of(st);
   const Layout L = layout(dt, a.B, a.U, a.Hs, ncu);
-  const int64_t B = a.B, U = a.U, Hs = a.Hs, Hp = L.Hp, mm = L.mm;
+  const int64_t B = a.B, Hs = a.Hs, Hp = L.Hp, mm = L.mm;
   auto P_ = [&](int64_t off) { return (void*)(ws + off); };
-  float* XHu = (float*)P_(L.XHu);
+  float* xpair = (float*)P_(L.xpair);
   TA* XH = (TA*)P_(L.XH);
   TA *S = (TA*)P_(L.S), *X1 = (TA*)P_(L.X1), *X2 = (TA*)P_(L.X2), *XP = (TA*)P_(L.XP), *Y = (TA*)P_(L.Y);
   float* users = a.users ? a.users : (float*)P_(L.users);
@@ -510,12 +550,17 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
     NR_CHECK_LAUNCH("nr_final_train_step (zero)");
   }
   // ---- forward
-  // xhat of the U token rows (LN without the affine), then the slots' S and XH
-  NR_FT(gather_ln_dispatch(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1, nullptr, nullptr, 1e-12f, XHu, D, st));
+  // the slots' S and XH: the token LN of each slot's news (one kernel, no [U][D] table)
   {
     const int64_t g = (Hp + 3) / 4;
-    hipLaunchKernelGGL((slots_kernel<TA>), dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, Hp, Hs, XHu,
-                       a.hist_idx, a.tok_g, a.tok_b, S, XH);
+    const dim3 grid((unsigned)(g < 4096 ? g : 4096));
+#define NR_FT_TOK(TT) \
+    hipLaunchKernelGGL((slots_kernel<TA, TT>), grid, dim3(256), 0, st, Hp, Hs, (const TT*)a.tok_last, a.hist_idx, \
+                       a.tok_g, a.tok_b, S, XH)
+    if (a.tok_dtype == NR_F32) NR_FT_TOK(float);
+    else if (a.tok_dtype == NR_BF16) NR_FT_TOK(__bf16);
+    else NR_FT_TOK(_Float16);
+#undef NR_FT_TOK
     NR_CHECK_LAUNCH("nr_final_train_step (slots)");
   }
   // relu(dropout) GEMM over Hp rows: main rows on the persistent kernel, the tail as K-slices + fixup
@@ -538,12 +583,20 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   NR_FT(gemm_dispatch(dt, dt, NR_EPI_EXP, Hp, D, H, Y, H, W5, H, nullptr, nullptr, 0, Pexp, 2 * D, st));
   NR_FT(nr_final_pool_fwd(dt, B, a.hist_off, XP, 2 * D, users, z, st));
   // ---- loss and its gradient into the pooled users and E[pos] / E[neg]
-  hipLaunchKernelGGL(cos_pairs_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, users, XHu, a.tok_g,
-                     a.tok_b, a.pos, a.neg, a.margin, lrow, du, gpair);
+  {
+    const dim3 grid((unsigned)((B + 3) / 4));
+#define NR_FT_TOK(TT) \
+    hipLaunchKernelGGL((cos_pairs_kernel<TT>), grid, dim3(256), 0, st, B, users, (const TT*)a.tok_last, xpair, \
+                       a.tok_g, a.tok_b, a.pos, a.neg, a.margin, lrow, du, gpair)
+    if (a.tok_dtype == NR_F32) NR_FT_TOK(float);
+    else if (a.tok_dtype == NR_BF16) NR_FT_TOK(__bf16);
+    else NR_FT_TOK(_Float16);
+#undef NR_FT_TOK
+  }
   NR_CHECK_LAUNCH("nr_final_train_step (cosine)");
   // the pairs' token LN grad partials (after the W1 fold's chunks) and the loss
-  hipLaunchKernelGGL(pair_ln_kernel, dim3((unsigned)(D / 64), kPairChunks), dim3(256), 0, st, B, gpair, XHu, a.pos,
-                     a.neg, lrow, (float*)P_(L.w1p) + (H / 64) * 2 * D, a.loss);
+  hipLaunchKernelGGL(pair_ln_kernel, dim3((unsigned)(D / 64), kPairChunks), dim3(256), 0, st, B, gpair, xpair, lrow,
+                     (float*)P_(L.w1p) + (H / 64) * 2 * D, a.loss);
   NR_CHECK_LAUNCH("nr_final_train_step (pair LN grads)");
   NR_FT(nr_final_pool_bwd(dt, B, a.hist_off, Hp, XP, 2 * D, users, z, du, dXp, D, dL, D, st));
   // ---- data-grad chain (weights transposed on the side stream)
