@@ -527,16 +527,18 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   TrainSide side;
   NR_FT(train_side_streams(st, "nr_final_train_step", side));
 
-  // ---- fork: the weight transposes the data-grad GEMMs need, beside the forward
-  NR_FT_EV(hipEventRecord(side.fork, st), "fork record");
-  NR_FT_EV(hipStreamWaitEvent(side.s, side.fork, 0), "fork wait");
-  {
+  // ---- the weight transposes the data-grad GEMMs need, on the side stream beside
+  // the two N = 1024 forward GEMMs (X, P: 132 tiles, half of the CUs idle) rather
+  // than beside the full-chip ones; joined (event wt) before the first data-grad GEMM
+  auto transposes = [&](int i0, int i1, hipEvent_t fork) -> int {
     const TA* w[5] = {W5, W4, W3, W2, W1};
     TA* t[5] = {W5t, W4t, W3t, W2t, W1t};
     const int64_t r[5] = {D, H, D, H, H}, c[5] = {H, D, H, H, D};  // W5 [D][H], W4 [H][D], W3 [D][H], W2, W1 [H][D]
-    for (int i = 0; i < 5; ++i) NR_FT(nr_transpose(dt, dt, r[i], c[i], w[i], c[i], t[i], r[i], side.s));
-  }
-  NR_FT_EV(hipEventRecord(side.wt, side.s), "transpose record");
+    NR_FT_EV(hipEventRecord(fork, st), "fork record");
+    NR_FT_EV(hipStreamWaitEvent(side.s, fork, 0), "fork wait");
+    for (int i = i0; i < i1; ++i) NR_FT(nr_transpose(dt, dt, r[i], c[i], w[i], c[i], t[i], r[i], side.s));
+    return NR_OK;
+  };
 
   // ---- accumulators: f32 mode's bias grads (nr_col_sum adds); everything else is
   // written whole (the loss and token LN grads by ordered sums, no atomics)
@@ -578,8 +580,11 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   };
   NR_FT(relu_gemm(S, D, W1, D, a.b1, a.seed[0], X1, H));
   NR_FT(relu_gemm(X1, H, W2, H, a.b2, a.seed[1], X2, H));
+  NR_FT(transposes(0, 3, side.fork));  // W5^T, W4^T, W3^T beside X
   NR_FT(gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, H, X2, H, W3, H, a.b3, nullptr, 0, X, 2 * D, st));
   NR_FT(relu_gemm(X, 2 * D, W4, D, a.b4, a.seed[2], Y, H));
+  NR_FT(transposes(3, 5, side.fork2));  // W2^T, W1^T beside P
+  NR_FT_EV(hipEventRecord(side.wt, side.s), "transpose record");
   NR_FT(gemm_dispatch(dt, dt, NR_EPI_EXP, Hp, D, H, Y, H, W5, H, nullptr, nullptr, 0, Pexp, 2 * D, st));
   NR_FT(nr_final_pool_fwd(dt, B, a.hist_off, XP, 2 * D, users, z, st));
   // ---- loss and its gradient into the pooled users and E[pos] / E[neg]
