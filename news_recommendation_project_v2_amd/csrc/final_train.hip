@@ -32,8 +32,11 @@
 // weight-grad GEMMs as ONE grouped TN launch that reads the row-major
 // activations through transposed LDS reads (no transposed copies); the five
 // weight transposes the data-grad GEMMs need on a side stream beside the
-// forward.  f32 (the parity mode): the same sequence on the exact-f32 MFMA tile
-// kernels, with explicit transposes for the weight grads.
+// forward's two N = 1024 GEMMs.  The token LN (E) is never stored as a [U][D]
+// table: the slot kernel computes it per history slot from the token states,
+// the cosine kernel per pos / neg row.  f32 (the parity mode): the same sequence
+// on the exact-f32 MFMA tile kernels, with explicit transposes for the weight
+// grads.
 #include "nr_common.h"
 
 namespace nr {
