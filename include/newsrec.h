@@ -528,6 +528,8 @@ typedef struct nr_latent_train_args {
   /* outputs */
   float* loss;  /* device scalar (set, not accumulated) */
   float* users; /* nullable [B][1024] */
+  float* sumsq; /* nullable device scalar: set to the squared L2 norm of all the
+                   gradients above (the clip's input to nr_adamw) */
 } nr_latent_train_args;
 
 int64_t nr_latent_train_workspace_bytes(int dtype, int64_t B, int64_t U, int64_t Hs);

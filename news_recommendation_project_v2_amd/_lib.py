@@ -150,7 +150,7 @@ class LatentTrainArgs(ctypes.Structure):
                  ("Hs", ctypes.c_int64)]
                 + [(n, ctypes.c_void_p) for n in ("tok_last", "hist_idx", "hist_off", "pos", "neg")]
                 + [("margin", ctypes.c_float)]
-                + [(n, ctypes.c_void_p) for n in LATENT_TRAIN_PARAMS + LATENT_TRAIN_GRADS + ("loss", "users")])
+                + [(n, ctypes.c_void_p) for n in LATENT_TRAIN_PARAMS + LATENT_TRAIN_GRADS + ("loss", "users", "sumsq")])
 
 
 FINAL_TRAIN_PARAMS = ("tok_g", "tok_b", "W1", "b1", "W2", "b2", "W3", "b3", "W4", "b4", "W5")

@@ -656,7 +656,7 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
     float* sqp = a.sumsq ? (float*)P_(L.sqp) : nullptr;
     const bool sqf[5] = {true, true, true, true, false};  // dW1 is M here: counted by the fold
     int ntiles = 0;
-    NR_FT(gemm_group_tn_dispatch(NR_F32, p, 5, st, sqp, sqf, &ntiles));
+    NR_FT(gemm_group_tn_dispatch(NR_F32, p, 5, st, sqp, sqf, &ntiles, kSqTn));
     if (sqp && ntiles != kSqTn) {
       set_error("nr_final_train_step: %d weight-grad tiles (expected %d)", ntiles, kSqTn);
       return NR_ERR_INVALID;

@@ -779,7 +779,8 @@ __global__ __launch_bounds__(512, 2) void gemm256p_group_kernel(GemmGroup g) {
                                                (TO*)g.C[p] + b * g.sC[p], g.ldc[p], ea);
 }
 
-int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, int n, hipStream_t s) {
+int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, int n, hipStream_t s, float* sq_part,
+                        const bool* sq, int* n_tiles, int sq_cap) {
   NR_CHECK_ARG(dtype_in == NR_BF16 || dtype_in == NR_F32, "gemm_group: bad dtype_in %d", dtype_in);
   NR_CHECK_ARG(dtype_out == NR_F32 || dtype_out == NR_BF16, "gemm_group: bad dtype_out %d", dtype_out);
   NR_CHECK_ARG(n >= 0 && n <= kGroupMax, "gemm_group: n=%d outside [0, %d]", n, kGroupMax);
@@ -805,6 +806,7 @@ int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, i
     g.lda[j] = q.lda; g.ldw[j] = q.ldw; g.ldc[j] = q.ldc;
     g.sA[j] = q.sA; g.sW[j] = q.sW; g.sC[j] = q.sC;
     g.alpha[j] = q.alpha;
+    g.sq[j] = sq ? sq[i] : false;
     g.ntn[j] = (int)(q.N / G2BN);
     const int64_t tpb = ((q.M + G2BM - 1) / G2BM) * g.ntn[j];
     NR_CHECK_ARG(tpb <= 0x7fffffff, "gemm_group: too many tiles");
@@ -813,7 +815,11 @@ int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, i
     NR_CHECK_ARG(tiles <= 0x7fffffff, "gemm_group: too many tiles");
     g.tile_end[j] = (int)tiles;
   }
+  if (n_tiles) *n_tiles = (int)tiles;
   if (g.n == 0) return NR_OK;
+  NR_CHECK_ARG(!sq_part || tiles <= sq_cap, "gemm_group: %lld workgroups exceed the %d sum-of-squares slots",
+               (long long)tiles, sq_cap);
+  g.sq_part = sq_part;
   if (dtype_in == NR_F32 && dtype_out == NR_F32)
     hipLaunchKernelGGL((gemm256p_group_kernel<float, float, false>), dim3((unsigned)tiles), dim3(512), 0, s, g);
   else if (dtype_in == NR_F32)
@@ -832,11 +838,10 @@ int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, i
 // activations.  Batches (sA / sW / sC) give split-K slices: A + b sA is K-rows
 // b kw.. of the same activation.  M, N multiples of 256, K of 64.
 int gemm_group_tn_dispatch(int dtype_out, const GemmProblem* probs, int n, hipStream_t s, float* sq_part,
-                           const bool* sq, int* n_tiles) {
+                           const bool* sq, int* n_tiles, int sq_cap) {
   NR_CHECK_ARG(dtype_out == NR_F32 || dtype_out == NR_BF16, "gemm_group_tn: bad dtype_out %d", dtype_out);
   NR_CHECK_ARG(n >= 0 && n <= kGroupMax, "gemm_group_tn: n=%d outside [0, %d]", n, kGroupMax);
   GemmGroup g{};
-  g.sq_part = sq_part;
   int64_t tiles = 0;
   const int64_t vo = dtype_out == NR_F32 ? 4 : 8;
   for (int i = 0; i < n; ++i) {
@@ -867,6 +872,9 @@ int gemm_group_tn_dispatch(int dtype_out, const GemmProblem* probs, int n, hipSt
   }
   if (n_tiles) *n_tiles = (int)tiles;
   if (g.n == 0) return NR_OK;
+  NR_CHECK_ARG(!sq_part || tiles <= sq_cap, "gemm_group_tn: %lld workgroups exceed the %d sum-of-squares slots",
+               (long long)tiles, sq_cap);
+  g.sq_part = sq_part;
   if (dtype_out == NR_F32)
     hipLaunchKernelGGL((gemm256p_group_kernel<__bf16, float, true, true>), dim3((unsigned)tiles), dim3(512), 0, s, g);
   else

@@ -124,9 +124,72 @@ __device__ __forceinline__ float block_sum(float v, float* scratch /* [4] */) {
 // zero up to 16 f32 ranges in one launch (the step's accumulated gradients)
 struct ZList {
   int n;
-  float* p[16];
-  int64_t len[16];
+  float* p[17];
+  int64_t len[17];
 };
+
+// *out += sum over up to 8 f32 ranges of their squares (gradients a stream of the step
+// finished writing) or, for ranges added with square = false, of their values (the
+// per-workgroup sums of squares a weight-grad GEMM's epilogue left); 16-B lane
+// loads, one atomic per block.  The clip's norm so needs no pass over the whole
+// gradient buffer after the step's last kernel.
+struct SqList {
+  int n = 0;
+  const float* p[8];
+  int64_t len[8];
+  bool square[8];
+  void add(const float* x, int64_t l, bool sq = true) { p[n] = x; len[n] = l; square[n] = sq; ++n; }
+};
+__global__ __launch_bounds__(256) void sq_list_kernel(SqList q, float* __restrict__ out) {
+  __shared__ float part[4];
+  float s = 0.f;
+  const int64_t gs = (int64_t)gridDim.x * 256, t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int r = 0; r < q.n; ++r) {
+    const float* x = q.p[r];
+    const int64_t n = q.len[r];
+    if (!q.square[r]) {  // a few hundred GEMM-epilogue partials
+      for (int64_t k = t; k < n; k += gs) s += x[k];
+      continue;
+    }
+    const int64_t n4 = ((uintptr_t)x & 15) == 0 ? n / 4 : 0;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    int64_t i = t;
+    for (; i + 3 * gs < n4; i += 4 * gs) {
+      float4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = x4[i + k * gs];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s = fmaf(v[k].x, v[k].x, s);
+        s = fmaf(v[k].y, v[k].y, s);
+        s = fmaf(v[k].z, v[k].z, s);
+        s = fmaf(v[k].w, v[k].w, s);
+      }
+    }
+    for (; i < n4; i += gs) {
+      const float4 v = x4[i];
+      s = fmaf(v.x, v.x, s);
+      s = fmaf(v.y, v.y, s);
+      s = fmaf(v.z, v.z, s);
+      s = fmaf(v.w, v.w, s);
+    }
+    for (int64_t k = 4 * n4 + t; k < n; k += gs) s = fmaf(x[k], x[k], s);
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, (part[0] + part[1]) + (part[2] + part[3]));
+}
+
+static int sq_list(const SqList& q, float* out, hipStream_t st) {
+  if (!out || q.n == 0) return NR_OK;
+  int64_t n = 0;
+  for (int i = 0; i < q.n; ++i) n += q.len[i];
+  const int64_t g = (n / 4 + 1023) / 1024;  // ~4 float4 per thread
+  hipLaunchKernelGGL(sq_list_kernel, dim3((unsigned)(g < 1 ? 1 : g < 1024 ? g : 1024)), dim3(256), 0, st, q, out);
+  NR_CHECK_LAUNCH("nr_latent_train_step (grad sumsq)");
+  return NR_OK;
+}
 __global__ __launch_bounds__(256) void zero_kernel(ZList z) {
   for (int i = 0; i < z.n; ++i)
     for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < z.len[i]; k += (int64_t)gridDim.x * 256)
@@ -901,6 +964,9 @@ constexpr int kZParts = 4;     // split-K slices of dZ = dmc W2 (K = 1024 -> 256
 constexpr int kGRows = 16;     // slot rows per GEGLU-backward block
 constexpr int kWParts = 8;     // split-K slices of dA / dBt (K = Hp -> Hpp / 8)
 constexpr int kLatParts = 32;  // split-K slices of dlatents' GEMM (K = 8192 -> 256)
+// per-workgroup sum-of-squares slots of the weight-grad GEMMs (the clip's norm):
+// dW1 / dW2 (192 workgroups), the fold group (160), dWkv + dlatents (256)
+constexpr int kSqW12 = 0, kSqFold = 320, kSqKv = 512, kSqSlots = 832;
 
 // Workspace layout (byte offsets), shared by the size query and the step.
 struct Layout {
@@ -909,7 +975,7 @@ struct Layout {
       dS, dX, dE;
   int64_t dGT, YT, dH1T, PT, dST, XT, dmT, zbarT;
   int64_t WqT, W1T, W2T, WoT, WkvT, latn, latnT, KVp, KV, KVT, A, AT, BtT, Bt;
-  int64_t gA, gBt, gA16, gAT16, gBt16, gBtT16, dKV, dKV16, dKVT16, dlat;
+  int64_t gA, gBt, gA16, gAT16, gBt16, gBtT16, dKV, dKV16, dKVT16, dlat, sqp;
   int64_t total;
 };
 
@@ -947,6 +1013,7 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs) {
   L.gA16 = take(S * D * es); L.gAT16 = take(D * S * es); L.gBt16 = take(D * S * es); L.gBtT16 = take(S * D * es);
   L.dKV = take(NL * 2 * F * 4); L.dKV16 = take(NL * 2 * F * es); L.dKVT16 = take(2 * F * NL * es);
   L.dlat = take((int64_t)kLatParts * NL * D * 4);
+  L.sqp = take(kSqSlots * 4);
   L.total = o;
   return L;
 }
@@ -989,6 +1056,8 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   float* dKV = (float*)P_(L.dKV);
   TA *dKV16 = (TA*)P_(L.dKV16), *dKVT16 = (TA*)P_(L.dKVT16);
   float* dlat = (float*)P_(L.dlat);
+  float* sqp = a.sumsq ? (float*)P_(L.sqp) : nullptr;  // GEMM-epilogue sum-of-squares slots
+  int n_sq12 = 0, n_sqf = 0, n_sqkv = 0;
   const TA *Wq = (const TA*)a.Wq, *Wkv = (const TA*)a.Wkv, *Wo = (const TA*)a.Wo, *W1 = (const TA*)a.W1,
            *W2 = (const TA*)a.W2;
   const float scale = 1.0f / sqrtf((float)DH);  // SDPA default scale (latent_attention.py:72)
@@ -1020,6 +1089,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     z.p[14] = (float*)(dH1 + Hp * D); z.len[14] = tail * D;
     z.p[15] = (float*)(dS + Hp * S); z.len[15] = tail * S;
     z.n = 16;
+    if (a.sumsq) { z.p[16] = a.sumsq; z.len[16] = 1; z.n = 17; }
     hipLaunchKernelGGL(zero_kernel, dim3(1024), dim3(256), 0, st, z);
     NR_LT_CHECK("zero");
   }
@@ -1132,7 +1202,10 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
         {2 * F, D, Hp, dG, 2 * F, 0, Y, D, 0, a.g_W1, D, 0, 1, 1.0f},
         {D, F, Bp, dmA, D, 0, zbar, F, 0, a.g_W2, F, 0, 1, 1.0f},
     };
-    if ((rc = gemm_group_tn_dispatch(NR_F32, p, 2, side.s))) return rc;
+    const bool sqf[2] = {true, true};
+    if ((rc = gemm_group_tn_dispatch(NR_F32, p, 2, side.s, sqp ? sqp + kSqW12 : nullptr, sqf, &n_sq12,
+                                     kSqFold - kSqW12)))
+      return rc;
   } else {
     TList t;
     t.add(dG, 2 * F, dGT, Hp, Hp, 2 * F, true);
@@ -1144,7 +1217,10 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
         {2 * F, D, Hp, dGT, Hp, 0, YT, Hp, 0, a.g_W1, D, 0, 1, 1.0f},
         {D, F, Bp, dmT, Bp, 0, zbarT, Bp, 0, a.g_W2, F, 0, 1, 1.0f},
     };
-    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, side.s))) return rc;
+    const bool sqf[2] = {true, true};
+    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, side.s, sqp ? sqp + kSqW12 : nullptr, sqf, &n_sq12,
+                                  kSqFold - kSqW12)))
+      return rc;
   }
   {
     if (hipEventRecord(side.join, side.s) != hipSuccess) {
@@ -1184,6 +1260,14 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   // token LayerNorm parameter grads from dE (history scatter + cosine grads)
   if ((rc = nr_ln_param_grad(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1e-12f, dE, D, a.g_tok_g, a.g_tok_b, st)))
     return rc;
+  {
+    // this stream's gradients are all final here
+    SqList q;
+    const float* gp[] = {a.g_tok_g, a.g_tok_b, a.g_nq_g, a.g_nq_b, a.g_nf_g, a.g_nf_b, a.g_b1, a.g_b2};
+    const int64_t gn[] = {D, D, D, D, D, D, 2 * F, D};
+    for (int i = 0; i < 8; ++i) q.add(gp[i], gn[i]);
+    if ((rc = sq_list(q, a.sumsq, st))) return rc;
+  }
   hipStream_t s2 = side.s2;
   // ---- dA = dS^T X and dBt = dH1^T P as kWParts K-slices (16 + 16 tiles alone would hold 32 CUs
   // for a K = Hp tile time), summed while converting to the fold backward's operands
@@ -1229,7 +1313,9 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
         // dWo_h [1024, 512] = gBt_h V_h: A = gBt cols h*64 [1024, 64], W = VT rows h*512 [512, 64]
         {D, DH, NL, gBt16, S, NL, KVT + (int64_t)F * NL, NL, (int64_t)DH * NL, a.g_Wo, F, DH, HEADS, 1.0f},
     };
-    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 4, s2))) return rc;
+    const bool sqf[4] = {true, false, false, true};  // dWq, dWo
+    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 4, s2, sqp ? sqp + kSqFold : nullptr, sqf, &n_sqf, kSqKv - kSqFold)))
+      return rc;
   }
   {
     SCList t;
@@ -1244,7 +1330,9 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
         // dlatn [64, 1024] = dKV Wkv, split-K: A = dKV16 cols, W = WkvT cols
         {NL, D, ks, dKV16, 2 * F, ks, WkvT, 2 * F, ks, dlat, D, (int64_t)NL * D, kLatParts, 1.0f},
     };
-    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, s2))) return rc;
+    const bool sqf[2] = {true, false};  // dWkv
+    if ((rc = gemm_group_dispatch(dt, NR_F32, p, 2, s2, sqp ? sqp + kSqKv : nullptr, sqf, &n_sqkv, kSqSlots - kSqKv)))
+      return rc;
   }
   if ((rc = sum_parts(dlat, kLatParts, (int64_t)NL * D, dlat, (int64_t)NL * D, s2))) return rc;
   hipLaunchKernelGGL(lnc_bwd_kernel, dim3(NL / 4), dim3(256), 0, s2, a.latents, a.nc_g, 1e-5f, 1, dlat,
@@ -1258,6 +1346,19 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   if (hipStreamWaitEvent(st, side.join, 0) != hipSuccess || hipStreamWaitEvent(st, side.join2, 0) != hipSuccess) {
     set_error("nr_latent_train_step: join failed");
     return NR_ERR_HIP;
+  }
+  if (sqp) {
+    // the side streams' weight grads: their GEMM-epilogue partials and the squares of
+    // the small fold grads (here, not on s2: the optimizer that follows on this stream
+    // then starts without a second cross-stream wait)
+    SqList q;
+    q.add(sqp + kSqW12, n_sq12, false);
+    q.add(sqp + kSqFold, n_sqf, false);
+    q.add(sqp + kSqKv, n_sqkv, false);
+    q.add(a.g_latents, NL * D);
+    q.add(a.g_nc_g, D);
+    q.add(a.g_nc_b, D);
+    if ((rc = sq_list(q, a.sumsq, st))) return rc;
   }
 #undef NR_LT_CHECK
   return NR_OK;
@@ -1320,7 +1421,8 @@ extern "C" int nr_latent_train_step(const nr_latent_train_args* args, void* ws, 
   NR_CHECK_DEVICE("nr_latent_train_step", a.tok_last, a.hist_idx, a.hist_off, a.pos, a.neg, a.tok_g, a.tok_b,
                   a.latents, a.nq_g, a.nq_b, a.nc_g, a.nc_b, a.Wq, a.Wkv, a.Wo, a.nf_g, a.nf_b, a.W1, a.b1, a.W2, a.b2);
   NR_CHECK_DEVICE("nr_latent_train_step", a.g_tok_g, a.g_tok_b, a.g_latents, a.g_nq_g, a.g_nq_b, a.g_nc_g, a.g_nc_b,
-                  a.g_Wq, a.g_Wkv, a.g_Wo, a.g_nf_g, a.g_nf_b, a.g_W1, a.g_b1, a.g_W2, a.g_b2, a.loss, a.users, ws);
+                  a.g_Wq, a.g_Wkv, a.g_Wo, a.g_nf_g, a.g_nf_b, a.g_W1, a.g_b1, a.g_W2, a.g_b2, a.loss, a.users, a.sumsq,
+                  ws);
   NR_CHECK_ARG(a.tok_last && a.hist_idx && a.hist_off && a.pos && a.neg && a.loss && ws,
                "nr_latent_train_step: null pointer");
   const int64_t need = nr::lt::layout(a.dtype, a.B, a.U, a.Hs).total;

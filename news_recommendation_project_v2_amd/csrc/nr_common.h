@@ -86,12 +86,18 @@ struct GemmProblem {
   float alpha;
 };
 constexpr int kGroupMax = 16;
-int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, int n, hipStream_t s);
+// sq_part (nullable): per-workgroup sums of squares of the problems flagged in sq (0 for
+// the others), one per workgroup; refused before launch when the workgroup count
+// exceeds sq_cap; *n_tiles (nullable) = the workgroup count.
+int gemm_group_dispatch(int dtype_in, int dtype_out, const GemmProblem* probs, int n, hipStream_t s,
+                        float* sq_part = nullptr, const bool* sq = nullptr, int* n_tiles = nullptr,
+                        int sq_cap = 0);
 // C = alpha A^T W per problem, A [K][M] and W [K][N] bf16 row-major (gemm.hip, TN grouped launch)
 // sq_part (nullable): per-workgroup sums of squares of the problems flagged in sq
-// (0 for the others), one per workgroup; *n_tiles (nullable) = the workgroup count.
+// (0 for the others), one per workgroup, refused before launch past sq_cap workgroups;
+// *n_tiles (nullable) = the workgroup count.
 int gemm_group_tn_dispatch(int dtype_out, const GemmProblem* probs, int n, hipStream_t s, float* sq_part = nullptr,
-                           const bool* sq = nullptr, int* n_tiles = nullptr);
+                           const bool* sq = nullptr, int* n_tiles = nullptr, int sq_cap = 0);
 int inv_norm_dispatch(int dtype, int64_t rows, int64_t dim, const void* x, int64_t ldx, float eps,
                       float* out, hipStream_t s);
 

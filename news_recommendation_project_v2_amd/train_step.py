@@ -313,7 +313,7 @@ class LatentAttentionTrainStep:
       per batch row:    m = mean(Z) W2ᵀ + b2 + mean(H1)  (the last linear layer commutes
                         with the history mean: its three GEMMs run over B rows, not slots)
       users = normalize(m); loss = MarginRankingLoss(2)(cos(users, E[pos]), cos(users, E[neg]))
-      backward of all of it; clip_grad_norm_(0.5) + AdamW   nr_sumsq, nr_adamw
+      backward of all of it; clip_grad_norm_(0.5) + AdamW   (grad norm in the step), nr_adamw
 
     dtype float32: exact-f32 MFMA GEMMs and f32 activations (the parity mode);
     bfloat16: bf16 operands and activations with f32 accumulation, statistics
@@ -411,7 +411,7 @@ class LatentAttentionTrainStep:
             setattr(a, f, src.data_ptr())
             setattr(a, "g_" + f, self.gviews[name].data_ptr())
         loss = self.loss if loss_out is None else _check_loss_out(loss_out, self.device)
-        a.loss, a.users = loss.data_ptr(), self._users.data_ptr()
+        a.loss, a.users, a.sumsq = loss.data_ptr(), self._users.data_ptr(), self.sumsq.data_ptr()
         # (no grad.zero_(): the step writes every gradient and zeroes its own accumulators;
         # the flat buffer's alignment gaps were zeroed at construction and are never written)
         _lib.check(lib.nr_latent_train_step(ctypes.byref(a), self._ws.data_ptr(), self._ws.numel(),
@@ -421,11 +421,11 @@ class LatentAttentionTrainStep:
         return loss, self._users[:B], None
 
     def optimizer_step(self) -> None:
-        """clip_grad_norm_(max_norm) + AdamW, one launch each (trainer.py:1067-1069);
-        the bf16 mode's weight mirror is rewritten by the same AdamW launch."""
+        """clip_grad_norm_(max_norm) + AdamW in one launch (trainer.py:1067-1069): the
+        squared grad norm was summed by the step itself (``sumsq``, each stream over
+        the gradients it wrote); the bf16 mode's weight mirror is rewritten by the
+        same AdamW launch."""
         self.step_count += 1
-        self.sumsq.zero_()
-        ops.sumsq(self.grad, self.sumsq)
         ops.adamw(self.flat, self.grad, self.m, self.v, self.step_count, self.lr, self.betas, self.eps, self.wd,
                   self.max_norm, self.sumsq if self.max_norm > 0 else None, self.flat16)
         if hasattr(self.model, "_hip_cache"):
