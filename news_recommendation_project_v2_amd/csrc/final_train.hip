@@ -356,35 +356,51 @@ __global__ __launch_bounds__(256) void pair_ln_kernel(int64_t B, const float* __
   }
 }
 
-// out[r0 / 128 + b][c] = sum of rows [r0 + 128 b, r0 + 128 (b + 1)) of src's column c
-// (rows < rows_end): the column sums of a split-K tail's rows, in the layout of
-// the persistent GEMM's CS partials.  Block = 256 columns x one 128-row block:
-// 8 row groups of 32 lanes x 8 columns (16-B loads), folded in LDS in a fixed order.
+// A DRELU split-K tail in one launch: C = drop'(sum_s P[s] + 0) against the forward
+// output R, as nr_splitk_fixup's DRELU (the same f32 sum order and rounding), and
+// the stored values' column sums per 32-row block into CS row cs_row0 + block (the
+// tail's rows of the CS layout, after the persistent GEMM's 128-row ones), folded
+// in LDS in a fixed order.  Block = 64 columns (8 lanes x 8) x 32 rows, one row
+// per thread: 256 blocks for a 128-row tail of N = 4096.
 template <typename TA>
-__global__ __launch_bounds__(256) void colsum_block_kernel(int64_t r0, int64_t rows_end, int64_t cols, const TA* src,
-                                                           int64_t lds, float* out) {
-  __shared__ float red[8][256];
-  const int grp = threadIdx.x >> 5, cl = threadIdx.x & 31;
-  const int64_t c = (int64_t)blockIdx.x * 256 + 8 * cl;
-  const int64_t b0 = r0 + (int64_t)blockIdx.y * 128;
-  const int64_t e = b0 + 128 < rows_end ? b0 + 128 : rows_end;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-  for (int64_t r = b0 + grp; r < e; r += 8) {
-    float v[4], w[4];
-    ld4<TA>(src + r * lds + c, v);
-    ld4<TA>(src + r * lds + c + 4, w);
+__global__ __launch_bounds__(256) void fixup_drelu_cs_kernel(int64_t cs_row0, int64_t rows, int64_t N, int parts,
+                                                             const float* __restrict__ P, const TA* __restrict__ R,
+                                                             int64_t ldr, TA* __restrict__ C, int64_t ldc, float scale,
+                                                             float* __restrict__ cs) {
+  __shared__ float red[32][64];
+  const int rg = threadIdx.x >> 3, cl = threadIdx.x & 7;
+  const int64_t c = (int64_t)blockIdx.x * 64 + 8 * cl;
+  const int64_t r = (int64_t)blockIdx.y * 32 + rg;
+  float y[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (r < rows) {
+    float v[8], w[8], rv[8];
+    ld4<float>(P + r * N + c, v);
+    ld4<float>(P + r * N + c + 4, v + 4);
+    for (int s = 1; s < parts; ++s) {
+      ld4<float>(P + ((int64_t)s * rows + r) * N + c, w);
+      ld4<float>(P + ((int64_t)s * rows + r) * N + c + 4, w + 4);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) { acc[t] += v[t]; acc[4 + t] += w[t]; }
+      for (int k = 0; k < 8; ++k) v[k] += w[k];
+    }
+    ld4<TA>(R + r * ldr + c, rv);
+    ld4<TA>(R + r * ldr + c + 4, rv + 4);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float x = v[k] + 0.f;  // (no bias: as the fixup's x + 0)
+      y[k] = rv[k] > 0.f ? x * scale : 0.f;
+    }
+    st4<TA>(C + r * ldc + c, y);
+    st4<TA>(C + r * ldc + c + 4, y + 4);
   }
 #pragma unroll
-  for (int t = 0; t < 8; ++t) red[grp][8 * cl + t] = acc[t];
+  for (int k = 0; k < 8; ++k) red[rg][8 * cl + k] = (float)(TA)y[k];  // the stored value
   __syncthreads();
-  const int col = threadIdx.x;
-  float s = 0.f;
+  if (threadIdx.x < 64) {
+    float t = 0.f;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) s += red[k][col];
-  out[(b0 >> 7) * cols + (int64_t)blockIdx.x * 256 + col] = s;
+    for (int k = 0; k < 32; ++k) t += red[k][threadIdx.x];
+    cs[(cs_row0 + blockIdx.y) * N + (int64_t)blockIdx.x * 64 + threadIdx.x] = t;
+  }
 }
 
 // g[c] = sum_r part[r][c] over up to 4 (partials, rows, cols, out) problems: the
@@ -434,7 +450,7 @@ __global__ __launch_bounds__(256) void rowsum_kernel(RSum r, float* __restrict__
 
 // ------------------------------------------------------------------ workspace
 struct Layout {
-  int64_t Hp, es, mm, csr;
+  int64_t Hp, es, mm, csr, csr3;
   int64_t xpair, S, XH, X1, X2, XP, Y, users, z, du, gpair, lrow, dXp, dL, dY, dX, dZ2, dZ1, w1p, sqp;
   int64_t W1t, W2t, W3t, W4t, W5t, skP, cs4, cs3, cs2, cs1;
   int64_t T[10];  // f32 mode: the weight-grad operands transposed
@@ -457,7 +473,11 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs, int ncu) {
   L.Hp = pad64(Hs);
   L.es = dtype == NR_F32 ? 4 : 2;
   L.mm = main_rows(dtype, L.Hp, ncu);
-  L.csr = (L.Hp + 127) / 128;
+  // CS partial rows (bf16 column-sum epilogues): 128-row blocks of the persistent
+  // GEMM over rows [0, mm), then 32-row blocks of a split-K tail (fixup_drelu_cs_kernel);
+  // csr3 for the dX GEMM (N = 1024, no tail split)
+  L.csr3 = (L.Hp + 127) / 128;
+  L.csr = L.mm < L.Hp ? L.mm / 128 + (L.Hp - L.mm + 31) / 32 : L.csr3;
   const int64_t Hp = L.Hp, es = L.es, Bp = pad64(B);
   int64_t o = 0;
   auto take = [&](int64_t bytes) { const int64_t r = o; o += al(bytes); return r; };
@@ -473,7 +493,7 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs, int ncu) {
   L.W5t = take(H * D * es);
   if (dtype == NR_BF16) {
     L.skP = take((int64_t)kSplit * (Hp - L.mm) * H * 4);
-    L.cs4 = take(L.csr * H * 4); L.cs3 = take(L.csr * D * 4); L.cs2 = take(L.csr * H * 4); L.cs1 = take(L.csr * H * 4);
+    L.cs4 = take(L.csr * H * 4); L.cs3 = take(L.csr3 * D * 4); L.cs2 = take(L.csr * H * 4); L.cs1 = take(L.csr * H * 4);
   } else {
     // dL^T, Y^T, dY^T, X^T, dX^T, X2^T, dZ2^T, X1^T, dZ1^T, XH^T
     const int64_t w[10] = {D, H, H, D, D, H, H, H, H, D};
@@ -625,12 +645,10 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
       const int64_t kk = K / kSplit, rows = Hp - mm;
       GemmProblem p = {rows, H, kk, A + mm * K, K, kk, Wt, K, kk, Pk, H, rows * H, kSplit, 1.0f};
       NR_FT(gemm_group_dispatch(dt, NR_F32, &p, 1, st));
-      NR_FT(nr_splitk_fixup(dt, NR_EPI_DRELU, rows, H, kSplit, Pk, nullptr, Yf + mm * H, H, C + mm * H, H, mm, 0,
-                            0.f, scale, st));
-      // the tail rows' column sums (of the stored bf16 values) into the CS layout
-      hipLaunchKernelGGL((colsum_block_kernel<TA>), dim3((unsigned)(H / 256), (unsigned)((rows + 127) / 128)),
-                         dim3(256), 0, st, mm, Hp, H, C, H, cs);
-      NR_CHECK_LAUNCH("nr_final_train_step (tail column sums)");
+      // the fixup and the tail rows' column sums (of the stored bf16 values) in one launch
+      hipLaunchKernelGGL((fixup_drelu_cs_kernel<TA>), dim3((unsigned)(H / 64), (unsigned)((rows + 31) / 32)),
+                         dim3(256), 0, st, mm / 128, rows, H, kSplit, Pk, Yf + mm * H, H, C + mm * H, H, scale, cs);
+      NR_CHECK_LAUNCH("nr_final_train_step (tail fixup + column sums)");
       return NR_OK;
     }
   };
@@ -666,7 +684,8 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
     float* outs[4] = {a.g_b1, a.g_b2, a.g_b3, a.g_b4};
     const int64_t cols[4] = {H, H, D, H};
     r.n = 4;
-    for (int i = 0; i < 4; ++i) { r.part[i] = parts[i]; r.out[i] = outs[i]; r.rows[i] = L.csr; r.cols[i] = cols[i]; }
+    const int64_t crows[4] = {L.csr, L.csr, L.csr3, L.csr};
+    for (int i = 0; i < 4; ++i) { r.part[i] = parts[i]; r.out[i] = outs[i]; r.rows[i] = crows[i]; r.cols[i] = cols[i]; }
     hipLaunchKernelGGL(rowsum_kernel, dim3((unsigned)((3 * H + D) / 64)), dim3(256), 0, st, r,
                        sqp ? sqp + kSqTn + kSqFold : nullptr);
     NR_CHECK_LAUNCH("nr_final_train_step (bias grads)");
