@@ -43,7 +43,10 @@ namespace nr {
 namespace ft {
 
 constexpr int64_t D = 1024, H = 4096;
-constexpr int kSplit = 8;  // K-slices of a split-K tail
+constexpr int kSplit = 8;  // K-slices of a split-K tail (at most; see tail_split)
+// K = 1024 tails as 4 slices (20.4 vs 22.6 us per tail), K = 4096 as 8 (26.7 vs 33.1):
+// tools/tail_probe.py, profiles/round5/train/tail_probe_r5m.jsonl
+static int tail_split(int64_t K) { return K <= 1024 ? 4 : kSplit; }
 // sum-of-squares partials of the bf16 step: 512 weight-grad tiles, then the W1 fold's
 // 16 x 64 blocks, the bias reduction's 208 blocks, the token LN reduction's 16
 constexpr int kSqTn = 512, kSqFold = (1024 / 64) * (4096 / 64), kSqBias = (3 * 4096 + 1024) / 64, kSqLn = 1024 / 64;
@@ -595,10 +598,11 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
     NR_FT(gemm_dispatch_ex(dt, dt, NR_EPI_RELU_DROPOUT, mm, H, K, A, lda, W, K, bias, nullptr, 0, C, ldc, ea, st));
     if (mm == Hp) return NR_OK;
     float* Pk = (float*)P_(L.skP);
-    const int64_t kk = K / kSplit, rows = Hp - mm;
-    GemmProblem p = {rows, H, kk, A + mm * lda, lda, kk, W, K, kk, Pk, H, rows * H, kSplit, 1.0f};
+    const int ns = tail_split(K);
+    const int64_t kk = K / ns, rows = Hp - mm;
+    GemmProblem p = {rows, H, kk, A + mm * lda, lda, kk, W, K, kk, Pk, H, rows * H, ns, 1.0f};
     NR_FT(gemm_group_dispatch(dt, NR_F32, &p, 1, st));
-    return nr_splitk_fixup(dt, NR_EPI_RELU_DROPOUT, rows, H, kSplit, Pk, bias, nullptr, 0, C + mm * ldc, ldc, mm,
+    return nr_splitk_fixup(dt, NR_EPI_RELU_DROPOUT, rows, H, ns, Pk, bias, nullptr, 0, C + mm * ldc, ldc, mm,
                            seed, a.p, scale, st);
   };
   NR_FT(relu_gemm(S, D, W1, D, a.b1, a.seed[0], X1, H));
@@ -642,12 +646,13 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
       NR_FT(gemm_dispatch_ex(dt, dt, NR_EPI_DRELU, mm, H, K, A, K, Wt, K, nullptr, Yf, H, C, H, ea, st));
       if (mm == Hp) return NR_OK;
       float* Pk = (float*)P_(L.skP);
-      const int64_t kk = K / kSplit, rows = Hp - mm;
-      GemmProblem p = {rows, H, kk, A + mm * K, K, kk, Wt, K, kk, Pk, H, rows * H, kSplit, 1.0f};
+      const int ns = tail_split(K);
+      const int64_t kk = K / ns, rows = Hp - mm;
+      GemmProblem p = {rows, H, kk, A + mm * K, K, kk, Wt, K, kk, Pk, H, rows * H, ns, 1.0f};
       NR_FT(gemm_group_dispatch(dt, NR_F32, &p, 1, st));
       // the fixup and the tail rows' column sums (of the stored bf16 values) in one launch
       hipLaunchKernelGGL((fixup_drelu_cs_kernel<TA>), dim3((unsigned)(H / 64), (unsigned)((rows + 31) / 32)),
-                         dim3(256), 0, st, mm / 128, rows, H, kSplit, Pk, Yf + mm * H, H, C + mm * H, H, scale, cs);
+                         dim3(256), 0, st, mm / 128, rows, H, ns, Pk, Yf + mm * H, H, C + mm * H, H, scale, cs);
       NR_CHECK_LAUNCH("nr_final_train_step (tail fixup + column sums)");
       return NR_OK;
     }
