@@ -32,7 +32,7 @@
 // weight-grad GEMMs as ONE grouped TN launch that reads the row-major
 // activations through transposed LDS reads (no transposed copies); the five
 // weight transposes the data-grad GEMMs need on a side stream beside the
-// forward's two N = 1024 GEMMs.  The token LN (E) is never stored as a [U][D]
+// forward's first N = 1024 GEMM.  The token LN (E) is never stored as a [U][D]
 // table: the slot kernel computes it per history slot from the token states,
 // the cosine kernel per pos / neg row.  f32 (the parity mode): the same sequence
 // on the exact-f32 MFMA tile kernels, with explicit transposes for the weight
@@ -554,8 +554,8 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   NR_FT(train_side_streams(st, "nr_final_train_step", side));
 
   // ---- the weight transposes the data-grad GEMMs need, on the side stream beside
-  // the two N = 1024 forward GEMMs (X, P: 132 tiles, half of the CUs idle) rather
-  // than beside the full-chip ones; joined (event wt) before the first data-grad GEMM
+  // an N = 1024 forward GEMM (X: 132 tiles, half of the CUs idle) rather than
+  // beside the full-chip ones; joined (event wt) before the first data-grad GEMM
   auto transposes = [&](int i0, int i1, hipEvent_t fork) -> int {
     const TA* w[5] = {W5, W4, W3, W2, W1};
     TA* t[5] = {W5t, W4t, W3t, W2t, W1t};
@@ -607,11 +607,12 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   };
   NR_FT(relu_gemm(S, D, W1, D, a.b1, a.seed[0], X1, H));
   NR_FT(relu_gemm(X1, H, W2, H, a.b2, a.seed[1], X2, H));
-  NR_FT(transposes(0, 3, side.fork));  // W5^T, W4^T, W3^T beside X
+  // all five beside X (53 us of transposes in its 85 us; one fork: each fork delays
+  // the next kernel on this stream by ~7 us, so a second one beside P cost more than it hid)
+  NR_FT(transposes(0, 5, side.fork));
+  NR_FT_EV(hipEventRecord(side.wt, side.s), "transpose record");
   NR_FT(gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, H, X2, H, W3, H, a.b3, nullptr, 0, X, 2 * D, st));
   NR_FT(relu_gemm(X, 2 * D, W4, D, a.b4, a.seed[2], Y, H));
-  NR_FT(transposes(3, 5, side.fork2));  // W2^T, W1^T beside P
-  NR_FT_EV(hipEventRecord(side.wt, side.s), "transpose record");
   NR_FT(gemm_dispatch(dt, dt, NR_EPI_EXP, Hp, D, H, Y, H, W5, H, nullptr, nullptr, 0, Pexp, 2 * D, st));
   NR_FT(nr_final_pool_fwd(dt, B, a.hist_off, XP, 2 * D, users, z, st));
   // ---- loss and its gradient into the pooled users and E[pos] / E[neg]
