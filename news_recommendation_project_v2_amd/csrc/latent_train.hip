@@ -135,10 +135,14 @@ struct ZList {
 // gradient buffer after the step's last kernel.
 struct SqList {
   int n = 0;
+  bool full = false;  // an add past 8 ranges: sq_list refuses the list
   const float* p[8];
   int64_t len[8];
   bool square[8];
-  void add(const float* x, int64_t l, bool sq = true) { p[n] = x; len[n] = l; square[n] = sq; ++n; }
+  void add(const float* x, int64_t l, bool sq = true) {
+    if (n == 8) { full = true; return; }
+    p[n] = x; len[n] = l; square[n] = sq; ++n;
+  }
 };
 __global__ __launch_bounds__(256) void sq_list_kernel(SqList q, float* __restrict__ out) {
   __shared__ float part[4];
@@ -182,6 +186,10 @@ __global__ __launch_bounds__(256) void sq_list_kernel(SqList q, float* __restric
 }
 
 static int sq_list(const SqList& q, float* out, hipStream_t st) {
+  if (q.full) {
+    set_error("nr_latent_train_step: more than 8 grad-norm ranges in one launch");
+    return NR_ERR_INVALID;
+  }
   if (!out || q.n == 0) return NR_OK;
   int64_t n = 0;
   for (int i = 0; i < q.n; ++i) n += q.len[i];
