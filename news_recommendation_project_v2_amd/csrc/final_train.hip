@@ -163,22 +163,23 @@ __global__ __launch_bounds__(256) void slots_kernel(int64_t Hp, int64_t Hs, cons
 //   dW1 = dZ1^T S = gamma o M + g_b1 (x) beta      (M computed in dW1's buffer, rewritten here)
 // Block = 64 columns x 64 rows h (4 groups of 16 rows, folded in LDS); per-chunk
 // partials [H / 64][2][D] summed in chunk order by ln_reduce_kernel (deterministic).
+// (block (bx, by) of nbx x H / 64; gb1p[h - hbase] = g_b1[h] for the block's 64 rows h)
 template <typename TA>
-__global__ __launch_bounds__(256) void w1_fold_kernel(const TA* __restrict__ W1, float* __restrict__ gW1,
-                                                      const float* __restrict__ gb1, const float* __restrict__ g,
-                                                      const float* __restrict__ b, float* __restrict__ part,
-                                                      float* __restrict__ sqp) {
+__device__ __forceinline__ void w1_fold_body(int bx, int by, int nbx, const TA* __restrict__ W1, float* __restrict__ gW1,
+                                             const float* gb1p, int64_t hbase, const float* __restrict__ g,
+                                             const float* __restrict__ b, float* __restrict__ part,
+                                             float* __restrict__ sqp) {
   __shared__ float red[2][4][64];
   __shared__ float rsq[4];
   const int grp = threadIdx.x >> 6, cl = threadIdx.x & 63;
-  const int64_t c = (int64_t)blockIdx.x * 64 + cl;
-  const int64_t h0 = (int64_t)blockIdx.y * 64 + grp * 16;
+  const int64_t c = (int64_t)bx * 64 + cl;
+  const int64_t h0 = (int64_t)by * 64 + grp * 16;
   const float gc = g[c], bc = b[c];
   float sg = 0.f, sb = 0.f, sq = 0.f;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int64_t h = h0 + k;
-    const float w = (float)W1[h * D + c], m = gW1[h * D + c], gh = gb1[h];
+    const float w = (float)W1[h * D + c], m = gW1[h * D + c], gh = gb1p[h - hbase];
     sg = fmaf(w, m, sg);
     sb = fmaf(w, gh, sb);
     const float dw = fmaf(gc, m, bc * gh);
@@ -193,16 +194,23 @@ __global__ __launch_bounds__(256) void w1_fold_kernel(const TA* __restrict__ W1,
     if (cl == 0) rsq[grp] = sq;
   }
   __syncthreads();
-  if (sqp && threadIdx.x == 0)
-    sqp[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = (rsq[0] + rsq[1]) + (rsq[2] + rsq[3]);
+  if (sqp && threadIdx.x == 0) sqp[(int64_t)by * nbx + bx] = (rsq[0] + rsq[1]) + (rsq[2] + rsq[3]);
   if (threadIdx.x < 128) {
     const int w = threadIdx.x >> 6;
     const float v = (red[w][0][cl] + red[w][1][cl]) + (red[w][2][cl] + red[w][3][cl]);
-    part[(int64_t)blockIdx.y * 2 * D + w * D + c] = v;
+    part[(int64_t)by * 2 * D + w * D + c] = v;
   }
 }
+// f32 mode: g_b1 already summed (nr_col_sum)
+template <typename TA>
+__global__ __launch_bounds__(256) void w1_fold_kernel(const TA* __restrict__ W1, float* __restrict__ gW1,
+                                                      const float* __restrict__ gb1, const float* __restrict__ g,
+                                                      const float* __restrict__ b, float* __restrict__ part,
+                                                      float* __restrict__ sqp) {
+  w1_fold_body<TA>((int)blockIdx.x, (int)blockIdx.y, (int)gridDim.x, W1, gW1, gb1, 0, g, b, part, sqp);
+}
 // dg[c] = sum_k part[k][0][c], db[c] = sum_k part[k][1][c] over the W1 fold's and the
-// pairs' chunks: 64 columns x 4 chunk groups per block
+// pairs' chunks: 64 columns x 4 chunk groups per block (with sqp: their sum of squares)
 __global__ __launch_bounds__(256) void ln_reduce_kernel(int nchunk, const float* __restrict__ part,
                                                         float* __restrict__ dg, float* __restrict__ db,
                                                         float* __restrict__ sqp) {
@@ -230,9 +238,8 @@ __global__ __launch_bounds__(256) void ln_reduce_kernel(int nchunk, const float*
     }
   }
 }
-
-// *out = the ordered sum of n partial sums of squares (the step's grad norm^2:
-// clip_grad_norm_ reads it, trainer.py:1067-1070).  One block.
+// *out = sum of the n grad-norm partials (the step's grad norm^2: clip_grad_norm_
+// reads it, trainer.py:1067-1070).  One block, fixed order.
 __global__ __launch_bounds__(256) void sq_total_kernel(int64_t n, const float* __restrict__ part,
                                                        float* __restrict__ out) {
   __shared__ float red[4];
@@ -415,13 +422,13 @@ struct RSum {
   int64_t rows[4], cols[4];
   int n;
 };
-__global__ __launch_bounds__(256) void rowsum_kernel(RSum r, float* __restrict__ sqp) {
+__device__ __forceinline__ void rowsum_body(const RSum& r, int bid, float* __restrict__ sqp) {
   __shared__ float red[16][64];
-  int64_t c0 = (int64_t)blockIdx.x * 64;
+  int64_t c0 = (int64_t)bid * 64;
   int i = 0;
   while (i < r.n && c0 >= r.cols[i]) c0 -= r.cols[i++];
   if (i >= r.n) {  // block-uniform
-    if (sqp && threadIdx.x == 0) sqp[blockIdx.x] = 0.f;
+    if (sqp && threadIdx.x == 0) sqp[bid] = 0.f;
     return;
   }
   const int grp = threadIdx.x >> 4, q = threadIdx.x & 15;
@@ -446,9 +453,50 @@ __global__ __launch_bounds__(256) void rowsum_kernel(RSum r, float* __restrict__
       float q = s * s;
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o, 64);
-      if (threadIdx.x == 0) sqp[blockIdx.x] = q;
+      if (threadIdx.x == 0) sqp[bid] = q;
     }
   }
+}
+
+// bf16: the bias grads (rowsum blocks 0 .. nrs - 1) and the W1 fold (the rest, D / 64 x
+// H / 64 blocks) as one launch.  A fold block needs g_b1 over its 64 rows h: it sums
+// them from cs1 itself with rowsum_body's arithmetic for b1's block h / 64 (the same
+// bits as the g_b1 it writes).
+template <typename TA>
+__global__ __launch_bounds__(256) void bias_fold_kernel(RSum r, int nrs, float* __restrict__ sq_rs, const TA* __restrict__ W1,
+                                                        float* __restrict__ gW1, const float* __restrict__ g,
+                                                        const float* __restrict__ b, float* __restrict__ part,
+                                                        float* __restrict__ sq_fold) {
+  __shared__ float gb1s[64];
+  const int id = (int)blockIdx.x;
+  if (id < nrs) {  // block-uniform
+    rowsum_body(r, id, sq_rs);
+    return;
+  }
+  const int f = id - nrs, nbx = (int)(D / 64), bx = f % nbx, by = f / nbx;
+  {
+    __shared__ float red[16][64];
+    const int grp = threadIdx.x >> 4, q = threadIdx.x & 15;
+    const int64_t c0 = (int64_t)by * 64;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t k = grp; k < r.rows[0]; k += 16) {
+      float v[4];
+      ld4<float>(r.part[0] + k * r.cols[0] + c0 + 4 * q, v);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] += v[t];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) red[grp][4 * q + t] = acc[t];
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += red[k][threadIdx.x];
+      gb1s[threadIdx.x] = s;
+    }
+    __syncthreads();
+  }
+  w1_fold_body<TA>(bx, by, nbx, W1, gW1, gb1s, (int64_t)by * 64, g, b, part, sq_fold);
 }
 
 // ------------------------------------------------------------------ workspace
@@ -669,6 +717,7 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   NR_FT(drelu_gemm(dZ2, H, W2t, X1, dZ1, cs1, a.g_b1));
   // (no dS = dZ1 W1: its only consumer, the token LN parameters, folds into dW1 below)
   // ---- weight grads: dW = dOut^T X
+  RSum r{};  // bf16: the bias grads from the column-sum partials
   if constexpr (BF) {
     GemmProblem p[5] = {
         {D, H, Hp, dL, D, 0, Y, H, 0, a.g_W5, H, 0, 1, 1.0f},
@@ -685,16 +734,13 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
       set_error("nr_final_train_step: %d weight-grad tiles (expected %d)", ntiles, kSqTn);
       return NR_ERR_INVALID;
     }
-    RSum r{};
     float* parts[4] = {cs1, cs2, cs3, cs4};
     float* outs[4] = {a.g_b1, a.g_b2, a.g_b3, a.g_b4};
     const int64_t cols[4] = {H, H, D, H};
     r.n = 4;
     const int64_t crows[4] = {L.csr, L.csr, L.csr3, L.csr};
     for (int i = 0; i < 4; ++i) { r.part[i] = parts[i]; r.out[i] = outs[i]; r.rows[i] = crows[i]; r.cols[i] = cols[i]; }
-    hipLaunchKernelGGL(rowsum_kernel, dim3((unsigned)((3 * H + D) / 64)), dim3(256), 0, st, r,
-                       sqp ? sqp + kSqTn + kSqFold : nullptr);
-    NR_CHECK_LAUNCH("nr_final_train_step (bias grads)");
+    // (launched with the W1 fold below: bias_fold_kernel)
   } else {
     TA* T[10];
     for (int i = 0; i < 10; ++i) T[i] = (TA*)P_(L.T[i]);
@@ -712,15 +758,23 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   }
   // ---- token LayerNorm parameter grads: the history gather's part folded with dW1
   // (w1_fold_kernel; dW1 = gamma o M + g_b1 (x) beta), summed with the pairs' part
+  // (bf16: one launch with the bias grads)
   {
     float* w1p = (float*)P_(L.w1p);
     float* sqp = BF && a.sumsq ? (float*)P_(L.sqp) : nullptr;
-    hipLaunchKernelGGL((w1_fold_kernel<TA>), dim3((unsigned)(D / 64), (unsigned)(H / 64)), dim3(256), 0, st, W1,
-                       a.g_W1, a.g_b1, a.tok_g, a.tok_b, w1p, sqp ? sqp + kSqTn : nullptr);
-    NR_CHECK_LAUNCH("nr_final_train_step (W1 fold)");
+    if constexpr (BF) {
+      const int nrs = (int)((3 * H + D) / 64);
+      hipLaunchKernelGGL((bias_fold_kernel<TA>), dim3((unsigned)(nrs + (D / 64) * (H / 64))), dim3(256), 0, st, r, nrs,
+                         sqp ? sqp + kSqTn + kSqFold : nullptr, W1, a.g_W1, a.tok_g, a.tok_b, w1p,
+                         sqp ? sqp + kSqTn : nullptr);
+      NR_CHECK_LAUNCH("nr_final_train_step (bias grads + W1 fold)");
+    } else {
+      hipLaunchKernelGGL((w1_fold_kernel<TA>), dim3((unsigned)(D / 64), (unsigned)(H / 64)), dim3(256), 0, st, W1,
+                         a.g_W1, a.g_b1, a.tok_g, a.tok_b, w1p, nullptr);
+      NR_CHECK_LAUNCH("nr_final_train_step (W1 fold)");
+    }
     hipLaunchKernelGGL(ln_reduce_kernel, dim3((unsigned)(D / 64)), dim3(256), 0, st, (int)(H / 64) + kPairChunks, w1p,
-                       a.g_tok_g,
-                       a.g_tok_b, sqp ? sqp + kSqTn + kSqFold + kSqBias : nullptr);
+                       a.g_tok_g, a.g_tok_b, sqp ? sqp + kSqTn + kSqFold + kSqBias : nullptr);
     NR_CHECK_LAUNCH("nr_final_train_step (token LN grads)");
     if (sqp) {
       hipLaunchKernelGGL(sq_total_kernel, dim3(1), dim3(256), 0, st, (int64_t)kSqParts, sqp, a.sumsq);
