@@ -1139,19 +1139,6 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     set_error("nr_latent_train_step: join 0 record failed");
     return NR_ERR_HIP;
   }
-  // the data-grad GEMMs' W operands, first needed by the dZ GEMM (event wt)
-  {
-    TList t;
-    t.add(W1, D, W1T, 2 * F, 2 * F, D, true);  // [8192, 1024] -> [1024, 8192]
-    t.add(W2, F, W2T, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
-    t.add(Wo, F, WoT, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
-    t.add(Wkv, D, WkvT, 2 * F, 2 * F, D, true);
-    if ((rc = launch_tlist<TA, TA>(t, fs))) return rc;
-  }
-  if (hipEventRecord(side.wt, fs) != hipSuccess) {
-    set_error("nr_latent_train_step: weight transpose record failed");
-    return NR_ERR_HIP;
-  }
   // ---- E = token LN of the last tokens (f32)
   if ((rc = gather_ln_dispatch(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1, a.tok_g, a.tok_b, 1e-12f, E, D, st)))
     return rc;
@@ -1159,6 +1146,16 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   hipLaunchKernelGGL((gather_ln_kernel<TA>), dim3(grid_rows(Hp)), dim3(256), 0, st, Hp, a.Hs, E, (int64_t)D,
                      a.hist_idx, a.nq_g, a.nq_b, 1e-5f, Sx, X);
   NR_LT_CHECK("gather_ln");
+  // the data-grad GEMMs' W operands (first needed by the dZ GEMM), on this stream while
+  // it waits for the fold: no event, and the P GEMM runs without them beside it
+  {
+    TList t;
+    t.add(W1, D, W1T, 2 * F, 2 * F, D, true);  // [8192, 1024] -> [1024, 8192]
+    t.add(W2, F, W2T, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
+    t.add(Wo, F, WoT, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
+    t.add(Wkv, D, WkvT, 2 * F, 2 * F, D, true);
+    if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
+  }
   if (hipStreamWaitEvent(st, side.join, 0) != hipSuccess) {
     set_error("nr_latent_train_step: join 0 failed");
     return NR_ERR_HIP;
@@ -1183,10 +1180,6 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   NR_LT_CHECK("head");
   // ---- backward
   // dZ_b = (dm_b / h_b) W2 (f32, split-K partials [kZParts, Bp, 4096]): C = dmc . W2T^T
-  if (hipStreamWaitEvent(st, side.wt, 0) != hipSuccess) {
-    set_error("nr_latent_train_step: weight transpose wait failed");
-    return NR_ERR_HIP;
-  }
   {
     const int64_t ks = D / kZParts;
     GemmProblem p = {Bp, F, ks, dmc, D, ks, W2T, D, ks, dZ, F, Bp * F, kZParts, 1.0f};
