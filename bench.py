@@ -272,7 +272,7 @@ def metrics_ms(run: Run, reps: int = 3) -> float:
     return e0.elapsed_time(e1) / reps
 
 
-def train_step_ms(dev, batch_rows: int = 256, steps: int = 10, pooler: str = "final") -> dict:
+def train_step_ms(dev, batch_rows: int = 256, steps: int = 30, pooler: str = "final", warmup: int = 10) -> dict:
     """Config 5 (BASELINE configs[4]): one train step (fwd + bwd + clip + AdamW) on a
     synthetic MIND-shaped batch: FinalAttentionTrainStep in bf16 MFMA, or with
     pooler="latent" LatentAttentionTrainStep (one nr_latent_train_step call: bf16
@@ -301,7 +301,7 @@ def train_step_ms(dev, batch_rows: int = 256, steps: int = 10, pooler: str = "fi
         fa = FinalAttention(1024, 4096)
         fa.load_state_dict(W.final_attention_state_dict(1234))
         eng = FinalAttentionTrainStep(tm, fa.to(dev), dtype=torch.bfloat16, device=dev)
-    for _ in range(3):
+    for _ in range(warmup):  # (after the eval legs: let the clocks settle on this load)
         eng.step(b)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
