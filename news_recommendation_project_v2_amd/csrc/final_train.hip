@@ -44,8 +44,9 @@ namespace ft {
 
 constexpr int64_t D = 1024, H = 4096;
 constexpr int kSplit = 8;  // K-slices of a split-K tail (at most; see tail_split)
-// K = 1024 tails as 4 slices (20.4 vs 22.6 us per tail), K = 4096 as 8 (26.7 vs 33.1):
-// tools/tail_probe.py, profiles/round5/train/tail_probe_r5m.jsonl
+// K = 1024 tails as 4 slices (20.4 vs 22.6 us per tail alone), K = 4096 as 8 (26.7 vs
+// 33.1): tools/tail_probe.py, profiles/round5/train/tail_probe_r5m.jsonl (inside the
+// step the K = 1024 choice measured within noise: profiles/round5/train/ab_r7u)
 static int tail_split(int64_t K) { return K <= 1024 ? 4 : kSplit; }
 // sum-of-squares partials of the bf16 step: 512 weight-grad tiles, then the W1 fold's
 // 16 x 64 blocks, the bias reduction's 208 blocks, the token LN reduction's 16
@@ -655,8 +656,8 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   };
   NR_FT(relu_gemm(S, D, W1, D, a.b1, a.seed[0], X1, H));
   NR_FT(relu_gemm(X1, H, W2, H, a.b2, a.seed[1], X2, H));
-  // all five beside X (53 us of transposes in its 85 us; one fork: each fork delays
-  // the next kernel on this stream by ~7 us, so a second one beside P cost more than it hid)
+  // all five beside X (53 us of transposes in its 85 us) under one fork; a second fork
+  // for W2^T / W1^T beside P measured the same (interleaved A/B, profiles/round5/train/ab_r7u)
   NR_FT(transposes(0, 5, side.fork));
   NR_FT_EV(hipEventRecord(side.wt, side.s), "transpose record");
   NR_FT(gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, H, X2, H, W3, H, a.b3, nullptr, 0, X, 2 * D, st));
