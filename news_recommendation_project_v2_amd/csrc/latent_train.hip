@@ -204,23 +204,40 @@ __global__ __launch_bounds__(256) void zero_kernel(ZList z) {
       z.p[i][k] = 0.f;
 }
 
-// dst[i] = sum_p src[p * pstride + i] over n contiguous f32 (split-K partials), 4 per thread
+// dst[i] = sum_p src[p * pstride + i] over n contiguous f32 (split-K partials).  Block =
+// 64 float4 positions x 4 part groups (group g sums parts g, g + 4, ... in order, the
+// four group sums then added in group order: deterministic); the parts' loads spread
+// over 4x the threads of one-thread-per-position (the 32-part dlatents sum ran on 64
+// blocks at ~0.8 TB/s).  dst may alias src (in place): a block reads all its positions
+// before writing them.
 __global__ __launch_bounds__(256) void sum_parts_kernel(int64_t n4, int parts, int64_t pstride4,
-                                                        const float4* src, float4* dst) {  // dst may alias src (in place)
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    float4 v = src[i];
-    for (int p = 1; p < parts; ++p) {
+                                                        const float4* src, float4* dst) {
+  __shared__ float4 red[4][64];
+  const int pl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + pl;
+  float4 v = {0.f, 0.f, 0.f, 0.f};
+  if (i < n4)
+    for (int p = g; p < parts; p += 4) {
       const float4 w = src[p * pstride4 + i];
       v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
     }
-    dst[i] = v;
+  red[g][pl] = v;
+  __syncthreads();
+  if (g == 0 && i < n4) {
+    float4 t = red[0][pl];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 w = red[k][pl];
+      t.x += w.x; t.y += w.y; t.z += w.z; t.w += w.w;
+    }
+    dst[i] = t;
   }
 }
 
 static int sum_parts(const float* src, int parts, int64_t pstride, float* dst, int64_t n, hipStream_t st) {
-  const int64_t n4 = n / 4, g = (n4 + 255) / 256;
-  hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, st, n4, parts,
-                     pstride / 4, (const float4*)src, (float4*)dst);
+  const int64_t n4 = n / 4, g = (n4 + 63) / 64;
+  hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)g), dim3(256), 0, st, n4, parts, pstride / 4, (const float4*)src,
+                     (float4*)dst);
   NR_CHECK_LAUNCH("nr_latent_train_step (sum_parts)");
   return NR_OK;
 }
@@ -1297,7 +1314,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   // ---- fold backward
   {
     // the K-slices summed on the way into both converted operands (one launch; the
-    // same slice order as sum_parts, so bit-identical to summing first)
+    // slices summed in order)
     SCList t;
     if ((rc = t.add(gA, D, kWParts, (int64_t)S * D, S, D, gA16, D, gAT16, S))) return rc;
     if ((rc = t.add(gBt, S, kWParts, (int64_t)D * S, D, S, gBt16, S, gBtT16, D))) return rc;
