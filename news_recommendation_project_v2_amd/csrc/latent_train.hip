@@ -894,11 +894,12 @@ int launch_tlist(const TList& l, hipStream_t s) {
 
 // f32 split-K partials -> their sum in TO twice, as is (plain) and transposed:
 // the fold's operands (KV / KV^T, gA / gA^T, gBt / gBt^T, dKV / dKV^T).  One
-// 64 x 64 tile per block, up to kSCMax matrices per launch: each partial is
-// read once with 16-B loads, all `parts` loads of a row issued together, the sum
-// in slice order (as sum_parts), the plain tile stored from registers and the
-// transposed one through LDS.  The generic TBatch path read every partial twice
-// (once per output) with 4-B loads: 34-38 us for the gA / gBt set, ~12 us here.
+// 32-row x 64-column tile per block (64-row tiles: half the blocks, ~12 us/step
+// slower in an interleaved A/B, profiles/round5/train/ab_r8a), up to kSCMax
+// matrices per launch: each partial is read once with 16-B loads, all `parts`
+// loads of a row issued together, the sum in slice order, the plain tile stored
+// from registers and the transposed one through LDS.  The generic TBatch path read
+// every partial twice (once per output) with 4-B loads: 34-38 us for the gA / gBt set.
 constexpr int kSCMax = 2;
 struct SCBatch {
   int n;
@@ -911,12 +912,12 @@ struct SCBatch {
 
 template <typename TO>
 __global__ __launch_bounds__(256) void sumconv_kernel(SCBatch sb) {
-  __shared__ float tile[64][65];
+  __shared__ float tile[32][65];
   const int t = (int)blockIdx.x;
   int p = 0;
   while (p + 1 < sb.n && t >= sb.tile_end[p]) ++p;
   const int local = t - (p ? sb.tile_end[p - 1] : 0);
-  const int64_t r0 = (int64_t)(local / sb.tiles_x[p]) * 64, c0 = (int64_t)(local % sb.tiles_x[p]) * 64;
+  const int64_t r0 = (int64_t)(local / sb.tiles_x[p]) * 32, c0 = (int64_t)(local % sb.tiles_x[p]) * 64;
   const float* src = sb.src[p];
   const int np = sb.parts[p];
   const int64_t lds = sb.lds[p], ps = sb.pstride[p];
@@ -924,7 +925,7 @@ __global__ __launch_bounds__(256) void sumconv_kernel(SCBatch sb) {
   TO* plain = (TO*)sb.plain[p];
   const int64_t ldp = sb.ldp[p];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 2; ++k) {
     const int rr = rg + 16 * k;
     const float* s = src + (r0 + rr) * lds + c0 + c4;
     float4 v = *reinterpret_cast<const float4*>(s);
@@ -940,9 +941,8 @@ __global__ __launch_bounds__(256) void sumconv_kernel(SCBatch sb) {
   __syncthreads();
   TO* trans = (TO*)sb.trans[p];
   const int64_t ldt = sb.ldt[p];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int i = th + 256 * k, cc = i >> 3, rc = (i & 7) * 8;
+  {
+    const int cc = th >> 2, rc = (th & 3) * 8;
     float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = tile[rc + j][cc];
@@ -966,7 +966,7 @@ struct SCList {
     b.src[i] = src; b.plain[i] = plain; b.trans[i] = trans; b.parts[i] = parts; b.pstride[i] = pstride;
     b.cols[i] = cols; b.lds[i] = lds; b.ldp[i] = ldp; b.ldt[i] = ldt;
     b.tiles_x[i] = (int)(cols / 64);
-    tiles += (int)(rows / 64 * (cols / 64));
+    tiles += (int)(rows / 32 * (cols / 64));
     b.tile_end[i] = tiles;
     return NR_OK;
   }
