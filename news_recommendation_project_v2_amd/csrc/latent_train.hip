@@ -1091,13 +1091,25 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   if ((rc = train_side_streams(st, "nr_latent_train_step", side))) return rc;
 #define NR_LT_CHECK(name) NR_CHECK_LAUNCH("nr_latent_train_step (" name ")")
 
-  // ---- fork 0: the weight transposes and the fold (weights only) run on the side
-  // stream beside the token LN and the history gather (inputs only); the P GEMM
-  // joins them.  The side stream first waits for everything before the step on
+  // ---- fork 0: the fold (weights only) runs on the side stream beside Wq^T, the
+  // token LN, the history gather and the data-grad weight transposes on this one
+  // (interleaved A/B: Wq^T here 1.045-1.055 vs on the fold stream 1.053-1.061 ms/step,
+  // profiles/round5/train/ab_r8c); the P GEMM joins them.  The side stream first waits for everything before the step on
   // this one (the previous step's AdamW rewrote the weights).
   if (hipEventRecord(side.fork, st) != hipSuccess || hipStreamWaitEvent(side.s, side.fork, 0) != hipSuccess) {
     set_error("nr_latent_train_step: fork 0 failed");
     return NR_ERR_HIP;
+  }
+  // Wq^T (the A fold's operand) first on this stream, event wt: the fold stream runs
+  // LN_c and the KV GEMM meanwhile and waits for it just before the A / Bt GEMMs
+  {
+    TList t;
+    t.add(Wq, D, WqT, F, F, D, true);  // [4096, 1024] -> [1024, 4096]
+    if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
+    if (hipEventRecord(side.wt, st) != hipSuccess) {
+      set_error("nr_latent_train_step: Wq transpose record failed");
+      return NR_ERR_HIP;
+    }
   }
   // ---- accumulators: the step zeroes every gradient it accumulates (the GEMM-written
   // ones are overwritten whole), the loss and the history-gather gradient dE
@@ -1122,12 +1134,6 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   // weight transpose before the fold on the side stream 1.20, this layout 1.185 --
   // profiles/round4/train/step_tuning/r4ab1)
   hipStream_t fs = side.s;
-  // Wq^T, the fold's operand (the other weight transposes follow the fold)
-  {
-    TList t;
-    t.add(Wq, D, WqT, F, F, D, true);  // [4096, 1024] -> [1024, 4096]
-    if ((rc = launch_tlist<TA, TA>(t, fs))) return rc;
-  }
   // fold: latn = LN_c(latents); KV = latn Wkv^T (split-K); A_h = s K_h Wq_h; BtT_h = V_h Wo_h^T
   if ((rc = layernorm_dispatch(NR_F32, dt, NL, D, a.latents, D, a.nc_g, a.nc_b, 1e-5f, latn, D, fs))) return rc;
   {
@@ -1137,6 +1143,10 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     SCList t;
     if ((rc = t.add(KVp, 2 * F, kKVParts, (int64_t)NL * 2 * F, NL, 2 * F, KV, 2 * F, KVT, NL))) return rc;
     if ((rc = launch_sumconv<TA>(t, fs))) return rc;
+  }
+  if (hipStreamWaitEvent(fs, side.wt, 0) != hipSuccess) {
+    set_error("nr_latent_train_step: Wq transpose wait failed");
+    return NR_ERR_HIP;
   }
   {
     GemmProblem p[2] = {
