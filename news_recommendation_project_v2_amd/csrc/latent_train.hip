@@ -1111,6 +1111,18 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
       return NR_ERR_HIP;
     }
   }
+  // the data-grad GEMMs' W operands (first needed by the dZ GEMM), on this stream
+  // before the gathers: beside LN_c and the KV GEMM rather than the A / Bt GEMMs, and
+  // not beside the P GEMM (interleaved A/B: 1.090-1.095 vs after the gathers
+  // 1.097-1.102 ms/step, profiles/round5/train/ab_r8f)
+  {
+    TList t;
+    t.add(W1, D, W1T, 2 * F, 2 * F, D, true);  // [8192, 1024] -> [1024, 8192]
+    t.add(W2, F, W2T, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
+    t.add(Wo, F, WoT, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
+    t.add(Wkv, D, WkvT, 2 * F, 2 * F, D, true);
+    if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
+  }
   // ---- accumulators: the step zeroes every gradient it accumulates (the GEMM-written
   // ones are overwritten whole), the loss and the history-gather gradient dE
   {
@@ -1173,16 +1185,6 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   hipLaunchKernelGGL((gather_ln_kernel<TA>), dim3(grid_rows(Hp)), dim3(256), 0, st, Hp, a.Hs, E, (int64_t)D,
                      a.hist_idx, a.nq_g, a.nq_b, 1e-5f, Sx, X);
   NR_LT_CHECK("gather_ln");
-  // the data-grad GEMMs' W operands (first needed by the dZ GEMM), on this stream while
-  // it waits for the fold: no event, and the P GEMM runs without them beside it
-  {
-    TList t;
-    t.add(W1, D, W1T, 2 * F, 2 * F, D, true);  // [8192, 1024] -> [1024, 8192]
-    t.add(W2, F, W2T, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
-    t.add(Wo, F, WoT, D, D, F, true);          // [1024, 4096] -> [4096, 1024]
-    t.add(Wkv, D, WkvT, 2 * F, 2 * F, D, true);
-    if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
-  }
   if (hipStreamWaitEvent(st, side.join, 0) != hipSuccess) {
     set_error("nr_latent_train_step: join 0 failed");
     return NR_ERR_HIP;
