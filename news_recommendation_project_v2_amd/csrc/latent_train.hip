@@ -5,6 +5,8 @@
 // LatentAttentionModel (latent_attention.py:134-171) in FinalAttention's slot:
 //
 //   E  = g_mlp_LN(last token)                        token model (attention.py:193)
+//        (never stored as a [U][1024] table: the slot gather, the head's pos / neg
+//        rows and the LN_q backward recompute E rows from the token states, tok_ln)
 //   fold (weights only, once per step; the reference rebuilds K/V per batch row,
 //   latent_attention.py:161-162):
 //        KV = LN_c(latents) Wkv^T;  A_h = K_h Wq_h / sqrt(512);  BtT_h = V_h Wo_h^T
@@ -243,11 +245,69 @@ static int sum_parts(const float* src, int parts, int64_t pstride, float* dst, i
 }
 
 // ------------------------------------------------------------------ forward rows
-// S = E[idx[row]], X = LN_q(S) (eps 1e-5); idx < 0 or row >= nvalid
+// E row of news r: the token LayerNorm (g_mlp_layernorm, eps 1e-12, affine tg / tb)
+// of its last token state (TT = f32 / bf16 / f16), the arithmetic of rowops.hip's
+// gather_ln_kernel (nr_gather_layernorm): lane's columns 256 j + 4 lane .. +3.  The
+// step never stores the [U][1024] E table: the slot gather, the head (pos / neg
+// rows) and the LN_q backward recompute the rows they read from the token states.
+template <typename TT>
+__device__ __forceinline__ void tok_ln(const TT* __restrict__ row, int lane, const float* __restrict__ tg,
+                                       const float* __restrict__ tb, float (&v)[4][4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const TT* p = row + j * 256 + lane * 4;
+    if constexpr (std::is_same<TT, _Float16>::value) {
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      const h4 h = *reinterpret_cast<const h4*>(p);
+      v[j][0] = (float)h[0]; v[j][1] = (float)h[1]; v[j][2] = (float)h[2]; v[j][3] = (float)h[3];
+    } else {
+      ld4<TT>(p, v[j]);
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float d = v[j][t] - mean;
+      q = fmaf(d, d, q);
+    }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + 1e-12f);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int e = j * 256 + lane * 4 + t;
+      v[j][t] = (v[j][t] - mean) * rstd * tg[e] + tb[e];
+    }
+}
+
+// Epn rows k < B: E[pos[k]], rows B + k: E[neg[k]] (f32, for the head).  Wave per row.
+template <typename TT>
+__global__ __launch_bounds__(256) void pn_rows_kernel(int64_t B, const TT* __restrict__ tok,
+                                                      const int32_t* __restrict__ pos, const int32_t* __restrict__ neg,
+                                                      const float* __restrict__ tg, const float* __restrict__ tb,
+                                                      float* __restrict__ Epn) {
+  const int lane = threadIdx.x & 63;
+  const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= 2 * B) return;  // wave-uniform
+  const int64_t r = k < B ? pos[k] : neg[k - B];
+  float v[4][4];
+  tok_ln<TT>(tok + r * D, lane, tg, tb, v);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) st4<float>(Epn + k * D + j * 256 + lane * 4, v[j]);
+}
+
+// Sx = E[idx[row]], X = LN_q(Sx) (eps 1e-5); idx < 0 or row >= nvalid
 // (padding): both rows zero.  One wave per row, lane columns 256 j + 4 lane .. +3.
-template <typename TA>
-__global__ __launch_bounds__(256) void gather_ln_kernel(int64_t n, int64_t nvalid, const float* __restrict__ E,
-                                                        int64_t lde, const int32_t* __restrict__ idx,
+template <typename TA, typename TT>
+__global__ __launch_bounds__(256) void gather_ln_kernel(int64_t n, int64_t nvalid, const TT* __restrict__ tok,
+                                                        const float* __restrict__ tg, const float* __restrict__ tb,
+                                                        const int32_t* __restrict__ idx,
                                                         const float* __restrict__ g, const float* __restrict__ b,
                                                         float eps, TA* __restrict__ Sx, TA* __restrict__ X) {
   const int lane = threadIdx.x & 63;
@@ -262,12 +322,10 @@ __global__ __launch_bounds__(256) void gather_ln_kernel(int64_t n, int64_t nvali
       continue;
     }
     float v[4][4];
+    tok_ln<TT>(tok + (int64_t)r * D, lane, tg, tb, v);
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      ld4<float>(E + (int64_t)r * lde + j * 256 + lane * 4, v[j]);
-      s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
-    }
+    for (int j = 0; j < 4; ++j) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
     const float mean = wave_sum(s) / (float)D;
     float q = 0.f;
 #pragma unroll
@@ -400,7 +458,7 @@ __global__ __launch_bounds__(512) void segmean_kernel(int64_t B, int64_t Bp, con
 template <typename TA>
 __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int nparts, const float* __restrict__ parts,
                                                    const float* __restrict__ b2, const float* __restrict__ h1bar,
-                                                   const int64_t* __restrict__ off, const float* __restrict__ E,
+                                                   const int64_t* __restrict__ off, const float* __restrict__ Epn,
                                                    int64_t lde, const int32_t* __restrict__ pos,
                                                    const int32_t* __restrict__ neg, float margin,
                                                    float* __restrict__ loss, float* __restrict__ users,
@@ -421,8 +479,8 @@ __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int np
     return;
   }
   float m[4], ep[4], en[4];
-  const float* pr = E + (int64_t)pos[b] * lde;
-  const float* nr_ = E + (int64_t)neg[b] * lde;
+  const float* pr = Epn + b * D;         // E[pos[b]]
+  const float* nr_ = Epn + (B + b) * D;  // E[neg[b]]
   float mm = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -586,21 +644,22 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t n_rows, const TA
 //   dgamma += dy xhat, dbeta += dy (per-lane registers, one atomic per column per block)
 // MODE 0 (LN_f of H1): res = dmc32[row_seg[row]] (f32: the broadcast dH of the mean),
 //   dx -> out rows (TA); padding slots (row_seg < 0) -> zero rows.
-// MODE 1 (LN_q of S):  x = the f32 row E[idx[row]] the forward normalised (xf, not
-//   the bf16-stored S: the statistics of the rounded row moved the token LN
+// MODE 1 (LN_q of S):  x = the f32 row E[idx[row]] the forward normalised (tok_ln of
+//   the token row tokv[idx[row]], not the bf16-stored S: the statistics of the rounded row moved the token LN
 //   bias grad ~10x past the bf16 numerics model's drift, test_train_bf16_drift),
 //   res = dH1 row (TA); dx scattered into dE[idx[row]]
 //   (the gradient of the history gather): the row is staged in the wave's LDS
 //   and added with lane-contiguous f32 atomics (256 B per wave instruction, the
 //   full-rate shape of MI355X_MICROARCH.md "Global float atomics"); idx < 0 skipped.
-template <typename TA, int MODE>
+template <typename TA, int MODE, typename TT = float>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, const TA* __restrict__ x,
-                                                     const float* __restrict__ xf, const float* __restrict__ gamma,
+                                                     const void* __restrict__ tokv, const float* __restrict__ gamma,
                                                      float eps,
                                                      const TA* __restrict__ dy, const void* __restrict__ res_,
                                                      const int32_t* __restrict__ sel, TA* __restrict__ out,
                                                      float* __restrict__ dE, int64_t lde, float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta) {
+                                                     float* __restrict__ dbeta, const float* __restrict__ tg,
+                                                     const float* __restrict__ tb) {
   __shared__ float sg[4][D], sb[4][D];
   __shared__ float stage[MODE == 1 ? 4 : 1][MODE == 1 ? D : 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -626,12 +685,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int c = j * 256 + lane * 4;
-      if constexpr (MODE == 1) ld4<float>(xf + (int64_t)s * lde + c, v[j]);
-      else ld4<TA>(x + row * D + c, v[j]);
+      if constexpr (MODE == 0) ld4<TA>(x + row * D + c, v[j]);
       ld4<TA>(dy + row * D + c, dyv[j]);
       if constexpr (MODE == 0) ld4<float>(static_cast<const float*>(res_) + (int64_t)s * D + c, rv[j]);
       else ld4<TA>(static_cast<const TA*>(res_) + row * D + c, rv[j]);
     }
+    if constexpr (MODE == 1) tok_ln<TT>(static_cast<const TT*>(tokv) + (int64_t)s * D, lane, tg, tb, v);
     float sum = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) sum += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
@@ -1015,7 +1074,7 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs) {
   const int64_t Hp = L.Hp, Hpp = L.Hpp, Bp = L.Bp, es = L.es;
   int64_t o = 0;
   auto take = [&](int64_t bytes) { const int64_t r = o; o += al(bytes); return r; };
-  L.E = take(U * D * 4);
+  L.E = take(2 * Bp * D * 4);  // Epn: E[pos] rows then E[neg] rows (no [U][D] E table)
   // X, P, dH1, dS hold Hpp rows: the dA / dBt K-slices read them directly (bf16: TN
   // weight-grad GEMMs), rows [Hp, Hpp) zeroed by the step
   L.Sx = take(Hp * D * es); L.X = take(Hpp * D * es); L.P = take(Hpp * S * es); L.H1 = take(Hp * D * es);
@@ -1054,7 +1113,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   const Layout L = layout(dt, a.B, a.U, a.Hs);
   const int64_t B = a.B, U = a.U, Hp = L.Hp, Hpp = L.Hpp, Bp = L.Bp;
   auto P_ = [&](int64_t off) { return (void*)(ws + off); };
-  float* E = (float*)P_(L.E);
+  float* Epn = (float*)P_(L.E);
   TA *Sx = (TA*)P_(L.Sx), *X = (TA*)P_(L.X), *Pm = (TA*)P_(L.P), *H1 = (TA*)P_(L.H1), *Y = (TA*)P_(L.Y);
   TA *G = (TA*)P_(L.G), *zbar = (TA*)P_(L.zbar);
   float* h1bar = (float*)P_(L.h1bar);
@@ -1178,12 +1237,19 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     set_error("nr_latent_train_step: join 0 record failed");
     return NR_ERR_HIP;
   }
-  // ---- E = token LN of the last tokens (f32)
-  if ((rc = gather_ln_dispatch(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1, a.tok_g, a.tok_b, 1e-12f, E, D, st)))
-    return rc;
+#define NR_LT_TOK(...)                                                       \
+  do {                                                                       \
+    if (a.tok_dtype == NR_F32) { typedef float TT; __VA_ARGS__; }            \
+    else if (a.tok_dtype == NR_BF16) { typedef __bf16 TT; __VA_ARGS__; }     \
+    else { typedef _Float16 TT; __VA_ARGS__; }                              \
+  } while (0)
+  // ---- E[pos] / E[neg] rows for the head (the token LN of those news' last tokens)
+  NR_LT_TOK(hipLaunchKernelGGL((pn_rows_kernel<TT>), dim3((unsigned)((2 * B + 3) / 4)), dim3(256), 0, st, B,
+                               (const TT*)a.tok_last, a.pos, a.neg, a.tok_g, a.tok_b, Epn));
+  NR_LT_CHECK("pos / neg rows");
   // ---- per-slot forward
-  hipLaunchKernelGGL((gather_ln_kernel<TA>), dim3(grid_rows(Hp)), dim3(256), 0, st, Hp, a.Hs, E, (int64_t)D,
-                     a.hist_idx, a.nq_g, a.nq_b, 1e-5f, Sx, X);
+  NR_LT_TOK(hipLaunchKernelGGL((gather_ln_kernel<TA, TT>), dim3(grid_rows(Hp)), dim3(256), 0, st, Hp, a.Hs,
+                               (const TT*)a.tok_last, a.tok_g, a.tok_b, a.hist_idx, a.nq_g, a.nq_b, 1e-5f, Sx, X));
   NR_LT_CHECK("gather_ln");
   if (hipStreamWaitEvent(st, side.join, 0) != hipSuccess) {
     set_error("nr_latent_train_step: join 0 failed");
@@ -1205,7 +1271,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     if ((rc = sum_parts(hparts, kHParts, Bp * D, hsum, Bp * D, st))) return rc;
   }
   hipLaunchKernelGGL((head_kernel<TA>), dim3((unsigned)Bp), dim3(256), 0, st, B, Bp, 1, hsum, a.b2, h1bar,
-                     a.hist_off, E, (int64_t)D, a.pos, a.neg, a.margin, a.loss, a.users, dmA, dmc, dmc32, dE, a.g_b2);
+                     a.hist_off, Epn, (int64_t)D, a.pos, a.neg, a.margin, a.loss, a.users, dmA, dmc, dmc32, dE, a.g_b2);
   NR_LT_CHECK("head");
   // ---- backward
   // dZ_b = (dm_b / h_b) W2 (f32, split-K partials [kZParts, Bp, 4096]): C = dmc . W2T^T
@@ -1261,7 +1327,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, 2 * F, dG, 2 * F, W1T, 2 * F, nullptr, nullptr, 0, dY, D, st)))
     return rc;
   hipLaunchKernelGGL((ln_bwd_kernel<TA, 0>), dim3(grid_rows(Hp, 512)), dim3(256), 0, st, Hp, Hp, H1, nullptr, a.nf_g, 1e-5f, dY,
-                     dmc32, row_seg, dH1, nullptr, (int64_t)0, a.g_nf_g, a.g_nf_b);
+                     dmc32, row_seg, dH1, nullptr, (int64_t)0, a.g_nf_g, a.g_nf_b, nullptr, nullptr);
   NR_LT_CHECK("ln_f_bwd");
   if (dt == NR_BF16) {
     // dS = P (dP - sum_group P dP) in the dP GEMM's epilogue (NR_EPI_SOFTMAX64_BWD, R = P)
@@ -1284,8 +1350,9 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     return NR_ERR_HIP;
   }
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, S, dS, S, AT, S, nullptr, nullptr, 0, dX, D, st))) return rc;
-  hipLaunchKernelGGL((ln_bwd_kernel<TA, 1>), dim3(grid_rows(Hp, 512)), dim3(256), 0, st, Hp, a.Hs, Sx, E, a.nq_g, 1e-5f,
-                     dX, dH1, a.hist_idx, nullptr, dE, (int64_t)D, a.g_nq_g, a.g_nq_b);
+  NR_LT_TOK(hipLaunchKernelGGL((ln_bwd_kernel<TA, 1, TT>), dim3(grid_rows(Hp, 512)), dim3(256), 0, st, Hp, a.Hs, Sx,
+                               a.tok_last, a.nq_g, 1e-5f, dX, dH1, a.hist_idx, nullptr, dE, (int64_t)D, a.g_nq_g,
+                               a.g_nq_b, a.tok_g, a.tok_b));
   NR_LT_CHECK("ln_q_bwd");
   // token LayerNorm parameter grads from dE (history scatter + cosine grads)
   if ((rc = nr_ln_param_grad(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1e-12f, dE, D, a.g_tok_g, a.g_tok_b, st)))
@@ -1390,6 +1457,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     q.add(a.g_nc_b, D);
     if ((rc = sq_list(q, a.sumsq, st))) return rc;
   }
+#undef NR_LT_TOK
 #undef NR_LT_CHECK
   return NR_OK;
 }
