@@ -37,7 +37,9 @@ Also reported in the same JSON line:
                 cosine loop) on this host's CPU share (all affinity cores, or
                 OMP_NUM_THREADS where the pool declares a per-GPU share), on the
                 first 1,000 impressions of a MIND-small-shaped set (configs[0]),
-                for both poolers; ``--cpu-10k`` adds 10,000
+                for both poolers, and on the first 10,000
+                (capped at --cpu-10k-seconds of CPU time per
+                pooler, the impressions done reported; --no-cpu-10k drops it)
   extra         the FinalAttention pooler, f32, per-stage times, AUC of the GPU
                 path vs the CPU reference on the config-1 sample, MIND-large
                 test shape, Zipf ids, device metrics, PCIe costs, config 5
@@ -86,15 +88,92 @@ def _free_port() -> int:
     return port
 
 
-def spawn_ranks(n: int, argv: list) -> int:
-    """Run this script under torch.distributed.run with n ranks (child process;
-    nothing here has touched the GPU) and return its exit code."""
+PHASE_ENV = "NR_BENCH_PHASE_DIR"
+
+
+def phase(name: str) -> None:
+    """Record this rank's current phase (a file per rank under $NR_BENCH_PHASE_DIR,
+    written by rename so the parent never reads half a line): when the launch
+    has to be killed, spawn_ranks reports where every rank was.  A test hook
+    (NR_BENCH_TEST_STALL="rank:phase") parks that rank at that phase forever,
+    as a rank stuck in a collective would be."""
+    d = os.environ.get(PHASE_ENV)
+    rank = os.environ.get("RANK", "0")
+    if d:
+        tmp = Path(d) / f".rank{rank}.tmp"
+        tmp.write_text(json.dumps({"phase": name, "t": time.time()}))
+        tmp.replace(Path(d) / f"rank{rank}")
+    if os.environ.get("NR_BENCH_TEST_STALL") == f"{rank}:{name}":
+        while True:
+            time.sleep(3600)
+
+
+def _phases(d: Path, n: int) -> dict:
+    out = {}
+    for r in range(n):
+        try:
+            rec = json.loads((d / f"rank{r}").read_text())
+            out[str(r)] = {"phase": rec["phase"], "seconds_in_phase": round(time.time() - rec["t"], 1)}
+        except (OSError, ValueError, KeyError):
+            out[str(r)] = {"phase": "not started", "seconds_in_phase": None}
+    return out
+
+
+def spawn_ranks(n: int, argv: list, stall_s: float = 300.0, wall_s: float = 1800.0) -> int:
+    """Run this script under torch.distributed.run with n ranks (child process
+    group; nothing here has touched the GPU) and return its exit code.  A launch
+    that stops making progress -- no rank changes phase for `stall_s`, or the
+    whole run passes `wall_s` -- is killed (the whole process group) and one
+    JSON line with value null names every rank's phase, so a stuck RCCL init
+    or collective ends with a record instead of at the driver's kill with no
+    line at all.  If rank 0 already printed its result line
+    and only the teardown hangs, the stragglers are killed and 0 returned."""
+    import shutil
+    import signal
+    import tempfile
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(Path(__file__).resolve()), *argv]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    pdir = Path(tempfile.mkdtemp(prefix="nr_bench_phase_"))
+    env[PHASE_ENV] = str(pdir)
     log("[bench] launching", " ".join(cmd))
-    return subprocess.call(cmd, env=env)
+    t0 = time.time()
+    proc = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        while True:
+            try:
+                return proc.wait(timeout=1.0)
+            except subprocess.TimeoutExpired:
+                pass
+            ph = _phases(pdir, n)
+            started = [v["seconds_in_phase"] for v in ph.values() if v["seconds_in_phase"] is not None]
+            newest = min(started) if started else time.time() - t0
+            elapsed = time.time() - t0
+            if newest < stall_s and elapsed < wall_s:
+                continue
+            why = "stalled" if newest >= stall_s else "wall"
+            done = ph.get("0", {}).get("phase") == "printed"
+            try:
+                os.killpg(proc.pid, signal.SIGTERM)
+                proc.wait(timeout=15)
+            except (subprocess.TimeoutExpired, ProcessLookupError):
+                try:
+                    os.killpg(proc.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                proc.wait()
+            if done:
+                log(f"[bench] rank 0 printed its line; teardown {why} ({json.dumps(ph)}): stragglers killed")
+                return 0
+            print(json.dumps({"metric": "scored candidates/sec on MIND-large impressions; AUC parity vs CPU ref",
+                              "value": None, "unit": "scored candidates/s", "n_gpus": n, "higher_is_better": True,
+                              "error": (f"no rank changed phase for {stall_s:.0f} s" if why == "stalled" else
+                                        f"the launch passed its {wall_s:.0f} s wall limit") + "; killed",
+                              "elapsed_s": round(elapsed, 1), "rank_phases": ph}), flush=True)
+            return 124
+    finally:
+        shutil.rmtree(pdir, ignore_errors=True)
 
 
 def make_model(pooler: str, dev):
@@ -505,15 +584,17 @@ def cpu_leg(args, dev) -> tuple:
     full = synthetic.mind_impressions(n_news, n_imp_full, seed=1234)
     table_d = news_table(n_news, dev)
     table_c = table_d.cpu()
-    samples = [args.cpu_impressions] + ([10_000] if args.cpu_10k else [])
+    samples = [args.cpu_impressions] + ([] if args.no_cpu_10k else [10_000])
     out, parity = {}, {}
     for pooler in ("latent", "final"):
         for n_imp in samples:
             imps = full.slice(0, n_imp)
-            done, ncand, secs, cpu_scores = cpu_reference(pooler, imps, table_c, args.cpu_seconds)
+            cap = args.cpu_seconds if n_imp == args.cpu_impressions else min(args.cpu_seconds, args.cpu_10k_seconds)
+            done, ncand, secs, cpu_scores = cpu_reference(pooler, imps, table_c, cap)
             out.setdefault(pooler, {})[f"first_{n_imp}"] = {
                 "impressions": done, "candidates": ncand, "seconds": round(secs, 2),
-                "value": round(ncand / secs, 1)}
+                "value": round(ncand / secs, 1), "cpu_seconds_cap": cap,
+                "capped": done < n_imp}
             log(f"[bench] CPU reference {pooler} first {n_imp}: {done} imps {ncand} cands in {secs:.1f}s "
                 f"= {ncand / secs:.0f} cand/s on {cores} threads")
             if n_imp != args.cpu_impressions:
@@ -685,6 +766,7 @@ def dry_run(args, rank: int, world: int) -> None:
     table = torch.randn((n_news, 1024), generator=g, dtype=torch.float32)
     eng = _DryRunEngine(table, mine)
     tab = ShardedTable(eng, rank, world)
+    phase("dry_run_step")
     dist.barrier()
     t0 = time.perf_counter()
     local, _ = sharded_step(tab)
@@ -719,6 +801,7 @@ def dry_run(args, rank: int, world: int) -> None:
                           "impressions_total": int(c[1]), "candidates_expected": int(expected),
                           "allgather_ok": bool(ok_tab.item()), "scores_match_single_process": bool(ok_s.item()),
                           "step_s": float(t.item())}), flush=True)
+    phase("printed")
 
 
 def main():
@@ -737,26 +820,36 @@ def main():
                     help="gloo: test mode, ranks may share one GPU (tables staged through the host)")
     ap.add_argument("--cpu-shape", default="mind_small_dev", choices=list(synthetic.SHAPES))
     ap.add_argument("--cpu-impressions", type=int, default=1000)
-    ap.add_argument("--cpu-10k", action="store_true", help="also time the CPU reference on 10,000 impressions")
+    ap.add_argument("--no-cpu-10k", action="store_true", help="skip the 10,000-impression CPU reference sample")
+    ap.add_argument("--cpu-10k-seconds", type=float, default=30.0,
+                    help="CPU-time cap per pooler for the 10,000-impression sample (impressions done are reported)")
     ap.add_argument("--cpu-seconds", type=float, default=60.0, help="CPU-time cap per pooler and sample")
     ap.add_argument("--no-extra", action="store_true", help="headline config only")
     ap.add_argument("--no-auc-gate", action="store_true",
                     help="skip the full-size (376,471-impression) AUC parity gate vs the CPU reference")
     ap.add_argument("--dry-run", action="store_true", help="CPU-only check of the multi-rank plumbing")
     ap.add_argument("--dry-run-news", type=int, default=8192, help="--dry-run news-table rows (0: the shape's)")
+    ap.add_argument("--dist-timeout", type=float, default=600.0,
+                    help="seconds: torch.distributed's collective timeout and the RCCL communicator init deadline")
+    ap.add_argument("--stall-timeout", type=float, default=300.0,
+                    help="N > 1 launcher: kill the ranks when none changes phase for this many seconds")
+    ap.add_argument("--wall-timeout", type=float, default=1800.0, help="N > 1 launcher: kill the ranks after this")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], args.stall_timeout, args.wall_timeout))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    from datetime import timedelta
+    pg_timeout = timedelta(seconds=args.dist_timeout)
+    phase("init_process_group")
     if args.dry_run:
         if world > 1:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
         try:
             dry_run(args, rank, world) if world > 1 else print(json.dumps({"dry_run": True, "n_gpus": 1}))
         finally:
@@ -770,9 +863,10 @@ def main():
     host_reduce = args.backend == "gloo"
     if world > 1:
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
+    phase("data")
 
     n_news, n_imp = synthetic.SHAPES[args.shape]
     n_imp = args.impressions or n_imp
@@ -792,8 +886,10 @@ def main():
     log(f"[bench] data ready in {time.time() - t0:.1f}s: N={n_news} I={imps.n_imp} C={imps.n_cand} "
         f"H={imps.n_hist} (rank 0 of {world}, {args.scaling} scaling)")
 
+    phase("headline")
     head = Run(args.pooler, args.dtype, imps, table, dev, rank, world)
     dt = timed(head.step, args.steps, args.warmup, world, dev, host_reduce)
+    phase("headline_done")
     ms = dt / args.steps * 1e3
     if total_cand is None:  # weak: every rank's own set
         c = torch.tensor([imps.n_cand], dtype=torch.int64, device="cpu" if host_reduce else dev)
@@ -867,9 +963,11 @@ def main():
         # nr_allgather): its step time and its table against torch's bit for bit
         from news_recommendation_project_v2_amd.distributed import NrComm
         comm = None
+        phase("nr_comm_init")
         try:
             ref_table = head.tab.full.clone()
-            comm = NrComm(rank, world)
+            comm = NrComm(rank, world, timeout_s=args.dist_timeout)
+            phase("nr_allgather")
             r = Run(args.pooler, args.dtype, imps, table, dev, rank, world)
             r.tab = ShardedTable(r.eng, rank, world, comm=comm)
             r.tab.timing = True
@@ -892,6 +990,7 @@ def main():
             _lib.empty_cache()
 
     if world > 1 and not args.no_extra:
+        phase("overlapped_build")
         # the opt-in overlapped build (2 chunks, each chunk's all-gather beside the next
         # chunk's transform): its step time, and its table against the default's bit for bit
         ref_table = head.tab.full.clone()
@@ -906,6 +1005,7 @@ def main():
         del r, ref_table
         _lib.empty_cache()
         # the other scaling mode as an extra
+        phase("other_scaling")
         if args.scaling == "strong":  # every rank its own full MIND-large-dev-sized set
             other = synthetic.mind_impressions(n_news, n_imp, seed=1234 + rank)
         else:  # configs[3] as ONE eval job: the rank-0 set partitioned over the ranks
@@ -929,6 +1029,7 @@ def main():
         _lib.empty_cache()
         # configs[3]'s strong scaling on the MIND-large *test* shape: 2.37 M impressions
         # over 121 k news keep ~300 k impressions per GPU at N = 8
+        phase("mind_large_test")
         tn, ti = synthetic.SHAPES["mind_large_test"]
         one = synthetic.mind_impressions(tn, ti, seed=1234)
         ob = partition_by_cost(one.hist_len, one.cand_len, world, kw * 1024 * es, 1024 * es)
@@ -1067,6 +1168,7 @@ def main():
             "extra": extra,
         }
         print(json.dumps(out), flush=True)
+    phase("printed")
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -38,6 +38,7 @@ extern "C" {
 #define NR_ERR_INVALID -1     /* bad argument / shape */
 #define NR_ERR_HIP -2         /* HIP runtime or launch failure */
 #define NR_ERR_UNSUPPORTED -3 /* valid but not implemented (e.g. dim) */
+#define NR_ERR_TIMEOUT -4     /* a collective did not complete within its deadline */
 
 /* element types */
 #define NR_F32 0
@@ -588,6 +589,24 @@ int64_t nr_final_train_workspace_bytes(int dtype, int64_t B, int64_t U, int64_t 
 int nr_final_train_step(const nr_final_train_args* args, void* ws, int64_t ws_bytes, void* stream);
 
 /*
+ * ---- Host <-> device transfers of the drop-in API (csrc/xfer.hip): the CSR
+ * index arrays and the news table up, scores / ranks down.  Replaces the
+ * reference's pageable `.to(DEVICE)` / `.cpu()` copies (data_model_helper.py:
+ * 112-131, 199-230, 416-443).  The bytes move through a process-wide ring of
+ * pinned chunks, pipelined: NR_COPY_THREADS (default 8) host threads copy chunk
+ * i between the caller's pageable memory and the ring while the DMA engine
+ * moves chunk i - 1 (hipMemcpyAsync on `stream`).
+ * nr_copy_h2d: dst device, src host; returns once src has been read (reusable);
+ *   the data lands in stream order.
+ * nr_copy_d2h: dst host, src device; returns with dst complete (the copy runs
+ *   in stream order after the work queued before it).
+ * Calls are serialised process-wide.  Errors: NR_ERR_INVALID for a null pointer,
+ * bytes < 0 or a non-device pointer on the device side; NR_ERR_HIP otherwise.
+ */
+int nr_copy_h2d(void* dst, const void* src, int64_t bytes, void* stream);
+int nr_copy_d2h(void* dst, const void* src, int64_t bytes, void* stream);
+
+/*
  * ---- RCCL communicator of the multi-GPU eval (SURVEY §8(b) nr_allgather,
  * §8(e)): one process per GPU; every rank transforms a row shard of the
  * per-news table and ONE all-gather over xGMI gives each GPU the whole table.
@@ -599,6 +618,12 @@ int nr_final_train_step(const nr_final_train_args* args, void* ws, int64_t ws_by
  *   rank (any channel: torch.distributed broadcast, a file, MPI ...);
  *   every rank: nr_init(device); nr_comm_init(&c, id, nranks, rank)
  *   (collective: blocks until all nranks have called it).
+ * nr_comm_init_timeout: the same with a deadline.  timeout_ms > 0 forms a
+ *   non-blocking RCCL communicator (ncclCommInitRankConfig, blocking = 0) and
+ *   polls it; if it has not formed within timeout_ms (a peer never joined or
+ *   died inside its init) it is aborted (ncclCommAbort) and the call returns
+ *   NR_ERR_TIMEOUT, so a stuck rank fails with a record instead of hanging.
+ *   timeout_ms <= 0, or an RCCL without the non-blocking entries: as nr_comm_init.
  * nr_allgather: recv[r * bytes_per_rank ..] = rank r's send, async on `stream`;
  * in place when send == recv + rank * bytes_per_rank.
  */
@@ -607,6 +632,7 @@ typedef struct nr_comm* nr_comm_t;
 int nr_rccl_version(void); /* RCCL's NCCL_VERSION_CODE, 0 when RCCL is absent */
 int nr_comm_unique_id(unsigned char* id);
 int nr_comm_init(nr_comm_t* comm, const unsigned char* id, int nranks, int rank);
+int nr_comm_init_timeout(nr_comm_t* comm, const unsigned char* id, int nranks, int rank, int64_t timeout_ms);
 int nr_comm_destroy(nr_comm_t comm);
 int nr_allgather(nr_comm_t comm, const void* send, void* recv, int64_t bytes_per_rank, void* stream);
 

@@ -14,7 +14,9 @@
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <chrono>
 #include <mutex>
+#include <thread>
 
 namespace nr {
 namespace {
@@ -26,6 +28,10 @@ struct RcclApi {
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
   ncclResult_t (*get_version)(int*) = nullptr;
+  // non-blocking init with a deadline (optional: the blocking entries above suffice)
+  ncclResult_t (*comm_init_rank_config)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;
+  ncclResult_t (*get_async_error)(ncclComm_t, ncclResult_t*) = nullptr;
+  ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
   bool ok = false;
 };
 
@@ -46,6 +52,9 @@ const RcclApi& rccl() {
     api.all_gather = (decltype(api.all_gather))dlsym(h, "ncclAllGather");
     api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
     api.get_version = (decltype(api.get_version))dlsym(h, "ncclGetVersion");
+    api.comm_init_rank_config = (decltype(api.comm_init_rank_config))dlsym(h, "ncclCommInitRankConfig");
+    api.get_async_error = (decltype(api.get_async_error))dlsym(h, "ncclCommGetAsyncError");
+    api.comm_abort = (decltype(api.comm_abort))dlsym(h, "ncclCommAbort");
     api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.all_gather && api.error_string;
   });
   return api;
@@ -61,12 +70,29 @@ int rccl_fail(const char* fn, ncclResult_t r) {
   return NR_ERR_HIP;
 }
 
+// A non-blocking communicator's calls may return ncclInProgress: poll its state
+// until it settles, up to `deadline_ms` (<= 0: no deadline).  Returns the
+// settled state, or ncclInProgress when the deadline passed first.
+ncclResult_t settle(ncclComm_t c, ncclResult_t r, int64_t deadline_ms) {
+  const RcclApi& a = rccl();
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r == ncclInProgress) {
+    if (deadline_ms > 0 && std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0)
+                                   .count() >= deadline_ms)
+      return ncclInProgress;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+    if (a.get_async_error(c, &r) != ncclSuccess) return ncclInternalError;
+  }
+  return r;
+}
+
 }  // namespace
 }  // namespace nr
 
 struct nr_comm {
   ncclComm_t comm;
   int nranks, rank;
+  bool nonblocking;
 };
 
 extern "C" int nr_rccl_version(void) {
@@ -88,7 +114,7 @@ extern "C" int nr_comm_unique_id(unsigned char* id) {
   return NR_OK;
 }
 
-extern "C" int nr_comm_init(nr_comm_t* comm, const unsigned char* id, int nranks, int rank) {
+extern "C" int nr_comm_init_timeout(nr_comm_t* comm, const unsigned char* id, int nranks, int rank, int64_t timeout_ms) {
   nr::clear_error();
   NR_CHECK_ARG(comm && id, "nr_comm_init: null argument");
   NR_CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "nr_comm_init: rank %d of %d", rank, nranks);
@@ -98,17 +124,45 @@ extern "C" int nr_comm_init(nr_comm_t* comm, const unsigned char* id, int nranks
   ncclUniqueId u;
   memcpy(u.internal, id, NR_COMM_ID_BYTES);
   ncclComm_t c = nullptr;
-  const ncclResult_t r = a.comm_init_rank(&c, nranks, u, rank);  // collective over the nranks processes
-  if (r != ncclSuccess) return nr::rccl_fail("nr_comm_init", r);
-  *comm = new nr_comm{c, nranks, rank};
+  const bool nonblocking = timeout_ms > 0 && a.comm_init_rank_config && a.get_async_error && a.comm_abort;
+  if (!nonblocking) {
+    const ncclResult_t r = a.comm_init_rank(&c, nranks, u, rank);  // collective over the nranks processes
+    if (r != ncclSuccess) return nr::rccl_fail("nr_comm_init", r);
+    *comm = new nr_comm{c, nranks, rank, false};
+    return NR_OK;
+  }
+  // non-blocking init (config.blocking = 0): the call returns at once and the
+  // communicator settles in the background; a peer that never joins leaves it
+  // in progress, and at the deadline it is aborted instead of blocking forever
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclResult_t r = a.comm_init_rank_config(&c, nranks, u, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) return nr::rccl_fail("nr_comm_init", r);
+  r = nr::settle(c, r, timeout_ms);
+  if (r == ncclInProgress) {
+    a.comm_abort(c);
+    nr::set_error("nr_comm_init: rank %d of %d: the communicator did not form within %lld ms (a peer did not join); "
+                  "aborted", rank, nranks, (long long)timeout_ms);
+    return NR_ERR_TIMEOUT;
+  }
+  if (r != ncclSuccess) {
+    a.comm_abort(c);
+    return nr::rccl_fail("nr_comm_init", r);
+  }
+  *comm = new nr_comm{c, nranks, rank, true};
   return NR_OK;
+}
+
+extern "C" int nr_comm_init(nr_comm_t* comm, const unsigned char* id, int nranks, int rank) {
+  return nr_comm_init_timeout(comm, id, nranks, rank, 0);
 }
 
 extern "C" int nr_comm_destroy(nr_comm_t comm) {
   nr::clear_error();
   if (!comm) return NR_OK;
   const nr::RcclApi& a = nr::rccl();
-  const ncclResult_t r = a.ok ? a.comm_destroy(comm->comm) : ncclSuccess;
+  ncclResult_t r = a.ok ? a.comm_destroy(comm->comm) : ncclSuccess;
+  if (a.ok && comm->nonblocking) r = nr::settle(comm->comm, r, 0);
   delete comm;
   return r == ncclSuccess ? NR_OK : nr::rccl_fail("nr_comm_destroy", r);
 }
@@ -123,7 +177,8 @@ extern "C" int nr_allgather(nr_comm_t comm, const void* send, void* recv, int64_
   const nr::RcclApi& a = nr::rccl();
   if (!a.ok) return nr::rccl_missing("nr_allgather");
   // in place when send == recv + rank * bytes_per_rank (RCCL's in-place rule)
-  const ncclResult_t r = a.all_gather(send, recv, (size_t)bytes_per_rank, ncclUint8, comm->comm, (hipStream_t)stream);
+  ncclResult_t r = a.all_gather(send, recv, (size_t)bytes_per_rank, ncclUint8, comm->comm, (hipStream_t)stream);
+  if (comm->nonblocking) r = nr::settle(comm->comm, r, 0);  // enqueued once it settles
   if (r != ncclSuccess) return nr::rccl_fail("nr_allgather", r);
   return NR_OK;
 }

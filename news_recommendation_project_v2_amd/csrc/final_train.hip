@@ -404,7 +404,7 @@ __global__ __launch_bounds__(256) void fixup_drelu_cs_kernel(int64_t cs_row0, in
     st4<TA>(C + r * ldc + c + 4, y + 4);
   }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) red[rg][8 * cl + k] = (float)(TA)y[k];  // the stored value
+  for (int k = 0; k < 8; ++k) red[rg][8 * cl + k] = y[k];  // pre-rounding, as the persistent GEMM's CS epilogue
   __syncthreads();
   if (threadIdx.x < 64) {
     float t = 0.f;
@@ -504,7 +504,7 @@ __global__ __launch_bounds__(256) void bias_fold_kernel(RSum r, int nrs, float* 
 struct Layout {
   int64_t Hp, es, mm, csr, csr3;
   int64_t xpair, S, XH, X1, X2, XP, Y, users, z, du, gpair, lrow, dXp, dL, dY, dX, dZ2, dZ1, w1p, sqp;
-  int64_t W1t, W2t, W3t, W4t, W5t, skP, cs4, cs3, cs2, cs1;
+  int64_t W2t, W3t, W4t, W5t, skP, cs4, cs3, cs2, cs1;
   int64_t T[10];  // f32 mode: the weight-grad operands transposed
   int64_t total;
 };
@@ -541,7 +541,7 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs, int ncu) {
   L.sqp = take(kSqParts * 4);
   L.dXp = take(Hp * D * es); L.dL = take(Hp * D * es); L.dY = take(Hp * H * es); L.dX = take(Hp * D * es);
   L.dZ2 = take(Hp * H * es); L.dZ1 = take(Hp * H * es); L.w1p = take((H / 64 + kPairChunks) * 2 * D * 4);
-  L.W1t = take(D * H * es); L.W2t = take(H * H * es); L.W3t = take(H * D * es); L.W4t = take(D * H * es);
+  L.W2t = take(H * H * es); L.W3t = take(H * D * es); L.W4t = take(D * H * es);
   L.W5t = take(H * D * es);
   if (dtype == NR_BF16) {
     L.skP = take((int64_t)kSplit * (Hp - L.mm) * H * 4);
@@ -591,7 +591,7 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   float *z = (float*)P_(L.z), *du = (float*)P_(L.du), *gpair = (float*)P_(L.gpair), *lrow = (float*)P_(L.lrow);
   TA *dXp = (TA*)P_(L.dXp), *dL = (TA*)P_(L.dL), *dY = (TA*)P_(L.dY), *dX = (TA*)P_(L.dX), *dZ2 = (TA*)P_(L.dZ2);
   TA* dZ1 = (TA*)P_(L.dZ1);
-  TA *W1t = (TA*)P_(L.W1t), *W2t = (TA*)P_(L.W2t), *W3t = (TA*)P_(L.W3t), *W4t = (TA*)P_(L.W4t),
+  TA *W2t = (TA*)P_(L.W2t), *W3t = (TA*)P_(L.W3t), *W4t = (TA*)P_(L.W4t),
      *W5t = (TA*)P_(L.W5t);
   const TA *W1 = (const TA*)a.W1, *W2 = (const TA*)a.W2, *W3 = (const TA*)a.W3, *W4 = (const TA*)a.W4,
            *W5 = (const TA*)a.W5;
@@ -606,9 +606,10 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   // an N = 1024 forward GEMM (X: 132 tiles, half of the CUs idle) rather than
   // beside the full-chip ones; joined (event wt) before the first data-grad GEMM
   auto transposes = [&](int i0, int i1, hipEvent_t fork) -> int {
-    const TA* w[5] = {W5, W4, W3, W2, W1};
-    TA* t[5] = {W5t, W4t, W3t, W2t, W1t};
-    const int64_t r[5] = {D, H, D, H, H}, c[5] = {H, D, H, H, D};  // W5 [D][H], W4 [H][D], W3 [D][H], W2, W1 [H][D]
+    // (no W1^T: its only consumer was the dS = dZ1 W1 GEMM, folded away below)
+    const TA* w[4] = {W5, W4, W3, W2};
+    TA* t[4] = {W5t, W4t, W3t, W2t};
+    const int64_t r[4] = {D, H, D, H}, c[4] = {H, D, H, H};  // W5 [D][H], W4 [H][D], W3 [D][H], W2 [H][H]
     NR_FT_EV(hipEventRecord(fork, st), "fork record");
     NR_FT_EV(hipStreamWaitEvent(side.s, fork, 0), "fork wait");
     for (int i = i0; i < i1; ++i) NR_FT(nr_transpose(dt, dt, r[i], c[i], w[i], c[i], t[i], r[i], side.s));
@@ -656,9 +657,9 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   };
   NR_FT(relu_gemm(S, D, W1, D, a.b1, a.seed[0], X1, H));
   NR_FT(relu_gemm(X1, H, W2, H, a.b2, a.seed[1], X2, H));
-  // all five beside X (53 us of transposes in its 85 us) under one fork; a second fork
-  // for W2^T / W1^T beside P measured the same (interleaved A/B, profiles/round5/train/ab_r7u)
-  NR_FT(transposes(0, 5, side.fork));
+  // all four beside X under one fork; a second fork for the last ones beside P measured
+  // the same (interleaved A/B, profiles/round5/train/ab_r7u)
+  NR_FT(transposes(0, 4, side.fork));
   NR_FT_EV(hipEventRecord(side.wt, side.s), "transpose record");
   NR_FT(gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, H, X2, H, W3, H, a.b3, nullptr, 0, X, 2 * D, st));
   NR_FT(relu_gemm(X, 2 * D, W4, D, a.b4, a.seed[2], Y, H));
@@ -729,12 +730,9 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
     };
     float* sqp = a.sumsq ? (float*)P_(L.sqp) : nullptr;
     const bool sqf[5] = {true, true, true, true, false};  // dW1 is M here: counted by the fold
-    int ntiles = 0;
-    NR_FT(gemm_group_tn_dispatch(NR_F32, p, 5, st, sqp, sqf, &ntiles, kSqTn));
-    if (sqp && ntiles != kSqTn) {
-      set_error("nr_final_train_step: %d weight-grad tiles (expected %d)", ntiles, kSqTn);
-      return NR_ERR_INVALID;
-    }
+    // one sum-of-squares slot per tile: the five shapes are fixed, so is the tile count
+    static_assert(4 * (D / 256) * (H / 256) + (H / 256) * (H / 256) == kSqTn, "weight-grad tiles != kSqTn");
+    NR_FT(gemm_group_tn_dispatch(NR_F32, p, 5, st, sqp, sqf, nullptr, kSqTn));
     float* parts[4] = {cs1, cs2, cs3, cs4};
     float* outs[4] = {a.g_b1, a.g_b2, a.g_b3, a.g_b4};
     const int64_t cols[4] = {H, H, D, H};
@@ -818,12 +816,17 @@ extern "C" int nr_final_train_step(const nr_final_train_args* args, void* ws, in
   NR_CHECK_ARG(a.Hs <= (1ll << 31) - 1024 && a.U <= (1ll << 31) && a.B <= (1ll << 24),
                "nr_final_train_step: batch too large");
   NR_CHECK_ARG(a.p >= 0.f && a.p < 1.f, "nr_final_train_step: dropout p outside [0, 1)");
+  // bf16: the persistent GEMM (the column-sum epilogues have no other kernel) addresses
+  // its [Hp][4096] operands through 32-bit buffer offsets; refuse before any launch
+  NR_CHECK_ARG(a.dtype != NR_BF16 || nr::ft::pad64(a.Hs) * nr::ft::H * 2 <= 0xFFFFFFFFll,
+               "nr_final_train_step: bf16 batch of %lld history slots exceeds the persistent GEMM's 4 GiB operand "
+               "range (at most %lld)", (long long)a.Hs, 0xFFFFFFFFll / (2 * nr::ft::H) / 64 * 64);
   NR_CHECK_DEVICE("nr_final_train_step", a.tok_last, a.hist_idx, a.hist_off, a.pos, a.neg, a.tok_g, a.tok_b, a.W1,
                   a.b1, a.W2, a.b2, a.W3, a.b3, a.W4, a.b4, a.W5);
   NR_CHECK_DEVICE("nr_final_train_step", a.g_tok_g, a.g_tok_b, a.g_W1, a.g_b1, a.g_W2, a.g_b2, a.g_W3, a.g_b3, a.g_W4,
-                  a.g_b4, a.g_W5, a.loss, a.users, ws);
-  NR_CHECK_ARG(a.tok_last && a.hist_idx && a.hist_off && a.pos && a.neg && a.loss && ws && a.W1 && a.W2 && a.W3 &&
-                   a.W4 && a.W5 && a.g_W1 && a.g_W2 && a.g_W3 && a.g_W4 && a.g_W5 && a.g_b1 && a.g_b2 && a.g_b3 &&
+                  a.g_b4, a.g_W5, a.loss, a.users, a.sumsq, ws);
+  NR_CHECK_ARG(a.tok_last && a.hist_idx && a.hist_off && a.pos && a.neg && a.loss && ws && a.tok_g && a.tok_b &&
+                   a.W1 && a.b1 && a.W2 && a.b2 && a.W3 && a.b3 && a.W4 && a.b4 && a.W5 && a.g_W1 && a.g_W2 && a.g_W3 && a.g_W4 && a.g_W5 && a.g_b1 && a.g_b2 && a.g_b3 &&
                    a.g_b4 && a.g_tok_g && a.g_tok_b,
                "nr_final_train_step: null pointer");
   hipStream_t s = (hipStream_t)stream;

@@ -56,14 +56,17 @@ class NrComm:
     group, and every rank joins (nr_comm_init, collective).  ``allgather``
     issues ncclAllGather on the current torch stream."""
 
-    def __init__(self, rank: int, world: int, group=None):
+    def __init__(self, rank: int, world: int, group=None, timeout_s: float = 300.0):
         """Collective over the group: every rank returns, or every rank raises.
         A failure on one rank is agreed on before the next collective step (a
         status byte travels with the id; a MIN all-reduce of a ready flag
         precedes nr_comm_init and one of a success flag follows it), so no rank
-        is left waiting in a collective its peers have abandoned.  What this
-        cannot cover is a rank dying INSIDE ncclCommInitRank after the ready
-        check: RCCL's blocking init has no timeout."""
+        is left waiting in a collective its peers have abandoned.  A rank dying
+        INSIDE the RCCL init after the ready check is covered by the deadline:
+        the communicator is formed non-blocking (nr_comm_init_timeout) and
+        aborted after ``timeout_s`` (NR_ERR_TIMEOUT on the surviving ranks)
+        instead of blocking them forever; ``timeout_s <= 0``
+        is the blocking init."""
         import ctypes
         from . import _lib
         self.rank, self.world = rank, world
@@ -92,7 +95,9 @@ class NrComm:
             err = e
         self._agree(err is None, group, flag_dev, "before nr_comm_init", err)
         try:
-            _lib.check(self._lib.nr_comm_init(ctypes.byref(self._h), idb, world, rank), "nr_comm_init")
+            _lib.check(self._lib.nr_comm_init_timeout(ctypes.byref(self._h), idb, world, rank,
+                                                      int(timeout_s * 1000) if timeout_s > 0 else 0),
+                       "nr_comm_init_timeout")
         except Exception as e:  # noqa: BLE001
             err = e
         try:

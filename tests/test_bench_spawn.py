@@ -35,3 +35,27 @@ def test_bench_spawns_ranks(world, scaling):
         assert res["partition"] is None and res["impressions_total"] == 1500 * world
     assert res["candidates_total"] == res["candidates_expected"]
     assert res["allgather_ok"] and res["scores_match_single_process"]
+
+
+def test_bench_launcher_kills_a_stalled_rank_with_a_record():
+    """A rank that never reaches the collective (NR_BENCH_TEST_STALL parks rank 1
+    before the dry run's first barrier, as a rank stuck in an RCCL init or
+    collective would be) must not hang the launch: the parent sees no phase
+    change for --stall-timeout seconds, kills the rank group, prints ONE JSON line
+    with value null naming every rank's phase, and exits non-zero
+    (VERDICT r5 #5)."""
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["NR_BENCH_TEST_STALL"] = "1:dry_run_step"
+    t0 = time.time()
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dry-run", "--impressions", "300",
+                        "--stall-timeout", "20", "--dist-timeout", "600"],
+                       cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    dt = time.time() - t0
+    assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["value"] is None and res["n_gpus"] == 2 and "no rank changed phase" in res["error"]
+    assert res["rank_phases"]["1"]["phase"] == "dry_run_step"
+    assert res["rank_phases"]["0"]["phase"] == "dry_run_step"  # waiting in the barrier for rank 1
+    assert dt < 200, dt

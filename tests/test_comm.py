@@ -29,6 +29,8 @@ def test_comm_argument_errors(lib):
     assert lib.nr_comm_init(ctypes.byref(h), idb, 2, 2) == -1  # rank out of range
     assert "rank 2 of 2" in lib.nr_last_error().decode()
     assert lib.nr_comm_init(None, idb, 1, 0) == -1
+    assert lib.nr_comm_init_timeout(ctypes.byref(h), idb, 1, 1, 1000) == -1
+    assert lib.nr_comm_init_timeout(None, idb, 1, 0, 1000) == -1
     assert lib.nr_allgather(None, None, None, 16, None) == -1
     assert lib.nr_comm_destroy(None) == 0
     assert lib.nr_rccl_version() >= 0
@@ -71,3 +73,37 @@ def test_nr_allgather_one_rank_matches_torch(gpu_device, pooler, tmp_path):
         if comm is not None:
             comm.close()
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_comm_init_timeout_when_a_peer_never_joins(gpu_device):
+    """nr_comm_init_timeout for rank 0 of a 2-rank communicator whose rank 1 never
+    calls in: the non-blocking init is aborted at the deadline and the call
+    returns NR_ERR_TIMEOUT (-4) naming the rank, instead of blocking forever
+    (a stuck rank must fail with a record).  A second, one-rank
+    communicator formed afterwards still works (the abort left RCCL usable)."""
+    import time
+    lib = _lib.load()
+    _lib.check(lib.nr_init(gpu_device.index or 0), "nr_init")
+    idb = (ctypes.c_ubyte * 128)()
+    _lib.check(lib.nr_comm_unique_id(ctypes.cast(idb, ctypes.POINTER(ctypes.c_ubyte))), "nr_comm_unique_id")
+    h = ctypes.c_void_p()
+    t0 = time.perf_counter()
+    rc = lib.nr_comm_init_timeout(ctypes.byref(h), idb, 2, 0, 2000)
+    dt = time.perf_counter() - t0
+    msg = lib.nr_last_error().decode()
+    print(f"rc {rc} after {dt:.2f}s: {msg}")
+    assert rc == -4 and "did not form within 2000 ms" in msg and "rank 0 of 2" in msg, (rc, msg)
+    assert 1.9 <= dt <= 30.0, dt
+    assert not h.value
+    idb1 = (ctypes.c_ubyte * 128)()
+    _lib.check(lib.nr_comm_unique_id(ctypes.cast(idb1, ctypes.POINTER(ctypes.c_ubyte))), "nr_comm_unique_id")
+    h1 = ctypes.c_void_p()
+    _lib.check(lib.nr_comm_init_timeout(ctypes.byref(h1), idb1, 1, 0, 30000), "nr_comm_init_timeout")
+    x = torch.arange(1024, dtype=torch.uint8, device=gpu_device)
+    y = torch.zeros_like(x)
+    _lib.check(lib.nr_allgather(h1, x.data_ptr(), y.data_ptr(), 1024, torch.cuda.current_stream().cuda_stream),
+               "nr_allgather")
+    torch.cuda.synchronize()
+    assert torch.equal(x, y)
+    _lib.check(lib.nr_comm_destroy(h1), "nr_comm_destroy")

@@ -30,10 +30,19 @@ def _batch(seed=0, lens=(11, 3, 1, 7, 2, 5), L=11, D=1024):
     return torch.from_numpy(emb), torch.from_numpy(mask)
 
 
+# The f32 config-5 step (exact-f32 MFMA, f32 activations) against the f32 oracle, per
+# gradient tensor, max |d| over the tensor's max: measured <= 2.1e-6 against the float64
+# oracle and <= 7.1e-7 for the f32 oracle itself, over the golden trainer's first three
+# batches (tools/latent_f32_probe.py, profiles/round6/latent_f32_probe.jsonl).  Both are
+# f32 reassociation of sums up to 8,310 slots long; 1e-5 leaves ~3x over their sum.
+F32_GRAD_TOL = 1e-5
+
+
 def _rel_close(got, want, name, tol=1e-3):
     got, want = got.detach().cpu().float(), want.detach().cpu().float()
     scale = float(want.abs().max()) or 1.0
     err = float((got - want).abs().max())
+    print(f"{name}: max|d|/max|ref| = {err / scale:.3e} (tol {tol:.0e})")
     assert err <= tol * scale, f"{name}: max |d| {err:.3e} vs max |ref| {scale:.3e}"
 
 
@@ -205,19 +214,25 @@ def test_latent_train_step_matches_oracle(gpu_device, tmp_path):
     assert abs(float(loss) - float(want)) <= 1e-5 * max(1.0, abs(float(want)))
     names = list(ref)
     for k in names:  # the raw gradients (the engine folds the clip into AdamW)
-        _rel_close(grads[k], ref[k].grad, f"d {k}")
+        _rel_close(grads[k], ref[k].grad, f"d {k}", tol=F32_GRAD_TOL)
     params = list(ref.values())
+    exact = float(torch.sqrt(sum((v.grad.double() ** 2).sum() for v in params)))
     total = float(torch.nn.utils.clip_grad_norm_(params, 0.5))
     before = {k: v.detach().clone() for k, v in ref.items()}
     opt = torch.optim.AdamW(params, lr=1e-6, weight_decay=0.01)
     opt.step()
-    # the step summed the squared norm itself, each stream over the gradients it wrote
-    # (exactly the norm of the gradients it returned; the reference's within the
-    # gradients' own tolerance, as test_train.py's final-attention step)
+    # the step summed the squared norm itself, each stream over the gradients it wrote:
+    # the norm of the gradients it returned, and the float64 norm of the oracle's
+    # gradients, both to f32 reassociation (measured 1.3e-8 - 3.9e-8 relative to the
+    # float64 oracle, r6a).  torch's own CPU clip_grad_norm_ is NOT that reference: its
+    # f32 reduction over the 8.4 M-element net.0 / net.2 weights loses 2.5e-4 relative
+    # (torch 2.10; 0.4268632 against the exact 0.4269765 on this batch), which is the
+    # whole of the 2.65e-4 gap round 5 read as a kernel error.
     norm = float(eng.sumsq.sqrt())
     own = float(torch.sqrt(sum((v.double() ** 2).sum() for v in grads.values())))
-    assert abs(norm - own) <= 1e-5 * own, (norm, own)
-    assert abs(norm - total) <= 1e-3 * total, (norm, total)
+    assert abs(norm - own) <= 1e-6 * own, (norm, own)
+    assert abs(norm - exact) <= 1e-6 * exact, (norm, exact)
+    assert abs(total - exact) <= 1e-3 * exact, (total, exact)  # the CPU reduction's own error, for the record
     for k in names:
         assert k in grads, k
         upd_ref = ref[k].detach() - before[k]

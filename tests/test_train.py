@@ -102,6 +102,7 @@ def _check_grads(got: dict, g, rtol_max=1e-3, prefix="grad"):
         want = g[f"{prefix}_val:{k}"]
         have = got[k].detach().reshape(-1).cpu().double().numpy()
         scale = max(np.abs(want).max(), 1e-12)
+        print(f"{prefix} {k}: max|d|/max|ref| = {np.abs(have[idx] - want).max() / scale:.3e} (tol {rtol_max:.0e})")
         assert np.abs(have[idx] - want).max() <= rtol_max * scale, k
         np.testing.assert_allclose(have.sum(), float(g[f"grad_sum:{k}"]), rtol=1e-3, atol=1e-3 * scale, err_msg=k)
 
@@ -173,8 +174,21 @@ def test_gpu_train_step_f32_matches_reference(gpu_device, tmp_path):
     torch.cuda.synchronize()
     assert abs(float(loss) - float(g["step_loss"])) <= 1e-5 * abs(float(g["step_loss"]))
     _check_grads(eng.grad_dict(), g)
+    hip = {k: v.detach().cpu().double() for k, v in eng.grad_dict().items()}
     eng.optimizer_step()
     norm = float(eng.sumsq.sqrt())
+    # the golden's total_norm is the reference's CPU clip_grad_norm_, whose f32 reduction
+    # over the 16.8 M-element weights loses 6.0e-4 (3.11763 vs the exact 3.11950 of the
+    # same gradients, torch 2.10): hold the step's norm to the float64 norm of the
+    # oracle's gradients (oracle pinned to the golden gradients above at 1e-5) instead
+    from oracle import train_ref
+    last, hg, pos, neg, _ = _oracle_batch(ds, states, 0, int(g["batch_size"]))
+    ref = train_ref.train_step(_params(), last, hg, pos, neg, do_step=False)["grads"]
+    exact = float(torch.sqrt(sum((v.double() ** 2).sum() for v in ref.values())))
+    own = float(torch.sqrt(sum((v ** 2).sum() for v in hip.values())))
+    print(f"grad norm: step {norm:.9g}, own {own:.9g}, float64 oracle {exact:.9g}, golden {float(g['step_total_norm']):.9g}")
+    assert abs(norm - own) <= 1e-6 * own, (norm, own)
+    assert abs(norm - exact) <= 1e-6 * exact, (norm, exact)
     assert abs(norm - float(g["step_total_norm"])) <= 1e-3 * float(g["step_total_norm"])
     for k in g["step_grad_names"]:
         k = str(k)

@@ -27,6 +27,16 @@ is held to the model, per parameter tensor, d = p_22 - p_0 (the trained change):
   (margins: two bf16 realisations of the same arithmetic, summed in different
   orders, differ by a few % of their drift; 25-50 % slack and the absolute
   floors keep the check about the level, not the noise)
+and, independent of the model, a FIXED ceiling per (engine, lr) (a
+rounding point the model and the kernels shared but the reference lacked would
+raise both together and pass the relative check above):
+  ABS_CEIL   update rel err <= c_rel and 1 - cosine <= c_cos, every tensor
+  FinalAttention: the ceilings sit at ideal bf16 arithmetic's own drift on these
+  batches as the model measured it once (worst tensor linear4.bias: 0.141 /
+  0.9902 at lr 1e-6, 0.261 / 0.9663 at 1e-4) rounded up to the
+  next round number -- 0.15 / 0.99 and 0.28 / 0.96: the HIP step may not drift
+  beyond the format's floor, whatever the model says today.  Latent: its model
+  drifts 0.013 (cosine 0.9999): ceilings 0.03 / 0.999 at both lrs.
 and, at the reference's lr = 1e-6, the trained model itself: the bf16-trained
 pooler against the oracle-trained one (oracle eval) on 200,000 held-out
 impressions over 8,192 held-out news, clicks ~ logistic of the oracle score,
@@ -47,6 +57,9 @@ UPD_REL = (1.25, 0.01)      # HIP update rel err <= a * model + b
 UPD_COS = (1.5, 2e-3)       # 1 - HIP update cosine <= a * (1 - model cosine) + b
 LOSS = (2.0, 1e-5)          # per-step |l_hip - l_f32| <= a * model max + b |l_f32|
 AUC_4DP = 5e-5              # |dAUC| < half a unit in the 4th decimal
+# (engine, lr) -> (max update rel err, max 1 - update cosine): model-independent ceilings
+ABS_CEIL = {("final", 1e-6): (0.15, 0.01), ("final", 1e-4): (0.28, 0.04),
+            ("latent", 1e-6): (0.03, 1e-3), ("latent", 1e-4): (0.03, 1e-3)}
 HELD_NEWS, HELD_IMPS = 8192, 200_000
 
 
@@ -153,9 +166,11 @@ def test_bf16_training_tracks_f32_oracle(gpu_device, tmp_path, pooler, lr):
     worst = min(hip, key=lambda k: hip[k][0])
     print(f"[bf16 drift] {pooler} lr={lr:g}: worst tensor {worst}: update cosine {hip[worst][0]:.4f} "
           f"(bf16 model {mod[worst][0]:.4f}), rel err {hip[worst][1]:.3f} (model {mod[worst][1]:.3f})")
+    c_rel, c_cos = ABS_CEIL[(pooler, lr)]
     for k in hip:
         assert hip[k][1] <= UPD_REL[0] * mod[k][1] + UPD_REL[1], (pooler, lr, k, hip[k], mod[k])
         assert 1 - hip[k][0] <= UPD_COS[0] * (1 - mod[k][0]) + UPD_COS[1], (pooler, lr, k, hip[k], mod[k])
+        assert hip[k][1] <= c_rel and 1 - hip[k][0] <= c_cos, ("absolute ceiling", pooler, lr, k, hip[k])
     if lr != LRS[0]:
         return
 

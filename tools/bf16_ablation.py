@@ -12,6 +12,9 @@ oracle/train_ref.train_step (f32 autograd) per variant:
   grads f32           backward activations unrounded
   w-branch f32        X, Y, P, W4, W5 unrounded in the forward
   exact fwd, bf16 bwd forward unrounded, backward as hip-like
+  S,X1,X2 bf16x2      the inputs of linear1..3 kept as hi + lo bf16 pairs (2x
+                      those GEMMs' forward MFMA work), weights and the rest bf16
+  +W1..W3 bf16x2      the same with W1..W3 also split (4 products: 4x)
     python tools/bf16_ablation.py [--batches 2]
 """
 import argparse
@@ -34,8 +37,14 @@ def ident(t):
     return t
 
 
-def step(P, tl, hg, pos, neg, grads32=False, wbranch32=False, exact_fwd=False):
+def bf2(t):
+    hi = bf(t)
+    return hi + bf(t - hi)
+
+
+def step(P, tl, hg, pos, neg, grads32=False, wbranch32=False, exact_fwd=False, x2_in=False, x2_w=False):
     qa = ident if exact_fwd else bf           # forward activations
+    qi = bf2 if x2_in else qa                 # the inputs of linear1..3
     qg = ident if grads32 else bf             # backward activations
     E = F.layer_norm(tl.float(), (1024,), P["ln.weight"], P["ln.bias"], 1e-12)
     idx = torch.as_tensor(np.concatenate(hg).astype(np.int64))
@@ -44,10 +53,12 @@ def step(P, tl, hg, pos, neg, grads32=False, wbranch32=False, exact_fwd=False):
     seg = torch.repeat_interleave(torch.arange(B), torch.as_tensor(lens))
     Wb = {i: bf(P[f"linear{i}.weight"]) for i in range(1, 6)}          # backward weights: bf16
     Wf = {i: (P[f"linear{i}.weight"] if exact_fwd or (wbranch32 and i >= 4) else Wb[i]) for i in range(1, 6)}
+    if x2_w:
+        Wf.update({i: bf2(P[f"linear{i}.weight"]) for i in (1, 2, 3)})
     b = {i: P[f"linear{i}.bias"] for i in range(1, 5)}
-    S = qa(E[idx])
-    X1 = qa(F.relu(S @ Wf[1].T + b[1]))
-    X2 = qa(F.relu(X1 @ Wf[2].T + b[2]))
+    S = qi(E[idx])
+    X1 = qi(F.relu(S @ Wf[1].T + b[1]))
+    X2 = qi(F.relu(X1 @ Wf[2].T + b[2]))
     Xf = X2 @ Wf[3].T + b[3]
     X = Xf if wbranch32 else qa(Xf)
     Y = F.relu(X @ Wf[4].T + b[4])
@@ -88,7 +99,8 @@ def main():
     ds = _dataset(g, labels)
     p0 = _params("final")
     variants = [("hip-like", {}), ("grads f32", {"grads32": True}), ("w-branch f32", {"wbranch32": True}),
-                ("exact fwd, bf16 bwd", {"exact_fwd": True})]
+                ("exact fwd, bf16 bwd", {"exact_fwd": True}), ("S,X1,X2 bf16x2", {"x2_in": True}),
+                ("+W1..W3 bf16x2", {"x2_in": True, "x2_w": True})]
     for r in ds.batches()[:args.batches]:
         tl, hg, pos, neg = _oracle_batch(ds, states, *r)[:4]
         ref = train_ref.train_step(p0, tl, hg, pos, neg, do_step=False)["grads"]
