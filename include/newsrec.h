@@ -589,24 +589,6 @@ int64_t nr_final_train_workspace_bytes(int dtype, int64_t B, int64_t U, int64_t 
 int nr_final_train_step(const nr_final_train_args* args, void* ws, int64_t ws_bytes, void* stream);
 
 /*
- * ---- Host <-> device transfers of the drop-in API (csrc/xfer.hip): the CSR
- * index arrays and the news table up, scores / ranks down.  Replaces the
- * reference's pageable `.to(DEVICE)` / `.cpu()` copies (data_model_helper.py:
- * 112-131, 199-230, 416-443).  The bytes move through a process-wide ring of
- * pinned chunks, pipelined: NR_COPY_THREADS (default 8) host threads copy chunk
- * i between the caller's pageable memory and the ring while the DMA engine
- * moves chunk i - 1 (hipMemcpyAsync on `stream`).
- * nr_copy_h2d: dst device, src host; returns once src has been read (reusable);
- *   the data lands in stream order.
- * nr_copy_d2h: dst host, src device; returns with dst complete (the copy runs
- *   in stream order after the work queued before it).
- * Calls are serialised process-wide.  Errors: NR_ERR_INVALID for a null pointer,
- * bytes < 0 or a non-device pointer on the device side; NR_ERR_HIP otherwise.
- */
-int nr_copy_h2d(void* dst, const void* src, int64_t bytes, void* stream);
-int nr_copy_d2h(void* dst, const void* src, int64_t bytes, void* stream);
-
-/*
  * ---- RCCL communicator of the multi-GPU eval (SURVEY §8(b) nr_allgather,
  * §8(e)): one process per GPU; every rank transforms a row shard of the
  * per-news table and ONE all-gather over xGMI gives each GPU the whole table.

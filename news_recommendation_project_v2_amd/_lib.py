@@ -18,7 +18,7 @@ CSRC = Path(__file__).resolve().with_name("csrc")
 INCLUDE = Path(__file__).resolve().parent.parent / "include"
 # translation units of libnewsrec_hip.so, in link order (also the hash order)
 HIP_SOURCES = ("capi.hip", "gemm.hip", "pool_score.hip", "rowops.hip", "rank.hip", "encoder.hip", "train.hip",
-               "metrics.hip", "comm.hip", "latent_train.hip", "final_train.hip", "xfer.hip")
+               "metrics.hip", "comm.hip", "latent_train.hip", "final_train.hip")
 
 
 def hip_source_files() -> list:
@@ -82,8 +82,6 @@ SIGNATURES = {
     "nr_latent_train_step": (_i, [_p, _p, _l, _p]),
     "nr_final_train_workspace_bytes": (_l, [_i, _l, _l, _l]),
     "nr_final_train_step": (_i, [_p, _p, _l, _p]),
-    "nr_copy_h2d": (_i, [_p, _p, _l, _p]),
-    "nr_copy_d2h": (_i, [_p, _p, _l, _p]),
     "nr_comm_unique_id": (_i, [_p]),
     "nr_comm_init": (_i, [_p, _p, _i, _i]),
     "nr_comm_init_timeout": (_i, [_p, _p, _i, _i, _l]),

@@ -41,35 +41,41 @@ def _may_repeat(hist_idx: np.ndarray, hist_len: np.ndarray) -> bool:
     return 1.0 - len(np.unique(key)) / len(hist_len) >= DEDUPE_MIN_SHARE
 
 
-def _check_segments(idx: np.ndarray, lens: np.ndarray, what: str) -> int:
-    """Validate one CSR index set on the host; returns its largest row (-1 if
-    empty).  Negative lengths, a length sum that does not match the index
-    array (the offsets would run past it on the device) and negative rows are
-    refused; rows past a table are refused once the table size is known."""
+def _check_segments(idx: np.ndarray, lens: np.ndarray, what: str) -> None:
+    """Validate one CSR index set's lengths on the host (I entries): negative
+    lengths and a length sum that does not match the index array (the offsets
+    would run past it on the device) are refused.  The rows themselves are
+    range-checked on the device after the upload (_row_range)."""
     if len(lens) and int(lens.min()) < 0:
         raise ValueError(f"{what} lengths must be >= 0")
     if int(lens.sum()) != len(idx):
         raise ValueError(f"{what} lengths sum to {int(lens.sum())} but {len(idx)} indices were given")
-    if not len(idx):
+
+
+def _row_range(idx: torch.Tensor, what: str) -> int:
+    """Largest row of an uploaded index array (-1 if empty); a negative row is
+    refused (IndexError, as torch indexing does).  One min/max reduction where
+    the array already is (on the device: microseconds for the 26 M MIND-large-dev
+    rows that took ~20 ms of host passes) and one small sync."""
+    if idx.numel() == 0:
         return -1
-    lo, hi = int(idx.min()), int(idx.max())
+    lo, hi = (int(v) for v in torch.aminmax(idx))
     if lo < 0:
         raise IndexError(f"{what} index {lo} is negative (rows are 0-based indices into the news table)")
     return hi
 
 
 def _upload(x, dev: torch.device, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
-    """Host arrays / CPU tensors go up through the library's pinned staging ring
-    (ops.to_device, nr_copy_h2d: the pageable `.to()` ran at 14 GB/s, round 5);
-    a table converts to the compute dtype on the device.  Device tensors stay
-    where they are (converted / made contiguous by torch)."""
-    if isinstance(x, torch.Tensor) and x.device.type != "cpu":
-        return x.to(dev, dtype if dtype is not None else x.dtype).contiguous()
-    if dev.type != "cuda":
-        t = torch.as_tensor(x)
-        return t.to(dev, dtype if dtype is not None else t.dtype).contiguous()
-    t = ops.to_device(x, dev)
-    return t if dtype is None or t.dtype == dtype else t.to(dtype)
+    """Host arrays / CPU tensors to the device; a table converts to the compute
+    dtype on the device.  torch's own host-to-device copy of pageable memory runs
+    at the PCIe DMA rate here (56 GB/s for the MIND-large-dev index arrays,
+    tools/pcie_probe.py, profiles/round6/pcie_probe.jsonl), faster than staging
+    through a ring of pinned chunks (45 GB/s, measured and removed in round 6):
+    the round-5 "14 GB/s" upload was load_impressions' host-side checks and
+    offsets, not the copy."""
+    t = torch.as_tensor(x)
+    t = t.to(dev)
+    return (t if dtype is None or t.dtype == dtype else t.to(dtype)).contiguous()
 
 
 class PoolScoreEngine:
@@ -111,14 +117,22 @@ class PoolScoreEngine:
         hist_len = np.asarray(hist_len, dtype=np.int64)
         cand_idx = np.ascontiguousarray(cand_idx, dtype=np.int32)
         cand_len_a = np.asarray(cand_len, dtype=np.int64)
+        _check_segments(hist_idx, hist_len, "history")
+        _check_segments(cand_idx, cand_len_a, "candidate")
+        hi_d, ci_d = _upload(hist_idx, dev), _upload(cand_idx, dev)
         # the kernels index tables with these rows: an out-of-range row would be an
-        # out-of-bounds device read, so refuse it here as torch indexing does (IndexError)
-        self._max_row = {"hist": _check_segments(hist_idx, hist_len, "history"),
-                         "cand": _check_segments(cand_idx, cand_len_a, "candidate")}
-        self._check_rows()
-        self.hist_idx = _upload(hist_idx, dev)
+        # out-of-bounds device read, so refuse it here, before the engine takes the
+        # arrays (a refused load leaves the previous impressions in place), as torch
+        # indexing does (IndexError)
+        max_row = {"hist": _row_range(hi_d, "history"), "cand": _row_range(ci_d, "candidate")}
+        prev, self._max_row = getattr(self, "_max_row", None), max_row
+        try:
+            self._check_rows()
+        except IndexError:
+            self._max_row = prev
+            raise
+        self.hist_idx, self.cand_idx = hi_d, ci_d
         self.hist_off = _upload(lengths_to_offsets(hist_len), dev)
-        self.cand_idx = _upload(cand_idx, dev)
         self.cand_off = _upload(lengths_to_offsets(cand_len_a), dev)
         self.n_cand = int(cand_len_a.sum())
         self.n_imp = len(cand_len)

@@ -62,76 +62,6 @@ def _dtype(t: torch.Tensor, name: str) -> int:
     return _DT[t.dtype]
 
 
-def h2d(dst: torch.Tensor, src) -> torch.Tensor:
-    """Copy a host array (numpy array or CPU tensor, C-contiguous, the same
-    byte count) into the contiguous device tensor ``dst`` through the library's
-    pinned staging ring (nr_copy_h2d).  Returns once ``src`` has been read;
-    the data lands in stream order."""
-    import numpy as np
-    dev = _dev(dst)
-    if not dst.is_contiguous():
-        raise _lib.NewsRecHIPError("h2d: dst must be contiguous")
-    if isinstance(src, torch.Tensor):
-        if src.device.type != "cpu" or not src.is_contiguous():
-            raise _lib.NewsRecHIPError("h2d: src must be a contiguous CPU tensor or numpy array")
-        ptr, nb = src.data_ptr(), src.numel() * src.element_size()
-    else:
-        src = np.asarray(src)
-        if not src.flags.c_contiguous:
-            raise _lib.NewsRecHIPError("h2d: src must be C-contiguous")
-        ptr, nb = src.ctypes.data, src.nbytes
-    if nb != dst.numel() * dst.element_size():
-        raise _lib.NewsRecHIPError(f"h2d: {nb} source bytes for a {dst.numel() * dst.element_size()}-byte tensor")
-    _lib.call("nr_copy_h2d", _ptr(dst), ctypes.c_void_p(ptr), nb, _stream(dev))
-    return dst
-
-
-def d2h(dst, src: torch.Tensor):
-    """Copy the contiguous device tensor ``src`` into a host array (numpy array
-    or CPU tensor, C-contiguous, the same byte count) through the pinned
-    staging ring (nr_copy_d2h); ``dst`` is complete on return."""
-    import numpy as np
-    dev = _dev(src)
-    if not src.is_contiguous():
-        raise _lib.NewsRecHIPError("d2h: src must be contiguous")
-    if isinstance(dst, torch.Tensor):
-        if dst.device.type != "cpu" or not dst.is_contiguous():
-            raise _lib.NewsRecHIPError("d2h: dst must be a contiguous CPU tensor or numpy array")
-        ptr, nb = dst.data_ptr(), dst.numel() * dst.element_size()
-    else:
-        if not isinstance(dst, np.ndarray) or not dst.flags.c_contiguous or not dst.flags.writeable:
-            raise _lib.NewsRecHIPError("d2h: dst must be a writeable C-contiguous numpy array")
-        ptr, nb = dst.ctypes.data, dst.nbytes
-    if nb != src.numel() * src.element_size():
-        raise _lib.NewsRecHIPError(f"d2h: {nb} destination bytes for a {src.numel() * src.element_size()}-byte tensor")
-    _lib.call("nr_copy_d2h", ctypes.c_void_p(ptr), _ptr(src), nb, _stream(dev))
-    return dst
-
-
-def to_device(arr, device: torch.device, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
-    """A host array as a new device tensor (h2d); ``dtype`` converts first on
-    the host (numpy) when given and different."""
-    import numpy as np
-    if isinstance(arr, torch.Tensor):
-        arr = arr.detach()
-        if dtype is not None and arr.dtype != dtype:
-            arr = arr.to(dtype)
-        arr = arr.contiguous()
-        out = torch.empty(arr.shape, dtype=arr.dtype, device=device)
-    else:
-        arr = np.ascontiguousarray(arr)
-        out = torch.empty(arr.shape, dtype=torch.from_numpy(arr[:0]).dtype, device=device)
-    return h2d(out, arr)
-
-
-def to_host(t: torch.Tensor):
-    """A device tensor as a new numpy array (d2h)."""
-    import numpy as np
-    t = t.contiguous()
-    out = np.empty(tuple(t.shape), dtype=torch.empty(0, dtype=t.dtype).numpy().dtype)
-    return d2h(out, t)
-
-
 def set_persistent_workgroups(n: int = 0) -> None:
     """Workgroups of the persistent bf16 GEMM launches (0 = one per CU): set it
     to the CU count of a CU-masked stream the transform runs on."""

@@ -299,6 +299,20 @@ class FinalAttentionTrainStep:
         fwd = 2.0 * Hp * (D * H + H * H + H * D + D * H + H * D)
         return 3.0 * fwd
 
+    def hbm_bytes_per_step(self, Hs: int, U: int) -> dict:
+        """Algorithmic HBM bytes of the step's non-GEMM kernels (the GEMMs are
+        priced by their FLOPs): AdamW 30 B per parameter (f32 param, grad, m, v
+        read; param, m, v written; the bf16 mirror written) and the row kernels
+        per history slot (es = 2 bf16): slots_kernel reads the token row and
+        writes S and XH (2 D es), pool fwd reads (X, P) (2 D es), pool bwd reads
+        them again and writes dXp and dL (4 D es) -- 8 D es per slot -- plus the
+        four weight transposes read and written once (W5, W4, W3: D H each;
+        W2: H H)."""
+        es = 2 if self.dtype == torch.bfloat16 else 4
+        Hp = _pad64(Hs)
+        rows = Hp * 8 * D * es + U * D * 2 + 2 * es * (3 * D * H + H * H)
+        return {"adamw": 30.0 * self.n_flat, "row_kernels": float(rows)}
+
 
 class LatentAttentionTrainStep:
     """Config-5 step with ``LatentAttentionModel`` in the pooler slot (BASELINE
@@ -448,6 +462,20 @@ class LatentAttentionTrainStep:
         row = 2.0 * Bp * 4096 * D                                  # m = mean(Z) W2^T
         fold = 2.0 * 64 * D * 8192 + 2 * (2.0 * 8 * 64 * 512 * D)  # KV, A, Bt^T
         return 3.0 * (slot + row + fold)
+
+    def hbm_bytes_per_step(self, Hs: int, U: int) -> dict:
+        """Algorithmic HBM bytes of the step's non-GEMM kernels (the GEMMs are
+        priced by their FLOPs): AdamW 30 B per parameter (f32 param, grad, m, v
+        read; param, m, v written; the bf16 mirror written) and the row kernels
+        per history slot (es = 2 bf16): gather + LN_q writes S and X (2 D es);
+        segmean reads G and H1 (8192 es + D es); the GEGLU backward reads G and
+        writes dG (2 x 8192 es); the LN_f backward reads H1 and dY and writes dH1
+        (3 D es); the LN_q backward reads dX and X and adds dE in f32 (2 D es +
+        4 D) -- 32,768 es + 4 D bytes per slot -- plus the token rows read."""
+        es = 2 if self.dtype == torch.bfloat16 else 4
+        Hp = _pad64(Hs)
+        per_slot = (2 * D + 8192 + D + 2 * 8192 + 3 * D + 2 * D) * es + 4 * D
+        return {"adamw": 30.0 * self.n_flat, "row_kernels": float(Hp * per_slot + U * D * 2)}
 
     def model_flops_per_step(self, Hs: int) -> float:
         """The reference formulation's GEMM FLOPs (every linear layer per history

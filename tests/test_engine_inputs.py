@@ -4,7 +4,10 @@ The device kernels index the news tables with the CSR rows, so a row past a
 table (or offsets that run past the index array) would be an out-of-bounds
 device read.  The reference gathers rows by array indexing (e.g.
 data_model_helper.py:284), which raises IndexError; the engine refuses the same
-inputs on the host before any upload.  CPU-only: validation runs before .to().
+inputs before any kernel can read them: lengths on the host, the rows' range by
+one min/max reduction of the uploaded arrays (on the device on a GPU), and a
+refused load leaves the previous impressions in place.  CPU-only here (a CPU
+"device"); the GPU path is the same code.
 """
 import numpy as np
 import pytest
@@ -60,3 +63,13 @@ def test_table_loaded_after_impressions_is_checked():
     with pytest.raises(IndexError, match="candidate index 7 is out of bounds for dimension 0 with size 5"):
         eng.load_news(torch.zeros(5, 4), torch.zeros(8, 4))
     eng.load_news(torch.zeros(8, 4), torch.zeros(5, 4))  # history 4 < 5, candidate 7 < 8
+
+
+def test_refused_load_keeps_previous_impressions():
+    eng = _engine(10)
+    eng.load_impressions(_i(1, 2), [2], _i(3, 4), [2])
+    before = (eng.hist_idx.clone(), eng.cand_idx.clone(), dict(eng._max_row))
+    with pytest.raises(IndexError):
+        eng.load_impressions(_i(1, 2), [2], _i(3, 11), [2])
+    assert torch.equal(eng.hist_idx, before[0]) and torch.equal(eng.cand_idx, before[1])
+    assert eng._max_row == before[2]

@@ -40,8 +40,6 @@ def _calls(P):
     layer = _lib.EncoderLayer(*([P.value] * 12))
     return {
         "nr_gemm": (F32, F32, 0, 4, 128, 32, P, 32, P, 32, None, None, 0, P, 128, None),
-        "nr_copy_h2d": (P, P, 4096, None),  # the device side (dst) is checked
-        "nr_copy_d2h": (P, P, 4096, None),  # the device side (src) is checked
         "nr_gemm_relu_dropout": (BF16, BF16, 4, 256, 64, P, 64, P, 64, P, P, 256, 7, f(0.1), None),
         "nr_gemm_drelu": (BF16, BF16, 4, 256, 64, P, 64, P, 64, P, 256, P, 256, f(1.0), None),
         "nr_gemm_grouped": (BF16, F32, 1, (L * 1)(256), (L * 1)(256), (L * 1)(64), ptrs, (L * 1)(64), ptrs,

@@ -7,8 +7,9 @@ batching, its collate fn, one hand-run step of the train_one_epoch body and a
 full train_one_epoch.  Parameter tensors are pinned through 2048 sampled
 elements each (the fixture must stay small).
 
-Tolerances: f32 loss 1e-5 relative; f32 gradients 1e-3 relative to each
-tensor's max |g| (MFMA f32 vs CPU summation order over 4096-long dots);
+Tolerances: f32 loss 1e-5 relative; the f32 step's gradients 1e-5 relative to
+each tensor's max |g| (MFMA f32 vs CPU summation order over 4096-long dots;
+measured <= 2.5e-6), the multi-batch / dropout checks 1e-3;
 AdamW-updated parameters 3e-8 absolute + 2 f32 ulps of the parameter (the
 lr = 1e-6 update is ~1e-6 per element); bf16 step: loss within 2e-2 relative and gradient cosine > 0.99 of f32.
 """
@@ -173,7 +174,9 @@ def test_gpu_train_step_f32_matches_reference(gpu_device, tmp_path):
     loss, _, _ = eng.forward_backward(batch)
     torch.cuda.synchronize()
     assert abs(float(loss) - float(g["step_loss"])) <= 1e-5 * abs(float(g["step_loss"]))
-    _check_grads(eng.grad_dict(), g)
+    # exact-f32 MFMA against the reference's own CPU f32 gradients: measured <= 2.5e-6 of
+    # each tensor's max (linear4, r6b), f32 reassociation of 8,310-slot / 4,096-long sums
+    _check_grads(eng.grad_dict(), g, rtol_max=1e-5)
     hip = {k: v.detach().cpu().double() for k, v in eng.grad_dict().items()}
     eng.optimizer_step()
     norm = float(eng.sumsq.sqrt())
@@ -187,8 +190,13 @@ def test_gpu_train_step_f32_matches_reference(gpu_device, tmp_path):
     exact = float(torch.sqrt(sum((v.double() ** 2).sum() for v in ref.values())))
     own = float(torch.sqrt(sum((v ** 2).sum() for v in hip.values())))
     print(f"grad norm: step {norm:.9g}, own {own:.9g}, float64 oracle {exact:.9g}, golden {float(g['step_total_norm']):.9g}")
-    assert abs(norm - own) <= 1e-6 * own, (norm, own)
-    assert abs(norm - exact) <= 1e-6 * exact, (norm, exact)
+    # the f32 step's norm is nr_sumsq over the 11 gradient arrays: per-thread f32 sums of
+    # ~128 squares and 11 x 1,024 block partials added by f32 atomics (measured 5.3e-6 off
+    # the float64 norm of the same gradients, r6b; the gradients themselves are 2.6e-8 off
+    # the float64 oracle's): the bound is that reduction's f32 rounding, not the kernels'
+    print(f"grad norm rel: step vs own {abs(norm - own) / own:.2e}, own vs float64 oracle {abs(own - exact) / exact:.2e}")
+    assert abs(own - exact) <= 1e-6 * exact, (own, exact)
+    assert abs(norm - own) <= 2e-5 * own, (norm, own)
     assert abs(norm - float(g["step_total_norm"])) <= 1e-3 * float(g["step_total_norm"])
     for k in g["step_grad_names"]:
         k = str(k)

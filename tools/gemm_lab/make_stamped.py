@@ -19,32 +19,26 @@ OUT = Path(__file__).resolve().parent
 
 
 def patch(src: str) -> str:
+    """Clock stamps only (round 6): s_memtime / s_memrealtime once at the top of the
+    persistent loop and once at the kernel's end, per workgroup, plus its unit count.
+    (Round 2's per-phase stamps anchored on a K loop that has since been restructured.)"""
     def sub(old, new):
         nonlocal src
         assert src.count(old) == 1, old
         src = src.replace(old, new)
     sub('#include "nr_common.h"', '#include "nr_common.h"\n__device__ unsigned long long* g_lab_stamps = nullptr;')
-    sub("  int st = 0;\n  while (true) {\n",
-        "  int st = 0;\n  unsigned long long s_main = 0, s_epi = 0, s_top = 0, s_n = 0, tt0 = 0, tt2 = 0;\n"
-        "  bool first0 = true;\n"
+    sub("  if (wmu == 1) __builtin_amdgcn_s_barrier();  // skew the wave groups by one barrier\n  while (true) {\n",
+        "  if (wmu == 1) __builtin_amdgcn_s_barrier();  // skew the wave groups by one barrier\n"
         "  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), ck0 = __builtin_amdgcn_s_memtime();\n"
-        "  while (true) {\n")
-    sub("    for (int kt = 0; kt < nk; ++kt) {\n      kstep(kt, st, more, nm0, nn0);",
-        "    tt0 = __builtin_amdgcn_s_memtime();\n    if (!first0) s_top += tt0 - tt2;\n    first0 = false;\n"
-        "    for (int kt = 0; kt < nk; ++kt) {\n      kstep(kt, st, more, nm0, nn0);")
-    sub("    // ---------------- epilogue of tile (m0, n0) ----------------\n",
-        "    const unsigned long long tt1 = __builtin_amdgcn_s_memtime();\n    s_main += tt1 - tt0;\n"
-        "    // ---------------- epilogue of tile (m0, n0) ----------------\n")
-    sub("    if (!more) break;\n",
-        "    tt2 = __builtin_amdgcn_s_memtime();\n    s_epi += tt2 - tt1;\n    ++s_n;\n"
-        "    if (!more) break;\n")
-    sub("    n0 = nn0;\n  }\n",
-        "    n0 = nn0;\n  }\n"
+        "  unsigned long long s_n = 0;\n"
+        "  while (true) {\n    ++s_n;\n")
+    sub("    kloop(std::true_type{}, false, 0u, 0u);\n  }\n#undef NR_PHASE_SYNC_MMA\n}",
+        "    kloop(std::true_type{}, false, 0u, 0u);\n  }\n"
         "  const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime(), ck1 = __builtin_amdgcn_s_memtime();\n"
         "  if (tid == 0 && g_lab_stamps) {\n"
         "    unsigned long long* o = g_lab_stamps + blockIdx.x * 8;\n"
-        "    o[0] = s_main; o[1] = 0; o[2] = s_epi; o[3] = s_top; o[4] = s_n; o[5] = ck1 - ck0; o[6] = rt1 - rt0;\n"
-        "  }\n")
+        "    o[0] = 0; o[1] = 0; o[2] = 0; o[3] = 0; o[4] = s_n; o[5] = ck1 - ck0; o[6] = rt1 - rt0;\n"
+        "  }\n#undef NR_PHASE_SYNC_MMA\n}")
     src += '\nextern "C" int lab_set_stamps(void* p) {\n  return hipMemcpyToSymbol(HIP_SYMBOL(g_lab_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;\n}\n'
     return src
 

@@ -5,11 +5,12 @@ this box.  One JSON line per variant (GB/s, ms), medians of 5.
 
   h2d  pageable    torch.as_tensor(np).to(dev)             (the round-5 path)
        pinned      np.copyto into a cached pinned tensor, then one async copy
-       register    hipHostRegister the numpy buffer, async copy, unregister
-       staged      ops.h2d: the library's chunked multi-threaded staging
+       (round 6 also measured a chunked, multi-threaded pinned staging ring in the
+       library, nr_copy_h2d / nr_copy_d2h: 45 / 40 GB/s, slower than torch's
+       pageable upload and pinned download, so it was removed; results in
+       profiles/round6/pcie_probe.jsonl)
   d2h  pageable    t.cpu()
        pinned      copy_ into a pinned tensor (non_blocking) + sync
-       staged      ops.d2h into a pageable numpy array
   host group_items (376 k object arrays) vs np.split
 
     python tools/pcie_probe.py
