@@ -66,4 +66,3 @@ def test_gemm_grouped_tn_rejects_bad_shapes(gpu_device):
     w = torch.zeros((64, 256), device=gpu_device, dtype=torch.bfloat16)
     with pytest.raises(Exception, match="M, N"):
         ops.gemm_grouped_tn([(a, w, torch.zeros((200, 256), device=gpu_device))])
-
