@@ -166,7 +166,9 @@ def group_items(items: np.ndarray, imp_counts: np.ndarray,
     """Split ``items`` into consecutive runs of ``imp_counts`` (data_utils.py:400-411)."""
     ends = np.cumsum(np.asarray(imp_counts, dtype=np.int64))
     starts = ends - np.asarray(imp_counts, dtype=np.int64)
-    return np.array([func(items[s:e]) for s, e in zip(starts, ends)], dtype=object)
+    # slice bounds as Python ints (.tolist()): iterating numpy int64 scalars cost
+    # ~45 % of this call for MIND-large-dev's 376 k impressions (tools/pcie_probe.py)
+    return np.array([func(items[s:e]) for s, e in zip(starts.tolist(), ends.tolist())], dtype=object)
 
 
 def lengths_to_offsets(lengths: np.ndarray) -> np.ndarray:

@@ -4,8 +4,9 @@ a torch optimizer step -- the calls trainer.py:1046-1069 makes -- with the
 forward and backward on the HIP kernels (modeling_utils._FinalAttentionFn).
 Gradients are checked against torch autograd of the oracle's restatement of
 modeling_utils.py:195-228 (oracle/train_ref.final_attention_train: train mode,
-dropout drawn from the same counter-hash stream), with the tolerances of
-tests/test_train.py (each gradient within 1e-3 of its tensor's max)."""
+dropout drawn from the same counter-hash stream): each f32 gradient within 1e-5
+of its tensor's max, as the f32 step in tests/test_train.py; the oracle side
+clips with an exact norm (_clip_exact)."""
 import numpy as np
 import pytest
 import torch
@@ -30,10 +31,25 @@ def _batch(seed=0, B=6, L=11, D=1024):
     return torch.from_numpy(emb), torch.from_numpy(mask), slot_rows
 
 
-def _rel_close(got, want, name, tol=1e-3):
+def _clip_exact(params, max_norm):
+    """torch.nn.utils.clip_grad_norm_ (coefficient max_norm / (norm + 1e-6), clamped
+    to 1) with the norm summed in float64: torch 2.10's CPU clip sums the squares
+    in f32 and lands 2.5e-4 - 5.7e-4 low on these 4 M - 17 M-element gradients
+    (DESIGN.md §4), which scaled every clipped CPU gradient by that much."""
+    total = float(torch.sqrt(sum((q.grad.double() ** 2).sum() for q in params)))
+    coef = min(max_norm / (total + 1e-6), 1.0)
+    for q in params:
+        q.grad.mul_(coef)
+
+
+def _rel_close(got, want, name, tol=1e-5):
+    """max |got - want| <= tol * max |want|; f32 gradients through the module API
+    measured <= 3.7e-6 of their max (r6h, dropout 0 and 0.1): 1e-5 is f32
+    reassociation of the slot sums with ~3x margin.  Prints the achieved ratio."""
     got, want = got.detach().cpu().float(), want.detach().cpu().float()
     scale = float(want.abs().max()) or 1.0
     err = float((got - want).abs().max())
+    print(f"{name}: max|d|/max|ref| = {err / scale:.3e} (tol {tol:.0e})")
     assert err <= tol * scale, f"{name}: max |d| {err:.3e} vs max |ref| {scale:.3e}"
 
 
@@ -94,7 +110,10 @@ def test_reference_training_loop_through_the_module(gpu_device):
         opt = torch.optim.AdamW(params, lr=1e-6, weight_decay=0.01)
         opt.zero_grad()
         loss.backward()
-        torch.nn.utils.clip_grad_norm_(params, 0.5)
+        if params[0].device.type == "cpu":
+            _clip_exact(params, 0.5)  # the oracle side: clip_grad_norm_'s math with an exact norm
+        else:
+            torch.nn.utils.clip_grad_norm_(params, 0.5)
         opt.step()
         upd = [(q.detach() - b).cpu() for q, b in zip(params, before)]
         return float(loss), [q.grad.detach().cpu() for q in params], upd

@@ -9,8 +9,8 @@ latent-attention backward; no reference script trains this module, so the
 oracle is torch autograd of the reference's forward as restated in
 oracle/pool_ref.latent_attention_forward (latent_attention.py:157-170, pinned
 to the reference's golden outputs by tests/test_oracle_golden.py).
-Tolerances as tests/test_train.py: outputs 1e-4, each gradient within 1e-3
-of its tensor's max."""
+Tolerances: outputs 1e-4, each f32 gradient within F32_GRAD_TOL (1e-5) of its
+tensor's max (measured <= 2.7e-6 through the module API, r6c)."""
 import numpy as np
 import pytest
 import torch
@@ -38,7 +38,18 @@ def _batch(seed=0, lens=(11, 3, 1, 7, 2, 5), L=11, D=1024):
 F32_GRAD_TOL = 1e-5
 
 
-def _rel_close(got, want, name, tol=1e-3):
+def _clip_exact(params, max_norm):
+    """torch.nn.utils.clip_grad_norm_ (coefficient max_norm / (norm + 1e-6), clamped
+    to 1) with the norm summed in float64: torch 2.10's CPU clip sums the squares
+    in f32 and lands 2.5e-4 - 5.7e-4 low on these 4 M - 17 M-element gradients
+    (DESIGN.md §4), which scaled every clipped CPU gradient by that much."""
+    total = float(torch.sqrt(sum((q.grad.double() ** 2).sum() for q in params)))
+    coef = min(max_norm / (total + 1e-6), 1.0)
+    for q in params:
+        q.grad.mul_(coef)
+
+
+def _rel_close(got, want, name, tol=F32_GRAD_TOL):
     got, want = got.detach().cpu().float(), want.detach().cpu().float()
     scale = float(want.abs().max()) or 1.0
     err = float((got - want).abs().max())
@@ -120,7 +131,10 @@ def test_latent_attention_training_step_matches_oracle(gpu_device):
         opt = torch.optim.AdamW(params, lr=1e-6, weight_decay=0.01)
         opt.zero_grad()
         loss.backward()
-        torch.nn.utils.clip_grad_norm_(params, 0.5)
+        if params[0].device.type == "cpu":
+            _clip_exact(params, 0.5)  # the oracle side: clip_grad_norm_'s math with an exact norm
+        else:
+            torch.nn.utils.clip_grad_norm_(params, 0.5)
         opt.step()
         return float(loss.detach()), [q.grad.detach().cpu() for q in params], [(q.detach() - b).cpu() for q, b in
                                                                       zip(params, before)]
