@@ -509,8 +509,14 @@ struct Layout {
   int64_t total;
 };
 
-// rows of the N = 4096 GEMMs that fill whole rounds of 256x256 tiles over the
-// CUs (the rest run as kSplit K-slices + fixup); Hp when no split pays
+// rows of the K = 4096, N = 4096 GEMMs that fill whole rounds of 256x256 tiles
+// over the CUs (the rest run as kSplit K-slices + fixup); Hp when no split pays.
+// The K = 1024 ones run all Hp rows on the persistent kernel, whose half-tile
+// tail (the last partial round cut into 128-row units) costs half a 16-step
+// tile there, less than the split tail's two launches (tools/halves_probe.py:
+// 71.9 vs 59.0 + 19.0 us at Hp = 8,320); at K = 4096 half a tile is 64 steps
+// and the K-slices win (27 vs 46 us).
+static constexpr bool split_tail(int64_t K) { return K > 1024; }
 static int64_t main_rows(int dtype, int64_t Hp, int ncu) {
   const int64_t ntn = H / 256;
   if (dtype != NR_BF16 || Hp % 256 == 0 || ncu % ntn) return Hp;
@@ -527,7 +533,8 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs, int ncu) {
   L.mm = main_rows(dtype, L.Hp, ncu);
   // CS partial rows (bf16 column-sum epilogues): 128-row blocks of the persistent
   // GEMM over rows [0, mm), then 32-row blocks of a split-K tail (fixup_drelu_cs_kernel);
-  // csr3 for the dX GEMM (N = 1024, no tail split)
+  // csr3 (128-row blocks over all Hp rows, never more than csr) for the GEMMs
+  // with no tail split (dX, N = 1024; dY and dZ2, K = 1024)
   L.csr3 = (L.Hp + 127) / 128;
   L.csr = L.mm < L.Hp ? L.mm / 128 + (L.Hp - L.mm + 31) / 32 : L.csr3;
   const int64_t Hp = L.Hp, es = L.es, Bp = pad64(B);
@@ -582,7 +589,7 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   const int dt = a.dtype;
   const int ncu = ncu_of(st);
   const Layout L = layout(dt, a.B, a.U, a.Hs, ncu);
-  const int64_t B = a.B, Hs = a.Hs, Hp = L.Hp, mm = L.mm;
+  const int64_t B = a.B, Hs = a.Hs, Hp = L.Hp;
   auto P_ = [&](int64_t off) { return (void*)(ws + off); };
   float* xpair = (float*)P_(L.xpair);
   TA* XH = (TA*)P_(L.XH);
@@ -645,6 +652,7 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
   auto relu_gemm = [&](const TA* A, int64_t lda, const TA* W, int64_t K, const float* bias, uint64_t seed, TA* C,
                        int64_t ldc) -> int {
     EpiArgs ea{seed, thr, scale};
+    const int64_t mm = split_tail(K) ? L.mm : Hp;
     NR_FT(gemm_dispatch_ex(dt, dt, NR_EPI_RELU_DROPOUT, mm, H, K, A, lda, W, K, bias, nullptr, 0, C, ldc, ea, st));
     if (mm == Hp) return NR_OK;
     float* Pk = (float*)P_(L.skP);
@@ -694,6 +702,7 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
     } else {
       EpiArgs ea{0, 0, scale};
       ea.colsum = cs;
+      const int64_t mm = split_tail(K) ? L.mm : Hp;
       NR_FT(gemm_dispatch_ex(dt, dt, NR_EPI_DRELU, mm, H, K, A, K, Wt, K, nullptr, Yf, H, C, H, ea, st));
       if (mm == Hp) return NR_OK;
       float* Pk = (float*)P_(L.skP);
@@ -737,7 +746,9 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
     float* outs[4] = {a.g_b1, a.g_b2, a.g_b3, a.g_b4};
     const int64_t cols[4] = {H, H, D, H};
     r.n = 4;
-    const int64_t crows[4] = {L.csr, L.csr, L.csr3, L.csr};
+    // (cs1: dZ1, K = H, tail split; cs2 / cs4: dZ2 / dY, K = D, and cs3: dX, none)
+    static_assert(!split_tail(D) && split_tail(H), "column-sum row counts assume the K = D GEMMs run unsplit");
+    const int64_t crows[4] = {L.csr, L.csr3, L.csr3, L.csr3};
     for (int i = 0; i < 4; ++i) { r.part[i] = parts[i]; r.out[i] = outs[i]; r.rows[i] = crows[i]; r.cols[i] = cols[i]; }
     // (launched with the W1 fold below: bias_fold_kernel)
   } else {
