@@ -43,11 +43,10 @@ namespace nr {
 namespace ft {
 
 constexpr int64_t D = 1024, H = 4096;
-constexpr int kSplit = 8;  // K-slices of a split-K tail (at most; see tail_split)
-// K = 1024 tails as 4 slices (20.4 vs 22.6 us per tail alone), K = 4096 as 8 (26.7 vs
-// 33.1): tools/tail_probe.py, profiles/round5/train/tail_probe_r5m.jsonl (inside the
-// step the K = 1024 choice measured within noise: profiles/round5/train/ab_r7u)
-static int tail_split(int64_t K) { return K <= 1024 ? 4 : kSplit; }
+// K-slices of a split-K tail: K = 4096 as 8 (26.7 vs 33.1 us as 4; tools/tail_probe.py,
+// profiles/round5/train/tail_probe_r5m.jsonl).  Only the K = 4096 GEMMs split their
+// tail rows (split_tail below); the K = 1024 ones take the persistent kernel's half tile.
+constexpr int kSplit = 8;
 // sum-of-squares partials of the bf16 step: 512 weight-grad tiles, then the W1 fold's
 // 16 x 64 blocks, the bias reduction's 208 blocks, the token LN reduction's 16
 constexpr int kSqTn = 512, kSqFold = (1024 / 64) * (4096 / 64), kSqBias = (3 * 4096 + 1024) / 64, kSqLn = 1024 / 64;
@@ -509,13 +508,14 @@ struct Layout {
   int64_t total;
 };
 
-// rows of the K = 4096, N = 4096 GEMMs that fill whole rounds of 256x256 tiles
+// Rows of the K = 4096, N = 4096 GEMMs that fill whole rounds of 256x256 tiles
 // over the CUs (the rest run as kSplit K-slices + fixup); Hp when no split pays.
 // The K = 1024 ones run all Hp rows on the persistent kernel, whose half-tile
 // tail (the last partial round cut into 128-row units) costs half a 16-step
 // tile there, less than the split tail's two launches (tools/halves_probe.py:
-// 71.9 vs 59.0 + 19.0 us at Hp = 8,320); at K = 4096 half a tile is 64 steps
-// and the K-slices win (27 vs 46 us).
+// 71.9 vs 59.0 + 19.0 us at Hp = 8,320; in the step 1.735-1.739 -> 1.710-1.719
+// ms, profiles/round6/final_unsplit); at K = 4096 half a tile is 64 steps and
+// the K-slices win (27 vs 46 us).
 static constexpr bool split_tail(int64_t K) { return K > 1024; }
 static int64_t main_rows(int dtype, int64_t Hp, int ncu) {
   const int64_t ntn = H / 256;
@@ -656,7 +656,7 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
     NR_FT(gemm_dispatch_ex(dt, dt, NR_EPI_RELU_DROPOUT, mm, H, K, A, lda, W, K, bias, nullptr, 0, C, ldc, ea, st));
     if (mm == Hp) return NR_OK;
     float* Pk = (float*)P_(L.skP);
-    const int ns = tail_split(K);
+    const int ns = kSplit;
     const int64_t kk = K / ns, rows = Hp - mm;
     GemmProblem p = {rows, H, kk, A + mm * lda, lda, kk, W, K, kk, Pk, H, rows * H, ns, 1.0f};
     NR_FT(gemm_group_dispatch(dt, NR_F32, &p, 1, st));
@@ -706,7 +706,7 @@ int step(const nr_final_train_args& a, char* ws, hipStream_t st) {
       NR_FT(gemm_dispatch_ex(dt, dt, NR_EPI_DRELU, mm, H, K, A, K, Wt, K, nullptr, Yf, H, C, H, ea, st));
       if (mm == Hp) return NR_OK;
       float* Pk = (float*)P_(L.skP);
-      const int ns = tail_split(K);
+      const int ns = kSplit;
       const int64_t kk = K / ns, rows = Hp - mm;
       GemmProblem p = {rows, H, kk, A + mm * K, K, kk, Wt, K, kk, Pk, H, rows * H, ns, 1.0f};
       NR_FT(gemm_group_dispatch(dt, NR_F32, &p, 1, st));

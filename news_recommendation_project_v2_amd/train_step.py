@@ -187,8 +187,10 @@ class FinalAttentionTrainStep:
     def _tail_rows(self, M: int, N: int, K: int) -> int:
         """Rows of a bf16 GEMM that fill whole rounds of 256x256 tiles over the CUs
         (the rest, a few tiles that would hold one CU each for a full tile time,
-        run as K-slices instead); M when no such split pays."""
-        if self.dtype != torch.bfloat16 or N % 256 or K % 512 or M % 256 == 0:
+        run as K-slices instead); M when no such split pays -- and at K <= 1024,
+        where the persistent kernel's half-tile tail is the cheaper form
+        (final_train.hip split_tail)."""
+        if self.dtype != torch.bfloat16 or N % 256 or K % 512 or K <= 1024 or M % 256 == 0:
             return M
         ncu = self._ncu
         ntn = N // 256
