@@ -118,11 +118,12 @@ def main():
         rows = torch.tensor(sorted(set(np.random.default_rng(1).integers(0, args.m, 64).tolist()) | {args.m - 1}),
                             device=dev)
         ref = reference_rows(a, w, b, epi, r, rows)
-        err = {}
+        err, first = {}, {}
         for lab, lib in libs.items():
             run(lib, a, w, b, epi, r, outs[lab], tails[lab])
             torch.cuda.synchronize()
             err[lab] = float((outs[lab][rows].double() - ref).abs().max())
+            first[lab] = outs[lab].clone()
         fns = {lab: (lambda lib=lib, o=outs[lab], tl=tails[lab]: run(lib, a, w, b, epi, r, o, tl))
                for lab, lib in libs.items()}
         fns["torch"] = lambda: torch.matmul(a, w.T)
@@ -157,11 +158,16 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 times[lab].append(e0.elapsed_time(e1) / args.reps)
+        # builds that differ only in scheduling must agree bit for bit, and every
+        # timed call (each overwrote outs) with its own first call
+        lab0 = next(iter(libs))
+        bits = {f"{lab}_bit_equal_{lab0}": bool(torch.equal(first[lab], first[lab0])) for lab in libs}
+        bits.update({f"{lab}_repeatable": bool(torch.equal(outs[lab], first[lab])) for lab in libs})
         flop = 2.0 * args.m * n * k
         res = {"shape": name, "M": args.m, "N": n, "K": k,
                **{f"{lab}_ms": round(float(np.median(v)), 4) for lab, v in times.items()},
                **{f"{lab}_tflops": round(flop / (float(np.median(v)) * 1e-3) / 1e12, 1) for lab, v in times.items()},
-               **{f"{lab}_maxerr": e for lab, e in err.items()}}
+               **{f"{lab}_maxerr": e for lab, e in err.items()}, **bits}
         print(json.dumps(res), flush=True)
         summary.append(res)
     print(json.dumps({"summary": summary}))
