@@ -22,7 +22,9 @@
 // slot).  Backward:
 //   dm (normalize backward) -> dZ_b = (dm_b / h_b) W2 (per row, broadcast to its
 //   slots) -> dG = GEGLU' -> dY = dG W1 -> dH1 = LN_f'(dY) + dm_b / h_b ->
-//   dP = dH1 Bt -> dS = softmax64'(P, dP) -> dX = dS A -> dE[hist] += LN_q'(dX) + dH1
+//   dP = dH1 Bt -> dS = softmax64'(P, dP) -> dX = dS A -> dE_slot = LN_q'(dX) + dH1,
+//   and the token LN's parameter grads straight from the slots' dE_slot and the pos /
+//   neg rows' cosine grads (linear in dE: no [U][1024] dE table is formed)
 //   weight grads: W1 = dG^T Y, W2 = dm^T mean(Z), A = dS^T X, Bt = dH1^T P (one
 //   grouped launch), then the fold backward (Wq, Wkv, Wo, latents, norm_context)
 //   as two grouped launches of the 8 heads, and the LN parameter grads.
@@ -251,8 +253,7 @@ static int sum_parts(const float* src, int parts, int64_t pstride, float* dst, i
 // step never stores the [U][1024] E table: the slot gather, the head (pos / neg
 // rows) and the LN_q backward recompute the rows they read from the token states.
 template <typename TT>
-__device__ __forceinline__ void tok_ln(const TT* __restrict__ row, int lane, const float* __restrict__ tg,
-                                       const float* __restrict__ tb, float (&v)[4][4]) {
+__device__ __forceinline__ void tok_xhat(const TT* __restrict__ row, int lane, float (&v)[4][4]) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const TT* p = row + j * 256 + lane * 4;
@@ -280,26 +281,44 @@ __device__ __forceinline__ void tok_ln(const TT* __restrict__ row, int lane, con
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
+    for (int t = 0; t < 4; ++t) v[j][t] = (v[j][t] - mean) * rstd;
+}
+// the E row: xhat tg + tb (the module's affine after tok_xhat's normalisation)
+template <typename TT>
+__device__ __forceinline__ void tok_ln(const TT* __restrict__ row, int lane, const float* __restrict__ tg,
+                                       const float* __restrict__ tb, float (&v)[4][4]) {
+  tok_xhat<TT>(row, lane, v);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int e = j * 256 + lane * 4 + t;
-      v[j][t] = (v[j][t] - mean) * rstd * tg[e] + tb[e];
+      v[j][t] = v[j][t] * tg[e] + tb[e];
     }
 }
 
-// Epn rows k < B: E[pos[k]], rows B + k: E[neg[k]] (f32, for the head).  Wave per row.
+// Epn rows k < B: E[pos[k]], rows B + k: E[neg[k]] (f32, for the head), and Xpn the
+// same rows' token-LN xhat (the head's part of the token LN weight grad).  Wave per row.
 template <typename TT>
 __global__ __launch_bounds__(256) void pn_rows_kernel(int64_t B, const TT* __restrict__ tok,
                                                       const int32_t* __restrict__ pos, const int32_t* __restrict__ neg,
                                                       const float* __restrict__ tg, const float* __restrict__ tb,
-                                                      float* __restrict__ Epn) {
+                                                      float* __restrict__ Epn, float* __restrict__ Xpn) {
   const int lane = threadIdx.x & 63;
   const int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (k >= 2 * B) return;  // wave-uniform
   const int64_t r = k < B ? pos[k] : neg[k - B];
   float v[4][4];
-  tok_ln<TT>(tok + r * D, lane, tg, tb, v);
+  tok_xhat<TT>(tok + r * D, lane, v);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) st4<float>(Epn + k * D + j * 256 + lane * 4, v[j]);
+  for (int j = 0; j < 4; ++j) {
+    const int c = j * 256 + lane * 4;
+    st4<float>(Xpn + k * D + c, v[j]);
+    float e[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) e[t] = v[j][t] * tg[c + t] + tb[c + t];
+    st4<float>(Epn + k * D + c, e);
+  }
 }
 
 // Sx = E[idx[row]], X = LN_q(Sx) (eps 1e-5); idx < 0 or row >= nvalid
@@ -453,17 +472,18 @@ __global__ __launch_bounds__(512) void segmean_kernel(int64_t B, int64_t Bp, con
 // residual of LN_f's backward, where the bf16 dmc -- one rounding shared by all
 // h_b slots of the row -- gave the token LN bias grad, whose dominant term is
 // sum_b dm_b, a correlated 2^-9 error the bf16 numerics model does not have),
-// gb2 += dm, dE[pos / neg]
-// += their cosine grads (lane-contiguous atomics: 256 B per wave instruction).
+// gb2 += dm, and the pos / neg rows' cosine grads g straight into the token LN's
+// parameter grads: gtg += g xhat (Xpn), gtb += g (lane-contiguous atomics: 256 B per
+// wave instruction).
 template <typename TA>
 __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int nparts, const float* __restrict__ parts,
                                                    const float* __restrict__ b2, const float* __restrict__ h1bar,
                                                    const int64_t* __restrict__ off, const float* __restrict__ Epn,
-                                                   int64_t lde, const int32_t* __restrict__ pos,
-                                                   const int32_t* __restrict__ neg, float margin,
+                                                   float margin,
                                                    float* __restrict__ loss, float* __restrict__ users,
                                                    TA* __restrict__ dmA, TA* __restrict__ dmc,
-                                                   float* __restrict__ dmc32, float* __restrict__ dE,
+                                                   float* __restrict__ dmc32, const float* __restrict__ Xpn,
+                                                   float* __restrict__ gtg, float* __restrict__ gtb,
                                                    float* __restrict__ gb2) {
   constexpr float EPS = 1e-8f, NEPS = 1e-12f;
   __shared__ float red[4];
@@ -515,8 +535,8 @@ __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int np
   const float gsp = -act / (float)B, gsn = act / (float)B;
   if (tid == 0) atomicAdd(loss, fmaxf(v, 0.f) / (float)B);
   const float cu = nu > EPS ? 1.f : 0.f, cp = np_ > EPS ? 1.f : 0.f, cq = nq > EPS ? 1.f : 0.f;
-  float* dp = dE + (int64_t)pos[b] * lde;
-  float* dn = dE + (int64_t)neg[b] * lde;
+  const float* xp = Xpn + b * D;         // xhat of E[pos[b]]'s token LN
+  const float* xn = Xpn + (B + b) * D;   // and of E[neg[b]]'s
   float g[4];
   float ug = 0.f;
 #pragma unroll
@@ -525,8 +545,9 @@ __global__ __launch_bounds__(256) void head_kernel(int64_t B, int64_t Bp, int np
     const float uh = u[j] * iu, ph = ep[j] * ip, qh = en[j] * iq;
     g[j] = gsp * (ph - cu * sp * uh) * iu + gsn * (qh - cu * sn * uh) * iu;
     ug = fmaf(u[j], g[j], ug);
-    atomicAdd(dp + c, gsp * (uh - cp * sp * ph) * ip);
-    atomicAdd(dn + c, gsn * (uh - cq * sn * qh) * iq);
+    const float gp = gsp * (uh - cp * sp * ph) * ip, gn = gsn * (uh - cq * sn * qh) * iq;
+    atomicAdd(gtg + c, fmaf(gp, xp[c], gn * xn[c]));
+    atomicAdd(gtb + c, gp + gn);
   }
   ug = block_sum(ug, red);
   const float icnt = 1.0f / (float)(off[b + 1] - off[b]);
@@ -647,29 +668,34 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(int64_t n_rows, const TA
 // MODE 1 (LN_q of S):  x = the f32 row E[idx[row]] the forward normalised (tok_ln of
 //   the token row tokv[idx[row]], not the bf16-stored S: the statistics of the rounded row moved the token LN
 //   bias grad ~10x past the bf16 numerics model's drift, test_train_bf16_drift),
-//   res = dH1 row (TA); dx scattered into dE[idx[row]]
-//   (the gradient of the history gather): the row is staged in the wave's LDS
-//   and added with lane-contiguous f32 atomics (256 B per wave instruction, the
-//   full-rate shape of MI355X_MICROARCH.md "Global float atomics"); idx < 0 skipped.
+//   res = dH1 row (TA); dx = the slot's gradient of its E row, which only the token
+//   LN's parameters consume: tdg += dx xhat_tok, tdb += dx (per-lane registers, one
+//   atomic per column per block, as dgamma / dbeta), in place of a [U][1024] dE
+//   scatter (8.5 M f32 atomics at the benchmark batch) and a pass over it; idx < 0
+//   skipped.
 template <typename TA, int MODE, typename TT = float>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, const TA* __restrict__ x,
                                                      const void* __restrict__ tokv, const float* __restrict__ gamma,
                                                      float eps,
                                                      const TA* __restrict__ dy, const void* __restrict__ res_,
                                                      const int32_t* __restrict__ sel, TA* __restrict__ out,
-                                                     float* __restrict__ dE, int64_t lde, float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta, const float* __restrict__ tg,
-                                                     const float* __restrict__ tb) {
+                                                     float* __restrict__ tdg, float* __restrict__ tdb,
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                     const float* __restrict__ tg, const float* __restrict__ tb) {
   __shared__ float sg[4][D], sb[4][D];
-  __shared__ float stage[MODE == 1 ? 4 : 1][MODE == 1 ? D : 1];
+  constexpr int NT = MODE == 1 ? 4 : 1;  // token-LN grad accumulators (MODE 1)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float ag[4][4], ab[4][4], gm[4][4];
+  float ag[4][4], ab[4][4], gm[4][4], tga[NT][4], tba[NT][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     ld4<float>(gamma + j * 256 + lane * 4, gm[j]);
 #pragma unroll
     for (int t = 0; t < 4; ++t) { ag[j][t] = 0.f; ab[j][t] = 0.f; }
   }
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { tga[j][t] = 0.f; tba[j][t] = 0.f; }
   for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < n; row += (int64_t)gridDim.x * 4) {
     const int32_t s = row < nvalid ? sel[row] : -1;
     if (s < 0) {
@@ -681,7 +707,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, 
     }
     // x, dy and the residual row issued together (one memory round trip per row;
     // dy and res behind the statistics' reductions made the kernel latency-bound)
-    float v[4][4], g[4][4], dyv[4][4], rv[4][4];
+    float v[4][4], g[4][4], dyv[4][4], rv[4][4], xt[NT][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int c = j * 256 + lane * 4;
@@ -690,7 +716,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, 
       if constexpr (MODE == 0) ld4<float>(static_cast<const float*>(res_) + (int64_t)s * D + c, rv[j]);
       else ld4<TA>(static_cast<const TA*>(res_) + row * D + c, rv[j]);
     }
-    if constexpr (MODE == 1) tok_ln<TT>(static_cast<const TT*>(tokv) + (int64_t)s * D, lane, tg, tb, v);
+    if constexpr (MODE == 1) {
+      tok_xhat<TT>(static_cast<const TT*>(tokv) + (int64_t)s * D, lane, xt);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int e = j * 256 + lane * 4 + t;
+          v[j][t] = xt[j][t] * tg[e] + tb[e];
+        }
+    }
     float sum = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) sum += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
@@ -722,17 +757,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, 
       float o[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) o[t] = rstd * (g[j][t] - m1 - v[j][t] * m2) + rv[j][t];
-      if constexpr (MODE == 0) st4<TA>(out + row * D + c, o);
-      else *reinterpret_cast<float4*>(&stage[wave][c]) = float4{o[0], o[1], o[2], o[3]};
-    }
-    if constexpr (MODE == 1) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      float* d = dE + (int64_t)s * lde;
+      if constexpr (MODE == 0) {
+        st4<TA>(out + row * D + c, o);
+      } else {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) atomicAdd(d + k * 64 + lane, stage[wave][k * 64 + lane]);
-      __builtin_amdgcn_wave_barrier();  // the stage is rewritten by the wave's next row
+        for (int t = 0; t < 4; ++t) {
+          tga[j][t] = fmaf(o[t], xt[j][t], tga[j][t]);
+          tba[j][t] += o[t];
+        }
+      }
     }
   }
 #pragma unroll
@@ -746,6 +779,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t n, int64_t nvalid, 
   for (int c = threadIdx.x; c < D; c += 256) {
     atomicAdd(dgamma + c, (sg[0][c] + sg[1][c]) + (sg[2][c] + sg[3][c]));
     atomicAdd(dbeta + c, (sb[0][c] + sb[1][c]) + (sb[2][c] + sb[3][c]));
+  }
+  if constexpr (MODE == 1) {  // the token LN's grads, the same way
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        sg[wave][j * 256 + lane * 4 + t] = tga[j][t];
+        sb[wave][j * 256 + lane * 4 + t] = tba[j][t];
+      }
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 256) {
+      atomicAdd(tdg + c, (sg[0][c] + sg[1][c]) + (sg[2][c] + sg[3][c]));
+      atomicAdd(tdb + c, (sb[0][c] + sb[1][c]) + (sb[2][c] + sb[3][c]));
+    }
   }
 }
 
@@ -1055,8 +1103,8 @@ constexpr int kSqW12 = 0, kSqFold = 320, kSqKv = 512, kSqSlots = 832;
 // Workspace layout (byte offsets), shared by the size query and the step.
 struct Layout {
   int64_t Hp, Hpp, kw, Bp, es;
-  int64_t E, Sx, X, P, H1, Y, G, zbar, h1bar, row_seg, hparts, hsum, dmA, dmc, dmc32, dZ, dZs, gpart, dG, dY, dH1, dP,
-      dS, dX, dE;
+  int64_t E, Xpn, Sx, X, P, H1, Y, G, zbar, h1bar, row_seg, hparts, hsum, dmA, dmc, dmc32, dZ, dZs, gpart, dG, dY, dH1,
+      dP, dS, dX;
   int64_t dGT, YT, dH1T, PT, dST, XT, dmT, zbarT;
   int64_t WqT, W1T, W2T, WoT, WkvT, latn, latnT, KVp, KV, KVT, A, AT, BtT, Bt;
   int64_t gA, gBt, gA16, gAT16, gBt16, gBtT16, dKV, dKV16, dKVT16, dlat, sqp;
@@ -1075,6 +1123,7 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs) {
   int64_t o = 0;
   auto take = [&](int64_t bytes) { const int64_t r = o; o += al(bytes); return r; };
   L.E = take(2 * Bp * D * 4);  // Epn: E[pos] rows then E[neg] rows (no [U][D] E table)
+  L.Xpn = take(2 * Bp * D * 4);  // the same rows' token-LN xhat
   // X, P, dH1, dS hold Hpp rows: the dA / dBt K-slices read them directly (bf16: TN
   // weight-grad GEMMs), rows [Hp, Hpp) zeroed by the step
   L.Sx = take(Hp * D * es); L.X = take(Hpp * D * es); L.P = take(Hpp * S * es); L.H1 = take(Hp * D * es);
@@ -1085,7 +1134,7 @@ static Layout layout(int dtype, int64_t B, int64_t U, int64_t Hs) {
   L.dZs = take(Bp * F * 4);
   L.gpart = take((Hp + kGRows - 1) / kGRows * 2 * F * 4);
   L.dG = take(Hp * 2 * F * es); L.dY = take(Hp * D * es); L.dH1 = take(Hpp * D * es);
-  L.dP = take(Hp * S * es); L.dS = take(Hpp * S * es); L.dX = take(Hp * D * es); L.dE = take(U * D * 4);
+  L.dP = take(Hp * S * es); L.dS = take(Hpp * S * es); L.dX = take(Hp * D * es);
   L.dGT = take(2 * F * Hp * es); L.YT = take(D * Hp * es); L.dH1T = take(D * Hpp * es); L.PT = take(S * Hpp * es);
   L.dST = take(S * Hpp * es); L.XT = take(D * Hpp * es); L.dmT = take(D * Bp * es); L.zbarT = take(F * Bp * es);
   L.WqT = take(D * F * es); L.W1T = take(D * 2 * F * es); L.W2T = take(F * D * es); L.WoT = take(F * D * es);
@@ -1111,9 +1160,10 @@ template <typename TA>
 int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   const int dt = a.dtype;
   const Layout L = layout(dt, a.B, a.U, a.Hs);
-  const int64_t B = a.B, U = a.U, Hp = L.Hp, Hpp = L.Hpp, Bp = L.Bp;
+  const int64_t B = a.B, Hp = L.Hp, Hpp = L.Hpp, Bp = L.Bp;
   auto P_ = [&](int64_t off) { return (void*)(ws + off); };
   float* Epn = (float*)P_(L.E);
+  float* Xpn = (float*)P_(L.Xpn);
   TA *Sx = (TA*)P_(L.Sx), *X = (TA*)P_(L.X), *Pm = (TA*)P_(L.P), *H1 = (TA*)P_(L.H1), *Y = (TA*)P_(L.Y);
   TA *G = (TA*)P_(L.G), *zbar = (TA*)P_(L.zbar);
   float* h1bar = (float*)P_(L.h1bar);
@@ -1127,7 +1177,6 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   float* gpart = (float*)P_(L.gpart);
   TA *dG = (TA*)P_(L.dG), *dY = (TA*)P_(L.dY), *dH1 = (TA*)P_(L.dH1), *dP = (TA*)P_(L.dP), *dS = (TA*)P_(L.dS);
   TA* dX = (TA*)P_(L.dX);
-  float* dE = (float*)P_(L.dE);
   TA *dGT = (TA*)P_(L.dGT), *YT = (TA*)P_(L.YT), *dH1T = (TA*)P_(L.dH1T), *PT = (TA*)P_(L.PT), *dST = (TA*)P_(L.dST);
   TA *XT = (TA*)P_(L.XT), *dmT = (TA*)P_(L.dmT), *zbarT = (TA*)P_(L.zbarT);
   TA *WqT = (TA*)P_(L.WqT), *W1T = (TA*)P_(L.W1T), *W2T = (TA*)P_(L.W2T), *WoT = (TA*)P_(L.WoT),
@@ -1183,21 +1232,20 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     if ((rc = launch_tlist<TA, TA>(t, st))) return rc;
   }
   // ---- accumulators: the step zeroes every gradient it accumulates (the GEMM-written
-  // ones are overwritten whole), the loss and the history-gather gradient dE
+  // ones are overwritten whole) and the loss
   {
     ZList z{};
     float* zp[] = {a.g_tok_g, a.g_tok_b, a.g_nq_g, a.g_nq_b, a.g_nc_g, a.g_nc_b, a.g_nf_g, a.g_nf_b, a.g_b2, a.g_b1, a.loss};
     const int64_t zn[] = {D, D, D, D, D, D, D, D, D, 2 * F, 1};
     for (int i = 0; i < 11; ++i) { z.p[i] = zp[i]; z.len[i] = zn[i]; }
-    z.p[11] = dE; z.len[11] = U * D;
     // rows [Hp, Hpp) of the dA / dBt operands (read as the K-slices' zero tail)
     const int64_t tail = (Hpp - Hp) * L.es / 4;  // in f32 words (Hpp - Hp is a multiple of 64 rows)
-    z.p[12] = (float*)(X + Hp * D); z.len[12] = tail * D;
-    z.p[13] = (float*)(Pm + Hp * S); z.len[13] = tail * S;
-    z.p[14] = (float*)(dH1 + Hp * D); z.len[14] = tail * D;
-    z.p[15] = (float*)(dS + Hp * S); z.len[15] = tail * S;
-    z.n = 16;
-    if (a.sumsq) { z.p[16] = a.sumsq; z.len[16] = 1; z.n = 17; }
+    z.p[11] = (float*)(X + Hp * D); z.len[11] = tail * D;
+    z.p[12] = (float*)(Pm + Hp * S); z.len[12] = tail * S;
+    z.p[13] = (float*)(dH1 + Hp * D); z.len[13] = tail * D;
+    z.p[14] = (float*)(dS + Hp * S); z.len[14] = tail * S;
+    z.n = 15;
+    if (a.sumsq) { z.p[15] = a.sumsq; z.len[15] = 1; z.n = 16; }
     hipLaunchKernelGGL(zero_kernel, dim3(1024), dim3(256), 0, st, z);
     NR_LT_CHECK("zero");
   }
@@ -1243,9 +1291,9 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     else if (a.tok_dtype == NR_BF16) { typedef __bf16 TT; __VA_ARGS__; }     \
     else { typedef _Float16 TT; __VA_ARGS__; }                              \
   } while (0)
-  // ---- E[pos] / E[neg] rows for the head (the token LN of those news' last tokens)
+  // ---- E[pos] / E[neg] rows for the head (the token LN of those news' last tokens) and their xhat
   NR_LT_TOK(hipLaunchKernelGGL((pn_rows_kernel<TT>), dim3((unsigned)((2 * B + 3) / 4)), dim3(256), 0, st, B,
-                               (const TT*)a.tok_last, a.pos, a.neg, a.tok_g, a.tok_b, Epn));
+                               (const TT*)a.tok_last, a.pos, a.neg, a.tok_g, a.tok_b, Epn, Xpn));
   NR_LT_CHECK("pos / neg rows");
   // ---- per-slot forward
   NR_LT_TOK(hipLaunchKernelGGL((gather_ln_kernel<TA, TT>), dim3(grid_rows(Hp)), dim3(256), 0, st, Hp, a.Hs,
@@ -1271,7 +1319,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     if ((rc = sum_parts(hparts, kHParts, Bp * D, hsum, Bp * D, st))) return rc;
   }
   hipLaunchKernelGGL((head_kernel<TA>), dim3((unsigned)Bp), dim3(256), 0, st, B, Bp, 1, hsum, a.b2, h1bar,
-                     a.hist_off, Epn, (int64_t)D, a.pos, a.neg, a.margin, a.loss, a.users, dmA, dmc, dmc32, dE, a.g_b2);
+                     a.hist_off, Epn, a.margin, a.loss, a.users, dmA, dmc, dmc32, Xpn, a.g_tok_g, a.g_tok_b, a.g_b2);
   NR_LT_CHECK("head");
   // ---- backward
   // dZ_b = (dm_b / h_b) W2 (f32, split-K partials [kZParts, Bp, 4096]): C = dmc . W2T^T
@@ -1327,7 +1375,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, 2 * F, dG, 2 * F, W1T, 2 * F, nullptr, nullptr, 0, dY, D, st)))
     return rc;
   hipLaunchKernelGGL((ln_bwd_kernel<TA, 0>), dim3(grid_rows(Hp, 512)), dim3(256), 0, st, Hp, Hp, H1, nullptr, a.nf_g, 1e-5f, dY,
-                     dmc32, row_seg, dH1, nullptr, (int64_t)0, a.g_nf_g, a.g_nf_b, nullptr, nullptr);
+                     dmc32, row_seg, dH1, nullptr, nullptr, a.g_nf_g, a.g_nf_b, nullptr, nullptr);
   NR_LT_CHECK("ln_f_bwd");
   if (dt == NR_BF16) {
     // dS = P (dP - sum_group P dP) in the dP GEMM's epilogue (NR_EPI_SOFTMAX64_BWD, R = P)
@@ -1342,7 +1390,7 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
     NR_LT_CHECK("softmax64_bwd");
   }
   // fork 2: dA / dBt and the whole fold backward need only dS, dH1, P, X from here on,
-  // so they run on a third stream beside dX, the scatter and the token LN grads.
+  // so they run on a third stream beside dX and the LN_q / token LN grads.
   // (Starting dBt's transposes and GEMM before the dS GEMM, on a third event, measured
   // no gain: they slowed dS by as much, profiles/round4/train/r4s9.)
   if (hipEventRecord(side.fork2, st) != hipSuccess || hipStreamWaitEvent(side.s2, side.fork2, 0) != hipSuccess) {
@@ -1351,12 +1399,9 @@ int step(const nr_latent_train_args& a, char* ws, hipStream_t st) {
   }
   if ((rc = gemm_dispatch(dt, dt, NR_EPI_NONE, Hp, D, S, dS, S, AT, S, nullptr, nullptr, 0, dX, D, st))) return rc;
   NR_LT_TOK(hipLaunchKernelGGL((ln_bwd_kernel<TA, 1, TT>), dim3(grid_rows(Hp, 512)), dim3(256), 0, st, Hp, a.Hs, Sx,
-                               a.tok_last, a.nq_g, 1e-5f, dX, dH1, a.hist_idx, nullptr, dE, (int64_t)D, a.g_nq_g,
-                               a.g_nq_b, a.tok_g, a.tok_b));
-  NR_LT_CHECK("ln_q_bwd");
-  // token LayerNorm parameter grads from dE (history scatter + cosine grads)
-  if ((rc = nr_ln_param_grad(a.tok_dtype, U, D, a.tok_last, D, nullptr, 1e-12f, dE, D, a.g_tok_g, a.g_tok_b, st)))
-    return rc;
+                               a.tok_last, a.nq_g, 1e-5f, dX, dH1, a.hist_idx, nullptr, a.g_tok_g, a.g_tok_b,
+                               a.g_nq_g, a.g_nq_b, a.tok_g, a.tok_b));
+  NR_LT_CHECK("ln_q_bwd");  // (with the head's pos / neg part: the token LN's grads are final)
   {
     // this stream's gradients are all final here
     SqList q;
